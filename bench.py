@@ -1,0 +1,205 @@
+"""Benchmark: stylized images/s of the MI355X forward path (BASELINE.json metric).
+
+Default workload = BASELINE.json configs[1]: AdaINRPNet.test() (rp_blocks=5,
+hidden_dim=16), batch 32 per GPU, 512x512 fp32, synthetic U[0,1) images and
+He-uniform synthetic weights (no checkpoints exist offline). One "step" = one test()
+call over the whole per-GPU batch, inputs already resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model adain|wct|sanet]
+
+N>1 runs one process per GPU under torch.distributed.run; each rank stylises its own
+batch (weak scaling: the batch is split per image, no collective touches the data; a
+barrier and a MAX over per-rank times are the only communication).
+
+The JSON line also carries:
+  roofline     the dominant kernel's algorithmic FLOP (or bytes) per launch divided by
+               its mean launch time, measured with HIP events on the launch stream
+               during the timed steps, against the MI355X peak;
+  roofline_adain  the same for the AdaIN statistics+apply path (HBM-bound);
+  cpu_baseline the CPU oracle (PyTorch-CPU restatement of the reference) timed on this
+               host on a bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rp-style-transfer_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (matrix = vector rate), MI355X_MICROARCH.md
+PEAK_FP64_TFLOPS = 78.6    # MI355X dense FP64 matrix (vendor spec)
+PEAK_HBM_GBS = 8000.0      # HBM3E 8 TB/s
+
+
+def build_model(kind, dev):
+    import network as net
+    from rpst import synth
+    cfg = {"rp_blocks": 5, "hidden_dim": 16, "content_weight": 1.0, "style_weight": 10.0,
+           "resume": False}
+    if kind == "adain":
+        m = net.AdaINRPNet(cfg, copy.deepcopy(net.vgg))
+    elif kind == "wct":
+        m = net.WCTRPNet(cfg, copy.deepcopy(net.vgg))
+    else:
+        m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, 512)
+    synth.synth_module_(m, 0)
+    return m.to(dev)
+
+
+WORKLOADS = {
+    "adain": "AdaINRPNet.test() rp_blocks=5 hidden_dim=16, 512x512 (BASELINE configs[1])",
+    "wct": "WCTRPNet.test() rp_blocks=5 hidden_dim=16, 512x512, fp64 WCT (BASELINE configs[2])",
+    "sanet": "SAModel.test() VGG relu1_1-5_1 + SANet 4_1/5_1 + decoder, 512x512 (BASELINE configs[3])",
+}
+DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32}
+
+
+def cpu_baseline(kind, size, budget_s=12.0):
+    """Time the CPU oracle on a bounded sample: one content/style pair at size^2."""
+    from oracle import restate as R
+    from rpst import synth
+    import network as net
+    cfg = {"rp_blocks": 5, "hidden_dim": 16}
+    if kind == "adain":
+        m = net.AdaINRPNet(cfg, copy.deepcopy(net.vgg))
+        fn = lambda c, s, sd: R.adain_rp_test(c, s, sd, 5)  # noqa: E731
+    elif kind == "wct":
+        m = net.WCTRPNet(cfg, copy.deepcopy(net.vgg))
+        fn = lambda c, s, sd: R.wct_rp_test(c, s, sd, 5)  # noqa: E731
+    else:
+        m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, size)
+        fn = R.samodel_test
+    synth.synth_module_(m, 0)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    c = torch.from_numpy(synth.image(11, (1, 3, size, size)))
+    s = torch.from_numpy(synth.image(12, (1, 3, size, size)))
+    threads = torch.get_num_threads()
+    fn(c, s, sd)  # warm-up
+    reps, t0 = 0, time.perf_counter()
+    while reps < 8:
+        fn(c, s, sd)
+        reps += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": reps / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle {kind} test() on {reps} x 1 pair at {size}x{size}, "
+                      f"{threads} threads, {dt:.1f}s"}
+
+
+def roofline_from_trace(summary, flops_key=True):
+    best = None
+    for name, a in summary.items():
+        if not name.startswith("conv"):
+            continue
+        if best is None or a["ms"] > best[1]["ms"]:
+            best = (name, a)
+    if best is None:
+        return None
+    name, a = best
+    avg_ms = a["ms"] / a["launches"]
+    achieved = a["flops"] / (avg_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+            "kernel": f"conv_mfma_kernel [{name}]", "launch_ms": round(avg_ms, 4),
+            "flop_per_launch": a["flops"]}
+
+
+def adain_roofline(summary):
+    for name, a in summary.items():
+        if name.startswith("adain"):
+            avg_ms = a["ms"] / a["launches"]
+            gbs = a["bytes"] / (avg_ms * 1e-3) / 1e9
+            return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                    "kernel": f"plane_stats_kernel+plane_apply_kernel [{name}]",
+                    "launch_ms": round(avg_ms, 4), "bytes_per_launch": a["bytes"]}
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", choices=["adain", "wct", "sanet"], default="adain")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    from rpst import ops, synth
+
+    B = args.batch or DEFAULT_BATCH[args.model]
+    model = build_model(args.model, dev)
+    shape = (B, 3, args.size, args.size)
+    content = torch.from_numpy(synth.image(1000 + rank, shape)).to(dev)
+    style = torch.from_numpy(synth.image(2000 + rank, shape)).to(dev)
+
+    for _ in range(args.warmup):
+        model.test(content, style)
+    torch.cuda.synchronize()
+
+    ops.TRACE = ops.Trace()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = model.test(content, style)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    summary = ops.TRACE.summary()
+    ops.TRACE = None
+    assert out.shape == shape and torch.isfinite(out).all()
+
+    if world > 1:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    value = world * B * args.steps / dt
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32" if args.model != "wct"
+            else "fp32 conv / f64 WCT", "data": "synthetic U[0,1) images, synthetic He-uniform weights",
+            "config": {"workload": WORKLOADS[args.model], "per_gpu_batch": B,
+                       "global_batch": B * world, "image": f"{args.size}x{args.size}",
+                       "parallelism": f"per-image batch split over {world} GPU(s), no collectives"},
+            "roofline": roofline_from_trace(summary),
+            "roofline_adain": adain_roofline(summary),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(args.model, args.size)
+        else:
+            rec["cpu_baseline"] = None
+        kernels = sorted(summary.items(), key=lambda kv: -kv[1]["ms"])[:12]
+        rec["kernel_ms_per_step"] = {k: round(v["ms"] / args.steps, 3) for k, v in kernels}
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

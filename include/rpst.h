@@ -1,0 +1,106 @@
+/*
+ * rpst.h — C ABI of the MI355X (gfx950) style-transfer forward path.
+ *
+ * Drop-in boundary: the reference (LuletterSoul/RP-Style-Transfer) has no FFI; its
+ * boundary is the Python API of the `network` package (network/__init__.py:1-6).
+ * Each entry point below replaces the ATen work behind one reference function, cited
+ * as path:line relative to the reference root. The Python mirror in
+ * rp-style-transfer_amd/network/ binds these symbols with ctypes.
+ *
+ * Conventions
+ *  - All tensor pointers are DEVICE pointers to contiguous row-major (NCHW) data.
+ *  - The library never allocates: ops that need scratch take (workspace, bytes) and
+ *    expose a *_workspace_size() query; the caller allocates (e.g. torch caching
+ *    allocator).
+ *  - Every call is ordered on `stream` (a hipStream_t passed as void*; NULL = default
+ *    stream) and never synchronises the device.
+ *  - Return value: RPST_OK (0) or a negative RPST_E* code; rpst_last_error() returns a
+ *    thread-local message describing the last failure.
+ *  - fp32 in / fp32 out unless the name says f64. Results are deterministic (no float
+ *    atomics; fixed-order reductions).
+ */
+#ifndef RPST_H_
+#define RPST_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* rpst_stream_t;
+
+#define RPST_OK 0
+#define RPST_EINVAL (-1)  /* bad argument / unsupported shape            */
+#define RPST_EHIP (-2)    /* HIP launch or runtime error                  */
+#define RPST_EWORKSPACE (-3) /* workspace smaller than *_workspace_size() */
+
+/* conv2d padding mode */
+#define RPST_PAD_ZERO 0    /* nn.Conv2d(padding=1)            base.py:366-395            */
+#define RPST_PAD_REFLECT 1 /* nn.ReflectionPad2d((1,1,1,1))   base.py:26-54, base.py:59-110 */
+/* conv2d input operator applied on the fly while loading the input tile */
+#define RPST_IN_NONE 0
+#define RPST_IN_MAXPOOL2 1 /* nn.MaxPool2d((2,2),(2,2),(0,0),ceil_mode=True) base.py:65,72,85,98 */
+#define RPST_IN_UPSAMPLE2 2 /* nn.Upsample(scale_factor=2, mode='nearest') base.py:29,42,49     */
+#define RPST_IN_ADD_UPSAMPLE2 3 /* x + Upsample2(y)   sanet.py:149 (Transform merge input)   */
+
+/* Library version (major*10000 + minor*100 + patch). */
+int rpst_version(void);
+/* Message of the last failing call on this host thread ("" if none). */
+const char* rpst_last_error(void);
+
+/* ---- a1: calc_mean_std(feat, eps)  network/base.py:399-407 ----------------------
+ * mean[n,c] = mean over HW; std[n,c] = sqrt(var_unbiased + eps) (eps on the variance).
+ * feat (N,C,HW) -> mean, std (N,C). HW == 1 yields NaN std like torch.var. */
+int rpst_calc_mean_std(const float* feat, float* mean, float* std_out, int N, int C,
+                       int64_t HW, float eps, rpst_stream_t stream);
+
+/* ---- a2: adaptive_instance_normalization(c, s)  network/base.py:410-418 ----------
+ * out = (c - mean_c) / std_c * std_s + mean_s, statistics per (n,c) as in a1.
+ * content/style/out (N,C,HW). Workspace: rpst_adain_workspace_size(N, C). */
+size_t rpst_adain_workspace_size(int N, int C);
+int rpst_adain(const float* content, const float* style, float* out, int N, int C,
+               int64_t HW, float eps, void* workspace, size_t workspace_bytes,
+               rpst_stream_t stream);
+
+/* ---- a10: mean_variance_norm(feat)  network/sanet.py:20-24 -----------------------
+ * out = (x - mean) / std with a1 statistics. Workspace: rpst_adain_workspace_size(N,C). */
+int rpst_mean_variance_norm(const float* feat, float* out, int N, int C, int64_t HW,
+                            float eps, void* workspace, size_t workspace_bytes,
+                            rpst_stream_t stream);
+
+/* ---- a3/a5/a6/a12: Conv2d (3x3 or 1x1, stride 1) + bias [+ReLU] [+residual] -------
+ * nn.Conv2d(k=3, padding=1) + ReLU         base.py:363-396 (RP encoder / decoder)
+ * ReflectionPad2d(1) + Conv2d(k=3) [+ReLU] base.py:25-111, sanet.py:146-147,162-192
+ * Conv2d(k=1)                              base.py:58, sanet.py:76-80
+ * Weights are first repacked once into the kernel's K-major layout:
+ *   rpst_conv2d_pack(weight (Cout,Cin,k,k), packed) with
+ *   packed bytes = rpst_conv2d_packed_size(Cout, Cin, ksize).
+ * in_op is applied to the input while it is loaded (pool / upsample / add), so
+ *   RPST_IN_MAXPOOL2:     input (N,Cin,Hs,Ws), conv runs at H=ceil(Hs/2), W=ceil(Ws/2)
+ *   RPST_IN_UPSAMPLE2:    input (N,Cin,Hs,Ws), conv runs at H=2Hs, W=2Ws
+ *   RPST_IN_ADD_UPSAMPLE2: input (N,Cin,H,W) + aux (N,Cin,H/2,W/2) upsampled
+ *   RPST_IN_NONE:         input (N,Cin,H,W)
+ * (Hs, Ws) are the dims of `input`. out (N,Cout,H,W):
+ *   out = [relu](conv(in_op(input)) + bias) [+ residual]   (residual (N,Cout,H,W) or NULL)
+ * ksize 1 ignores pad_mode. Reflect padding needs H,W >= 2. */
+size_t rpst_conv2d_packed_size(int Cout, int Cin, int ksize);
+int rpst_conv2d_pack(const float* weight, float* packed, int Cout, int Cin, int ksize,
+                     rpst_stream_t stream);
+int rpst_conv2d(const float* input, const float* aux, const float* packed_weight,
+                const float* bias, const float* residual, float* out, int N, int Cin,
+                int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
+                rpst_stream_t stream);
+
+/* ---- stand-alone pool / upsample (same semantics as the conv input operators) ----- */
+int rpst_maxpool2x2_ceil(const float* in, float* out, int N, int C, int H, int W,
+                         rpst_stream_t stream);
+int rpst_upsample_nearest2x(const float* in, float* out, int N, int C, int H, int W,
+                            rpst_stream_t stream);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* RPST_H_ */

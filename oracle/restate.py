@@ -1,0 +1,254 @@
+"""ORACLE — CPU restatement of the reference hot path. TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module, and only as the checker / the timed CPU baseline; the product path
+(rp-style-transfer_amd/) never calls it and raises instead of falling back.
+
+Each function restates one reference function as plain functional PyTorch-CPU ops in
+the reference's own order (same ATen kernels: conv2d, var, mean, mm, svd, bmm,
+softmax), operating on a state_dict with the reference's keys. It is pinned against
+golden vectors produced by the reference itself (tests/golden/gen_golden.py,
+tests/test_oracle_golden.py); there the agreement is bitwise or within fp32 rounding.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+Tensor = torch.Tensor
+SD = Dict[str, Tensor]
+
+
+# ---- a1/a2/a10: statistics ---------------------------------------------------------
+def calc_mean_std(feat: Tensor, eps: float = 1e-5) -> Tuple[Tensor, Tensor]:
+    """network/base.py:399-407 — eps is added to the unbiased variance."""
+    N, C = feat.shape[:2]
+    var = feat.reshape(N, C, -1).var(dim=2) + eps
+    std = var.sqrt().view(N, C, 1, 1)
+    mean = feat.reshape(N, C, -1).mean(dim=2).view(N, C, 1, 1)
+    return mean, std
+
+
+def adain(content: Tensor, style: Tensor) -> Tensor:
+    """network/base.py:410-418."""
+    assert content.size() == style.size()
+    sm, ss = calc_mean_std(style)
+    cm, cs = calc_mean_std(content)
+    return (content - cm) / cs * ss + sm
+
+
+def mean_variance_norm(feat: Tensor) -> Tensor:
+    """network/sanet.py:20-24."""
+    m, s = calc_mean_std(feat)
+    return (feat - m) / s
+
+
+# ---- a3/a5/a6: conv stacks --------------------------------------------------------
+def conv(x: Tensor, sd: SD, key: str, pad: str, relu: bool) -> Tensor:
+    """Conv2d(k, stride 1) with zero padding 1 ('zero'), ReflectionPad2d(1) ('reflect')
+    or none ('none'), then optional ReLU."""
+    w, b = sd[key + ".weight"], sd[key + ".bias"]
+    if pad == "reflect":
+        x = F.pad(x, (1, 1, 1, 1), mode="reflect")
+        y = F.conv2d(x, w, b)
+    elif pad == "zero":
+        y = F.conv2d(x, w, b, padding=1)
+    else:
+        y = F.conv2d(x, w, b)
+    return F.relu(y) if relu else y
+
+
+def rp_stack(x: Tensor, sd: SD, prefix: str, n_conv: int) -> Tensor:
+    """build_{increase,decrease}_depth_rp_blocks: [Conv3x3(pad 1) + ReLU] x n
+    (network/base.py:363-396); Sequential indices 0,2,4,... hold the convs."""
+    for i in range(n_conv):
+        x = conv(x, sd, f"{prefix}{2 * i}", "zero", True)
+    return x
+
+
+# VGG "vgg_normalised" (network/base.py:57-111): index -> op
+_VGG_CONVS = {0: "1x1", 2: 3, 5: 3, 9: 3, 12: 3, 16: 3, 19: 3, 22: 3, 25: 3, 29: 3, 32: 3,
+              35: 3, 38: 3, 42: 3, 45: 3, 48: 3, 51: 3}
+_VGG_POOLS = (7, 14, 27, 40)
+
+
+def vgg_slice(x: Tensor, sd: SD, prefix: str, lo: int, hi: int) -> Tensor:
+    """Run vgg children [lo, hi); keys '{prefix}{idx}.weight' use the absolute index
+    (prefix '' for the bare vgg) — see vgg_slice_keys for module-relative prefixes."""
+    return vgg_slice_rel(x, sd, lambda idx: f"{prefix}{idx}", lo, hi)
+
+
+def vgg_slice_rel(x: Tensor, sd: SD, keyf, lo: int, hi: int) -> Tensor:
+    for idx in range(lo, hi):
+        if idx in _VGG_POOLS:
+            x = F.max_pool2d(x, (2, 2), (2, 2), (0, 0), ceil_mode=True)
+        elif idx in _VGG_CONVS:
+            if _VGG_CONVS[idx] == "1x1":
+                x = conv(x, sd, keyf(idx), "none", False)
+            else:
+                x = conv(x, sd, keyf(idx), "reflect", True)
+    return x
+
+
+# decoder (network/base.py:25-55 == sanet.py:162-192): conv indices, upsample indices
+_DEC_CONVS = (1, 5, 8, 11, 14, 18, 21, 25, 28)
+_DEC_UPS = (3, 16, 23)
+
+
+def decoder(x: Tensor, sd: SD, prefix: str) -> Tensor:
+    for idx in range(29):
+        if idx in _DEC_UPS:
+            x = F.interpolate(x, scale_factor=2, mode="nearest")
+        elif idx in _DEC_CONVS:
+            x = conv(x, sd, f"{prefix}{idx}", "reflect", idx != 28)
+    return x
+
+
+# VGG slices used by the models (adain_rp.py:21-24, sanet.py:202-206)
+ENC_SLICES = [(0, 4), (4, 11), (11, 18), (18, 31), (31, 44)]
+
+
+def encode_with_intermediate(x: Tensor, sd: SD, levels: int = 4) -> List[Tensor]:
+    """adain_rp.py:68-73 / sanet.py:219-224 with model keys 'enc_{i}.{j}'."""
+    out = []
+    for i, (lo, hi) in enumerate(ENC_SLICES[:levels]):
+        x = vgg_slice_rel(x, sd, lambda idx, i=i, lo=lo: f"enc_{i + 1}.{idx - lo}", lo, hi)
+        out.append(x)
+    return out
+
+
+# ---- a4: AdaINRPNet ---------------------------------------------------------------
+def adain_rp_test(content: Tensor, style: Tensor, sd: SD, rp_blocks: int) -> Tensor:
+    """AdaINRPNet.test (adain_rp.py:94-101)."""
+    with torch.no_grad():
+        cf = rp_stack(content, sd, "rp_shared_encoder.", rp_blocks)
+        sf = rp_stack(style, sd, "rp_shared_encoder.", rp_blocks)
+        return rp_stack(adain(cf, sf), sd, "rp_decoder.", rp_blocks)
+
+
+def style_loss(a: Tensor, b: Tensor) -> Tensor:
+    am, as_ = calc_mean_std(a)
+    bm, bs = calc_mean_std(b)
+    return F.mse_loss(am, bm) + F.mse_loss(as_, bs)
+
+
+def adain_rp_forward(content, style, sd, rp_blocks, content_weight, style_weight):
+    """AdaINRPNet.forward loss dict (adain_rp.py:110-138)."""
+    with torch.no_grad():
+        cf = rp_stack(content, sd, "rp_shared_encoder.", rp_blocks)
+        sf = rp_stack(style, sd, "rp_shared_encoder.", rp_blocks)
+        stylized = rp_stack(adain(cf, sf), sd, "rp_decoder.", rp_blocks)
+        ds = encode_with_intermediate(stylized, sd)
+        dt = encode_with_intermediate(style, sd)
+        dc = encode_with_intermediate(content, sd)
+        ls = style_loss(ds[0], dt[0])
+        for i in range(1, 4):
+            ls = ls + style_loss(ds[i], dt[i])
+        lc = F.mse_loss(ds[-1], dc[-1])
+        tot = content_weight * lc + style_weight * ls
+        return {"style_loss": ls, "content_loss": lc, "total_loss": tot}
+
+
+# ---- a7/a8/a9: WCT ----------------------------------------------------------------
+def _psd_power(A: Tensor, p: float) -> Tensor:
+    """matrix_sqrt / matrix_inv_sqrt body (wct_rp.py:7-40): +1e-4 on the diagonal,
+    torch.svd, truncate at the first singular value < 1e-5, V diag(s^p) V^T."""
+    A = A.clone()
+    A.diagonal().add_(1e-4)
+    _, e, v = torch.svd(A, some=False)
+    k = A.shape[-1]
+    small = (e < 1e-5).nonzero()
+    if small.numel():
+        k = int(small[0, 0])
+    d = e[:k].pow(p)
+    return (v[:, :k] @ torch.diag(d)) @ v[:, :k].t()
+
+
+def matrix_sqrt(A: Tensor) -> Tensor:
+    return _psd_power(A, 0.5)
+
+
+def matrix_inv_sqrt(A: Tensor) -> Tensor:
+    return _psd_power(A, -0.5)
+
+
+def whiten_and_color(cF: Tensor, sF: Tensor) -> Tensor:
+    """WCTRPNet.whiten_and_color(method='closed-form') (wct_rp.py:82-114), fp64."""
+    n = cF.shape[1]
+    c_mean = cF.mean(1, keepdim=True)
+    cF = cF - c_mean
+    cc = (cF @ cF.t()).div(n - 1) + torch.eye(cF.shape[0], dtype=cF.dtype)
+    s_mean = sF.mean(1, keepdim=True)
+    sF = sF - s_mean
+    cs = (sF @ sF.t()).div(sF.shape[1] - 1)
+    c_sqrt = matrix_sqrt(cc)
+    c_isqrt = matrix_inv_sqrt(cc)
+    middle = matrix_sqrt(c_sqrt @ cs @ c_sqrt)
+    T = c_isqrt @ middle @ c_isqrt
+    return T @ cF + s_mean
+
+
+def wct_fuse(cfeat: Tensor, sfeat: Tensor) -> Tensor:
+    """WCTRPNet.fuse (wct_rp.py:157-166): per image, fp64 internals, fp32 out."""
+    outs = []
+    for cf, sf in zip(cfeat, sfeat):
+        c, h, w = cf.shape
+        o = whiten_and_color(cf.reshape(c, -1).double(), sf.reshape(c, -1).double())
+        outs.append(o.view(c, h, w).float())
+    return torch.stack(outs, 0)
+
+
+def wct_rp_test(content, style, sd, rp_blocks):
+    """WCTRPNet.test (wct_rp.py:139-147)."""
+    with torch.no_grad():
+        cf = rp_stack(content, sd, "rp_shared_encoder.", rp_blocks)
+        sf = rp_stack(style, sd, "rp_shared_encoder.", rp_blocks)
+        return rp_stack(wct_fuse(cf, sf), sd, "rp_decoder.", rp_blocks)
+
+
+# ---- a10-a13: SANet ---------------------------------------------------------------
+def sanet(content: Tensor, style: Tensor, sd: SD, prefix: str) -> Tensor:
+    """SANet.forward (sanet.py:82-99): softmax(F^T G) over keys, no 1/sqrt(d) scale."""
+    Fm = conv(mean_variance_norm(content), sd, prefix + "f", "none", False)
+    G = conv(mean_variance_norm(style), sd, prefix + "g", "none", False)
+    H = conv(style, sd, prefix + "h", "none", False)
+    b, c, h, w = Fm.shape
+    Fq = Fm.view(b, -1, w * h).permute(0, 2, 1)
+    S = torch.softmax(torch.bmm(Fq, G.view(b, -1, G.shape[2] * G.shape[3])), dim=-1)
+    O = torch.bmm(H.view(b, -1, H.shape[2] * H.shape[3]), S.permute(0, 2, 1))
+    O = O.view(content.shape)
+    return conv(O, sd, prefix + "out_conv", "none", False) + content
+
+
+def transform(c4, s4, c5, s5, sd: SD, prefix: str) -> Tensor:
+    """Transform.forward (sanet.py:148-149)."""
+    a = sanet(c4, s4, sd, prefix + "sanet4_1.")
+    b = F.interpolate(sanet(c5, s5, sd, prefix + "sanet5_1."), scale_factor=2, mode="nearest")
+    return conv(a + b, sd, prefix + "merge_conv", "reflect", False)
+
+
+def samodel_test(content: Tensor, style: Tensor, sd: SD) -> Tensor:
+    """SAModel.test (sanet.py:238-246)."""
+    with torch.no_grad():
+        sfeat = encode_with_intermediate(style, sd, 5)
+        cfeat = encode_with_intermediate(content, sd, 5)
+        fusion = transform(cfeat[3], sfeat[3], cfeat[4], sfeat[4], sd, "transform.")
+        return decoder(fusion, sd, "decoder.")
+
+
+def rel_l2(a: Tensor, b: Tensor) -> float:
+    a = a.double()
+    b = b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-300))
+
+
+def model_state_dict(shapes: Sequence[Tuple[str, Tuple[int, ...]]], seed: int) -> SD:
+    """Synthetic weights for a key/shape template (same generator as the product)."""
+    import sys
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "rp-style-transfer_amd"))
+    from rpst import synth
+    return {k: torch.from_numpy(v) for k, v in synth.synth_state_dict(shapes, seed).items()}

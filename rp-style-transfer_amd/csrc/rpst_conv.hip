@@ -1,0 +1,452 @@
+// Direct 3x3 / 1x1 convolution as an implicit GEMM on fp32 MFMA (gfx950).
+//
+// Replaces the ATen conv stacks of the reference hot path:
+//   RP encoder / decoder  Conv2d(k3, zero pad 1) + ReLU      network/base.py:363-396
+//   VGG encoder           ReflectionPad2d(1) + Conv2d + ReLU network/base.py:57-111
+//                         (+ MaxPool2d(2,2,ceil) fused into the next conv's loader)
+//   VGG-mirror decoder    ReflectionPad2d(1) + Conv2d [+ReLU] network/base.py:25-55,
+//                         sanet.py:162-192 (+ nearest Upsample x2 fused into the loader)
+//   SANet 1x1 f/g/h/out   Conv2d(k1) (+ residual add)         network/sanet.py:76-98
+//   Transform merge_conv  ReflectionPad2d + Conv2d on a + up2(b) network/sanet.py:146-149
+//
+// GEMM view per image n:  out[co][p] = sum_k W[co][k] * X[k][p],  k = (ci, kh, kw).
+//   M = Cout (block tile BM), N = pixels (block tile TH rows x 32 cols), K = Cin*KS*KS.
+// Per K chunk of CK input channels the block stages into LDS
+//   Ws[tap][ci][co]  : CK*KS*KS rows of BM weights (pre-packed K-major, 16-B loads)
+//   Xs[ci][py][px]   : the (TH+KS-1) x (32+KS-1) input halo patch per channel, built by
+//                      the loader with zero/reflect padding and pool/upsample/add applied
+// and every wave runs v_mfma_f32_32x32x2_f32 over its MT x NT sub-tiles of 32x32.
+// MFMA operand maps (cdna_hip_programming.md §3): lane l holds A[i=l&31][k=l>>5] and
+// B[k=l>>5][j=l&31]; C row = (r&3) + 8*(r>>2) + 4*(l>>5), col = l&31. The two K values
+// of one MFMA are channels ci, ci+1 at the same tap, so lane half h reads channel 2cp+h.
+// Loads of chunk c+1 are issued into registers before the MFMAs of chunk c and written
+// to LDS after them (issue-early / write-late), two workgroups per CU.
+// Patch loader: thread -> (channel group tid>>5, column tid&31), so each half-wave reads
+// a 128-B row segment and all row index math is wave-uniform (scalar).
+// Numerics: exact fp32 products, fp32 accumulation (MFMA = k-ordered fmaf chain).
+#include "rpst_common.h"
+
+namespace rpst {
+
+constexpr int kConvThreads = 256;
+constexpr int kTW = 32;  // pixels per N sub-tile = one row segment
+
+struct ConvArgs {
+  const float* in;
+  const float* aux;
+  const float* wpk;
+  const float* bias;
+  const float* res;
+  float* out;
+  int N, Cin, Hs, Ws, H, W, Cout, Cout_pad, nchunks;
+  int tiles_x, tiles_y, co_tiles;
+  int pad, relu;
+};
+
+template <int KS>
+struct ConvK {
+  static constexpr int CK = (KS == 3) ? 8 : 16;  // input channels per chunk
+  static constexpr int TAPS = KS * KS;
+  static constexpr int KCH = TAPS * CK;  // K values per chunk
+};
+
+// Resolve a logical (post-in_op) coordinate against padding. Returns false for a zero
+// pad position. Tile overhang beyond the image is clamped (its results are discarded).
+__device__ __forceinline__ bool resolve(int& v, int n, int pad, bool padded) {
+  if (padded) {
+    if (pad == RPST_PAD_ZERO) {
+      if (v < 0 || v >= n) return false;
+    } else {
+      v = reflect1(v, n);
+    }
+  }
+  v = v < 0 ? 0 : (v >= n ? n - 1 : v);
+  return true;
+}
+
+// Input value at resolved logical (y, x) of one channel plane, applying the fused op.
+template <int INOP>
+__device__ __forceinline__ float fetch(const float* __restrict__ p,
+                                       const float* __restrict__ q, int y, int x,
+                                       const ConvArgs& a) {
+  if (INOP == RPST_IN_MAXPOOL2) {
+    const int sy = 2 * y, sx = 2 * x;
+    const bool xr = sx + 1 < a.Ws, yd = sy + 1 < a.Hs;
+    const float* r0 = p + (int64_t)sy * a.Ws + sx;
+    float v = r0[0];
+    if (xr) v = fmaxf(v, r0[1]);
+    if (yd) v = fmaxf(v, r0[a.Ws]);
+    if (xr && yd) v = fmaxf(v, r0[a.Ws + 1]);
+    return v;
+  } else if (INOP == RPST_IN_UPSAMPLE2) {
+    return p[(int64_t)(y >> 1) * a.Ws + (x >> 1)];
+  } else if (INOP == RPST_IN_ADD_UPSAMPLE2) {
+    return p[(int64_t)y * a.W + x] + q[(int64_t)(y >> 1) * (a.W >> 1) + (x >> 1)];
+  } else {
+    return p[(int64_t)y * a.W + x];
+  }
+}
+
+template <int KS, int BM, int TH, int WM, int WN, int INOP>
+__global__ __launch_bounds__(kConvThreads, 2) void conv_mfma_kernel(ConvArgs a) {
+  using K = ConvK<KS>;
+  constexpr int CK = K::CK, TAPS = K::TAPS, KCH = K::KCH;
+  constexpr int OFF = (KS == 3) ? 1 : 0;
+  constexpr int PH = TH + KS - 1, PW = kTW + KS - 1;
+  constexpr int WTM = BM / WM;       // co per wave
+  constexpr int MT = WTM / 32;       // 32-row M sub-tiles per wave
+  constexpr int NT = TH / WN;        // rows (32-px N sub-tiles) per wave
+  static_assert(WM * WN == kConvThreads / kWave, "4 waves");
+  static_assert(MT >= 1 && NT >= 1 && (CK % 8) == 0, "tile");
+  constexpr int NW4 = KCH * BM / 4;  // float4 weight loads per chunk
+  constexpr int WLD = (NW4 + kConvThreads - 1) / kConvThreads;
+  constexpr int CPT = CK / 8;        // patch channels per thread (8 channel groups)
+  constexpr int HALO = (KS == 3) ? (2 * PH + 31) / 32 : 0;  // halo loads per lane
+
+  __shared__ float Ws[KCH * BM];
+  __shared__ float Xs[CK * PH * PW];
+
+  // block -> (co tile, image, tile row, tile col); co tile slowest so resident blocks
+  // share one weight slice in L2
+  int bid = blockIdx.x;
+  const int tx = bid % a.tiles_x;
+  bid /= a.tiles_x;
+  const int ty = bid % a.tiles_y;
+  bid /= a.tiles_y;
+  const int n = bid % a.N;
+  const int ct = bid / a.N;
+  const int co0 = ct * BM;
+  const int y0 = ty * TH, x0 = tx * kTW;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int h = lane >> 5, j = lane & 31;
+
+  // patch loader geometry: thread -> (channel group cg, column jc); rows are uniform
+  const int cg = tid >> 5, jc = tid & 31;
+  int bx = x0 + jc;  // body column (logical)
+  const bool bx_ok = resolve(bx, a.W, a.pad, KS == 3);
+  // halo element e of this lane: hi = jc + 32e < 2*PH covers patch column 0 / PW-1 of
+  // row hi>>1
+  int hy[HALO > 0 ? HALO : 1], hx[HALO > 0 ? HALO : 1];
+  bool h_ok[HALO > 0 ? HALO : 1], has_halo[HALO > 0 ? HALO : 1];
+#pragma unroll
+  for (int e = 0; e < HALO; ++e) {
+    const int hi = jc + 32 * e;
+    has_halo[e] = hi < 2 * PH;
+    hy[e] = y0 - OFF + (hi >> 1);
+    hx[e] = (hi & 1) ? x0 + kTW : x0 - 1;
+    const bool ok1 = resolve(hy[e], a.H, a.pad, true);
+    const bool ok2 = resolve(hx[e], a.W, a.pad, true);
+    h_ok[e] = has_halo[e] && ok1 && ok2;
+  }
+  const int64_t in_plane = (INOP == RPST_IN_MAXPOOL2 || INOP == RPST_IN_UPSAMPLE2)
+                               ? (int64_t)a.Hs * a.Ws
+                               : (int64_t)a.H * a.W;
+  const int64_t aux_plane = (int64_t)(a.H >> 1) * (a.W >> 1);
+
+  floatx16 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
+
+  float4 wreg[WLD];
+  float xreg[CPT][PH + HALO];
+
+  auto load_chunk = [&](int c) {
+    const float4* wsrc = reinterpret_cast<const float4*>(
+        a.wpk + (int64_t)c * KCH * a.Cout_pad + co0);
+#pragma unroll
+    for (int u = 0; u < WLD; ++u) {
+      const int i = tid + u * kConvThreads;
+      if (i < NW4) {
+        const int row = i / (BM / 4), col4 = i % (BM / 4);
+        wreg[u] = wsrc[(int64_t)row * (a.Cout_pad / 4) + col4];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      const int ci = c * CK + cg + 8 * q;
+      const bool cok = ci < a.Cin;
+      const int64_t pl = (int64_t)n * a.Cin + ci;
+      const float* p = a.in + pl * in_plane;
+      const float* qa = a.aux + pl * aux_plane;
+#pragma unroll
+      for (int py = 0; py < PH; ++py) {
+        int y = y0 - OFF + py;
+        const bool yok = resolve(y, a.H, a.pad, KS == 3);
+        xreg[q][py] = (cok && yok && bx_ok) ? fetch<INOP>(p, qa, y, bx, a) : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < HALO; ++e)
+        xreg[q][PH + e] = (cok && h_ok[e]) ? fetch<INOP>(p, qa, hy[e], hx[e], a) : 0.f;
+    }
+  };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int u = 0; u < WLD; ++u) {
+      const int i = tid + u * kConvThreads;
+      if (i < NW4) reinterpret_cast<float4*>(Ws)[i] = wreg[u];
+    }
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      float* xs = Xs + (cg + 8 * q) * PH * PW;
+#pragma unroll
+      for (int py = 0; py < PH; ++py) xs[py * PW + jc + OFF] = xreg[q][py];
+#pragma unroll
+      for (int e = 0; e < HALO; ++e) {
+        const int hi = jc + 32 * e;
+        if (has_halo[e]) xs[(hi >> 1) * PW + ((hi & 1) ? PW - 1 : 0)] = xreg[q][PH + e];
+      }
+    }
+  };
+
+  const int aoff = h * BM + wm * WTM + j;
+  const int boff = h * PH * PW + (wn * NT) * PW + j;
+
+  load_chunk(0);
+  for (int c = 0; c < a.nchunks; ++c) {
+    store_chunk();
+    __syncthreads();
+    if (c + 1 < a.nchunks) load_chunk(c + 1);
+#pragma unroll
+    for (int t = 0; t < TAPS; ++t) {
+      const int kh = t / KS, kw = t % KS;
+#pragma unroll
+      for (int cp = 0; cp < CK / 2; ++cp) {
+        float av[MT], bv[NT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) av[mt] = Ws[aoff + (t * CK + 2 * cp) * BM + mt * 32];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          bv[nt] = Xs[boff + (2 * cp) * PH * PW + (nt + kh) * PW + kw];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mt], bv[nt], acc[mt][nt],
+                                                               0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // epilogue: bias, ReLU, residual, predicated coalesced stores (128 B per half-wave)
+  const int x = x0 + j;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + wm * WTM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (co >= a.Cout) continue;
+      const float b = a.bias ? a.bias[co] : 0.f;
+      const int64_t pbase = ((int64_t)n * a.Cout + co) * a.H * a.W;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int y = y0 + wn * NT + nt;
+        if (y < a.H && x < a.W) {
+          float v = acc[mt][nt][r] + b;
+          if (a.relu) v = fmaxf(v, 0.f);
+          const int64_t o = pbase + (int64_t)y * a.W + x;
+          if (a.res) v += a.res[o];
+          a.out[o] = v;
+        }
+      }
+    }
+  }
+}
+
+// ---- weight packing: (Cout,Cin,KS,KS) -> [chunk][tap][ci_local][Cout_pad] ------------
+__global__ void conv_pack_kernel(const float* __restrict__ w, float* __restrict__ pk,
+                                 int Cout, int Cin, int KS, int CK, int Cout_pad,
+                                 int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int taps = KS * KS;
+  const int co = (int)(i % Cout_pad);
+  int64_t r = i / Cout_pad;
+  const int cl = (int)(r % CK);
+  r /= CK;
+  const int t = (int)(r % taps);
+  const int c = (int)(r / taps);
+  const int ci = c * CK + cl;
+  float v = 0.f;
+  if (ci < Cin && co < Cout) v = w[(((int64_t)co * Cin + ci) * taps) + t];
+  pk[i] = v;
+}
+
+struct TileCfg {
+  int BM, TH;
+};
+
+static TileCfg pick_cfg(int Cout) {
+  if (Cout > 64) return {128, 8};
+  if (Cout > 32) return {64, 8};
+  return {32, 16};
+}
+
+static int pad_cout(int Cout) {
+  const int bm = pick_cfg(Cout).BM;
+  return (Cout + bm - 1) / bm * bm;
+}
+
+static int ck_of(int ksize) { return ksize == 3 ? ConvK<3>::CK : ConvK<1>::CK; }
+
+template <int KS, int INOP>
+static void launch_conv(const ConvArgs& a, int BM, hipStream_t st) {
+  const int blocks = a.tiles_x * a.tiles_y * a.N * a.co_tiles;
+  if (BM == 128)
+    conv_mfma_kernel<KS, 128, 8, 2, 2, INOP><<<blocks, kConvThreads, 0, st>>>(a);
+  else if (BM == 64)
+    conv_mfma_kernel<KS, 64, 8, 2, 2, INOP><<<blocks, kConvThreads, 0, st>>>(a);
+  else
+    conv_mfma_kernel<KS, 32, 16, 1, 4, INOP><<<blocks, kConvThreads, 0, st>>>(a);
+}
+
+}  // namespace rpst
+
+using namespace rpst;
+
+extern "C" size_t rpst_conv2d_packed_size(int Cout, int Cin, int ksize) {
+  if (Cout <= 0 || Cin <= 0 || (ksize != 1 && ksize != 3)) return 0;
+  const int ck = ck_of(ksize);
+  const size_t nch = (size_t)(Cin + ck - 1) / ck;
+  return nch * ksize * ksize * ck * (size_t)pad_cout(Cout) * sizeof(float);
+}
+
+extern "C" int rpst_conv2d_pack(const float* weight, float* packed, int Cout, int Cin,
+                                int ksize, rpst_stream_t stream) {
+  RPST_REQUIRE(weight && packed, "conv2d_pack: null pointer");
+  RPST_REQUIRE(Cout > 0 && Cin > 0, "conv2d_pack: bad channels");
+  RPST_REQUIRE(ksize == 1 || ksize == 3, "conv2d_pack: ksize must be 1 or 3, got %d", ksize);
+  const int64_t total = (int64_t)(rpst_conv2d_packed_size(Cout, Cin, ksize) / sizeof(float));
+  const int threads = 256;
+  conv_pack_kernel<<<(unsigned)((total + threads - 1) / threads), threads, 0,
+                     as_stream(stream)>>>(weight, packed, Cout, Cin, ksize, ck_of(ksize),
+                                          pad_cout(Cout), total);
+  return launch_status("conv_pack_kernel");
+}
+
+extern "C" int rpst_conv2d(const float* input, const float* aux, const float* packed_weight,
+                           const float* bias, const float* residual, float* out, int N,
+                           int Cin, int Hs, int Ws, int Cout, int ksize, int pad_mode,
+                           int in_op, int relu, rpst_stream_t stream) {
+  RPST_REQUIRE(input && packed_weight && out, "conv2d: null pointer");
+  RPST_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && Hs > 0 && Ws > 0, "conv2d: bad shape");
+  RPST_REQUIRE(ksize == 1 || ksize == 3, "conv2d: ksize must be 1 or 3, got %d", ksize);
+  RPST_REQUIRE(pad_mode == RPST_PAD_ZERO || pad_mode == RPST_PAD_REFLECT, "conv2d: bad pad");
+  RPST_REQUIRE(in_op >= RPST_IN_NONE && in_op <= RPST_IN_ADD_UPSAMPLE2, "conv2d: bad in_op");
+  ConvArgs a{};
+  a.in = input;
+  a.aux = aux;
+  a.wpk = packed_weight;
+  a.bias = bias;
+  a.res = residual;
+  a.out = out;
+  a.N = N;
+  a.Cin = Cin;
+  a.Hs = Hs;
+  a.Ws = Ws;
+  a.Cout = Cout;
+  a.pad = pad_mode;
+  a.relu = relu ? 1 : 0;
+  switch (in_op) {
+    case RPST_IN_MAXPOOL2:
+      a.H = (Hs + 1) / 2;
+      a.W = (Ws + 1) / 2;
+      break;
+    case RPST_IN_UPSAMPLE2:
+      a.H = 2 * Hs;
+      a.W = 2 * Ws;
+      break;
+    case RPST_IN_ADD_UPSAMPLE2:
+      RPST_REQUIRE(aux != nullptr, "conv2d: ADD_UPSAMPLE2 needs aux");
+      RPST_REQUIRE((Hs % 2) == 0 && (Ws % 2) == 0, "conv2d: ADD_UPSAMPLE2 needs even H,W");
+      a.H = Hs;
+      a.W = Ws;
+      break;
+    default:
+      a.H = Hs;
+      a.W = Ws;
+  }
+  if (ksize == 3 && pad_mode == RPST_PAD_REFLECT)
+    RPST_REQUIRE(a.H >= 2 && a.W >= 2, "conv2d: reflect padding needs H,W >= 2");
+  const TileCfg cfg = pick_cfg(Cout);
+  const int ck = ck_of(ksize);
+  a.Cout_pad = pad_cout(Cout);
+  a.nchunks = (Cin + ck - 1) / ck;
+  a.tiles_x = (a.W + kTW - 1) / kTW;
+  a.tiles_y = (a.H + cfg.TH - 1) / cfg.TH;
+  a.co_tiles = a.Cout_pad / cfg.BM;
+  const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * N * a.co_tiles;
+  RPST_REQUIRE(blocks <= 0x7fffffffLL, "conv2d: grid too large");
+  RPST_REQUIRE((int64_t)N * (Cout > Cin ? Cout : Cin) * a.H * a.W < (1LL << 40),
+               "conv2d: tensor too large");
+  hipStream_t st = as_stream(stream);
+  if (ksize == 1) {
+    RPST_REQUIRE(in_op == RPST_IN_NONE, "conv2d: 1x1 conv supports in_op NONE only");
+    launch_conv<1, RPST_IN_NONE>(a, cfg.BM, st);
+  } else if (in_op == RPST_IN_MAXPOOL2) {
+    launch_conv<3, RPST_IN_MAXPOOL2>(a, cfg.BM, st);
+  } else if (in_op == RPST_IN_UPSAMPLE2) {
+    launch_conv<3, RPST_IN_UPSAMPLE2>(a, cfg.BM, st);
+  } else if (in_op == RPST_IN_ADD_UPSAMPLE2) {
+    launch_conv<3, RPST_IN_ADD_UPSAMPLE2>(a, cfg.BM, st);
+  } else {
+    launch_conv<3, RPST_IN_NONE>(a, cfg.BM, st);
+  }
+  return launch_status("conv_mfma_kernel");
+}
+
+// ---- stand-alone max-pool / upsample (used where no conv follows directly) ----------
+__global__ void maxpool2_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                int64_t planes, int H, int W, int Ho, int Wo) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= planes * Ho * Wo) return;
+  const int x = (int)(i % Wo);
+  const int64_t r = i / Wo;
+  const int y = (int)(r % Ho);
+  const int64_t p = r / Ho;
+  const float* s = in + p * H * W;
+  const int sy = 2 * y, sx = 2 * x;
+  float v = s[(int64_t)sy * W + sx];
+  if (sx + 1 < W) v = fmaxf(v, s[(int64_t)sy * W + sx + 1]);
+  if (sy + 1 < H) v = fmaxf(v, s[(int64_t)(sy + 1) * W + sx]);
+  if (sx + 1 < W && sy + 1 < H) v = fmaxf(v, s[(int64_t)(sy + 1) * W + sx + 1]);
+  out[i] = v;
+}
+
+__global__ void upsample2_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                 int64_t planes, int H, int W) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int Wo = 2 * W, Ho = 2 * H;
+  if (i >= planes * Ho * Wo) return;
+  const int x = (int)(i % Wo);
+  const int64_t r = i / Wo;
+  const int y = (int)(r % Ho);
+  const int64_t p = r / Ho;
+  out[i] = in[p * H * W + (int64_t)(y >> 1) * W + (x >> 1)];
+}
+
+extern "C" int rpst_maxpool2x2_ceil(const float* in, float* out, int N, int C, int H, int W,
+                                    rpst_stream_t stream) {
+  RPST_REQUIRE(in && out && N > 0 && C > 0 && H > 0 && W > 0, "maxpool2x2: bad args");
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  const int64_t total = (int64_t)N * C * Ho * Wo;
+  maxpool2_kernel<<<(unsigned)((total + 255) / 256), 256, 0, as_stream(stream)>>>(
+      in, out, (int64_t)N * C, H, W, Ho, Wo);
+  return launch_status("maxpool2_kernel");
+}
+
+extern "C" int rpst_upsample_nearest2x(const float* in, float* out, int N, int C, int H,
+                                       int W, rpst_stream_t stream) {
+  RPST_REQUIRE(in && out && N > 0 && C > 0 && H > 0 && W > 0, "upsample2x: bad args");
+  const int64_t total = (int64_t)N * C * 4 * H * W;
+  upsample2_kernel<<<(unsigned)((total + 255) / 256), 256, 0, as_stream(stream)>>>(
+      in, out, (int64_t)N * C, H, W);
+  return launch_status("upsample2_kernel");
+}

@@ -1,0 +1,115 @@
+"""Drop-in WCT-RP (reference network/wct_rp.py) on MI355X kernels.
+
+  matrix_inv_sqrt / matrix_sqrt  wct_rp.py:7-40   -> fp64 HIP kernels (rpst.ops)
+  WCTRPNet                       wct_rp.py:42-194
+    .whiten_and_color            wct_rp.py:82-114 -> fp64 MFMA covariance / transform
+    .fuse                        wct_rp.py:157-166 -> batched over images on the GPU
+The closed-form WCT (Lu et al.) runs in fp64 like the reference: features are read as
+fp32, widened to fp64 in registers, and the fused feature is written back as fp32.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from rpst import ops
+from rpst.plan import KernelSequential
+
+from .adain_rp import AdaINRPNet, encode_both  # noqa: F401 (re-export, wct_rp.py:3)
+from .base import (BaseNet, build_decrease_depth_rp_blocks, build_increase_depth_rp_blocks,
+                   calc_mean_std, mse)
+
+
+def matrix_inv_sqrt(A):
+    """(A + 1e-4 I)^(-1/2) for symmetric PSD A (wct_rp.py:7-22), fp64 on the GPU."""
+    return ops.matrix_power_psd(A, -0.5)
+
+
+def matrix_sqrt(A):
+    """(A + 1e-4 I)^(1/2) for symmetric PSD A (wct_rp.py:24-40), fp64 on the GPU."""
+    return ops.matrix_power_psd(A, 0.5)
+
+
+class WCTRPNet(BaseNet):
+    def __init__(self, config, vgg_encoder) -> None:
+        super().__init__()
+        enc_layers = list(vgg_encoder.children())
+        self.config = config
+        self.enc_1 = KernelSequential(*enc_layers[:4])
+        self.enc_2 = KernelSequential(*enc_layers[4:11])
+        self.enc_3 = KernelSequential(*enc_layers[11:18])
+        self.enc_4 = KernelSequential(*enc_layers[18:31])
+        for name in ['enc_1', 'enc_2', 'enc_3', 'enc_4']:
+            for param in getattr(self, name).parameters():
+                param.requires_grad = False
+        assert self.config['rp_blocks'] - 2 >= 0
+        self.encoder_out_dim = self.config['hidden_dim'] * 2 ** (self.config['rp_blocks'] - 1)
+        self.rp_shared_encoder = build_increase_depth_rp_blocks(
+            self.config['rp_blocks'], 3, self.config['hidden_dim'], self.encoder_out_dim)
+        if self.config.get('resume'):
+            ckpt = torch.load(self.config['checkpoint_path'], map_location='cpu',
+                              weights_only=True)
+            self.rp_shared_encoder.load_state_dict(ckpt['encoder'])
+            print(f"Loaded checkpoint from {self.config['checkpoint_path']}")
+            for param in self.rp_shared_encoder.parameters():
+                param.requires_grad = False
+        self.decoder_in_dim = self.encoder_out_dim
+        self.decoder_hidden_dim = self.decoder_in_dim // 2
+        self.rp_decoder = build_decrease_depth_rp_blocks(
+            self.config['rp_blocks'], self.decoder_in_dim, self.decoder_hidden_dim, 3)
+        self.mse_loss = nn.MSELoss()
+
+    def whiten_and_color(self, cF, sF, method='closed-form'):
+        """cF, sF: (C, HW) fp64 device tensors -> (C, HW) fp64."""
+        assert method == 'closed-form', "only the closed-form (Lu et al.) branch is used"
+        return ops.whiten_and_color(cF, sF)
+
+    def encode_with_intermediate(self, input):
+        results = [input]
+        for i in range(4):
+            results.append(getattr(self, 'enc_{:d}'.format(i + 1))(results[-1]))
+        return results[1:]
+
+    def encode(self, input):
+        for i in range(4):
+            input = getattr(self, 'enc_{:d}'.format(i + 1))(input)
+        return input
+
+    def calc_content_loss(self, input, target):
+        return mse(input, target)
+
+    def calc_style_loss(self, input, target):
+        input_mean, input_std = calc_mean_std(input)
+        target_mean, target_std = calc_mean_std(target)
+        return mse(input_mean, target_mean) + mse(input_std, target_std)
+
+    def test(self, content, style, iterations=0, bid=0, c_mask_path=None, s_mask_path=None):
+        self.eval()
+        with torch.no_grad():
+            content_feat, style_feat = encode_both(self.rp_shared_encoder, content, style)
+            fusion_feat = self.fuse(content_feat, style_feat)
+            stylized = self.rp_decoder(fusion_feat)
+            self.train()
+            return stylized
+
+    def save(self, save_path, iterations=0):
+        torch.save({'encoder': self.rp_shared_encoder.state_dict(),
+                    'decoder': self.rp_decoder.state_dict()}, save_path)
+
+    def fuse(self, content_feats, style_feats):
+        """Per-image closed-form WCT, all images of the batch in one set of launches."""
+        return ops.wct_fuse(content_feats, style_feats)
+
+    def forward(self, content, style, alpha=1.0):
+        assert 0 <= alpha <= 1
+        content_feat, style_feat = encode_both(self.rp_shared_encoder, content, style)
+        stylized = self.rp_decoder(self.fuse(content_feat, style_feat))
+        down_stylized_feats = self.encode_with_intermediate(stylized)
+        down_style_feats = self.encode_with_intermediate(style)
+        down_content_feats = self.encode_with_intermediate(content)
+        loss_s = self.calc_style_loss(down_stylized_feats[0], down_style_feats[0])
+        for i in range(1, 4):
+            loss_s += self.calc_style_loss(down_stylized_feats[i], down_style_feats[i])
+        loss_c = self.calc_content_loss(down_stylized_feats[-1], down_content_feats[-1])
+        total_loss = self.config['content_weight'] * loss_c + self.config['style_weight'] * loss_s
+        return {'style_loss': loss_s, 'content_loss': loss_c, 'total_loss': total_loss}, total_loss

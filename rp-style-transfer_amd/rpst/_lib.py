@@ -1,0 +1,78 @@
+"""ctypes binding of librpst.so (the C ABI declared in include/rpst.h).
+
+The library is built in-tree (`make -C rp-style-transfer_amd/csrc`, or
+`__graft_entry__.build()`) and loaded from there; RPST_LIB overrides the path.
+There is no fallback: if the library is missing or a call fails, a RuntimeError is
+raised with the library's own message (rpst_last_error()).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RPST_LIB", os.path.join(os.path.dirname(_HERE), "csrc", "librpst.so"))
+
+_c_float_p = ctypes.c_void_p
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_F = ctypes.c_float
+_D = ctypes.c_double
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); must match include/rpst.h exactly
+SIGNATURES = {
+    "rpst_version": (_I, []),
+    "rpst_last_error": (ctypes.c_char_p, []),
+    "rpst_calc_mean_std": (_I, [_P, _P, _P, _I, _I, _I64, _F, _P]),
+    "rpst_adain_workspace_size": (_SZ, [_I, _I]),
+    "rpst_adain": (_I, [_P, _P, _P, _I, _I, _I64, _F, _P, _SZ, _P]),
+    "rpst_mean_variance_norm": (_I, [_P, _P, _I, _I, _I64, _F, _P, _SZ, _P]),
+    "rpst_conv2d_packed_size": (_SZ, [_I, _I, _I]),
+    "rpst_conv2d_pack": (_I, [_P, _P, _I, _I, _I, _P]),
+    "rpst_conv2d": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "rpst_maxpool2x2_ceil": (_I, [_P, _P, _I, _I, _I, _I, _P]),
+    "rpst_upsample_nearest2x": (_I, [_P, _P, _I, _I, _I, _I, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class RpstError(RuntimeError):
+    pass
+
+
+def load():
+    """Load librpst.so once; raise RpstError if it is absent (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RpstError(
+                f"rpst: HIP library not found at {LIB_PATH}; build it with "
+                "`make -C rp-style-transfer_amd/csrc` or __graft_entry__.build()")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = load().rpst_last_error().decode(errors="replace")
+        raise RpstError(f"{what} failed (status {status}): {msg}")
+
+
+def call(name: str, *args):
+    """Call an rpst_* entry point that returns a status code; raise on failure."""
+    st = getattr(load(), name)(*args)
+    check(st, name)

@@ -1,0 +1,204 @@
+"""Tensor-level wrappers over the rpst C ABI (device memory and streams come from torch).
+
+Every op takes ROCm-device fp32 tensors, allocates its outputs/workspace through the
+torch caching allocator and launches on torch's current stream. CPU tensors, wrong
+dtypes and autograd-requiring inputs raise: this is the product path and it has no
+CPU or ATen fallback (the CPU restatement lives in oracle/, for tests only).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+
+PAD_ZERO, PAD_REFLECT = 0, 1
+IN_NONE, IN_MAXPOOL2, IN_UPSAMPLE2, IN_ADD_UPSAMPLE2 = 0, 1, 2, 3
+
+
+class Trace:
+    """Optional per-launch HIP-event timing (bench.py): records (name, flops, bytes,
+    start, end) around each traced launch on torch's current stream, which is the
+    stream every rpst kernel is launched on."""
+
+    def __init__(self):
+        self.records = []
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for name, flops, nbytes, e0, e1 in self.records:
+            ms = e0.elapsed_time(e1)
+            a = agg.setdefault(name, {"launches": 0, "ms": 0.0, "flops": flops, "bytes": nbytes})
+            a["launches"] += 1
+            a["ms"] += ms
+        return agg
+
+
+TRACE: Optional[Trace] = None
+
+
+class _traced:
+    def __init__(self, name, flops=0.0, nbytes=0.0):
+        self.args = (name, flops, nbytes)
+
+    def __enter__(self):
+        if TRACE is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+
+    def __exit__(self, *exc):
+        if TRACE is not None:
+            self.e1.record()
+            TRACE.records.append((*self.args, self.e0, self.e1))
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _check(*ts: torch.Tensor) -> None:
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(
+                "rpst kernels run on a ROCm GPU only; got a CPU tensor (the CPU reference "
+                "path is oracle/, which is test infrastructure, not a fallback)")
+        if t.dtype != torch.float32:
+            raise RuntimeError(f"rpst kernels take float32 tensors, got {t.dtype}")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"rpst: tensors on different devices ({dev} vs {t.device})")
+        if torch.is_grad_enabled() and t.requires_grad:
+            raise NotImplementedError(
+                "rpst: backward kernels are not implemented (training path is SURVEY §8(f) "
+                "rank 2); call under torch.no_grad()")
+
+
+def _c(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def calc_mean_std(feat: torch.Tensor, eps: float = 1e-5) -> Tuple[torch.Tensor, torch.Tensor]:
+    """network/base.py:399-407 on the GPU: (N,C,H,W) -> mean, std of shape (N,C,1,1)."""
+    assert feat.dim() == 4
+    _check(feat)
+    feat = _c(feat)
+    N, C = feat.shape[:2]
+    hw = feat.numel() // (N * C)
+    mean = torch.empty((N, C, 1, 1), device=feat.device, dtype=torch.float32)
+    std = torch.empty_like(mean)
+    _lib.call("rpst_calc_mean_std", feat.data_ptr(), mean.data_ptr(), std.data_ptr(),
+              N, C, hw, eps, _stream(feat))
+    return mean, std
+
+
+def adaptive_instance_normalization(content: torch.Tensor, style: torch.Tensor,
+                                    eps: float = 1e-5,
+                                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """network/base.py:410-418 on the GPU (stats + apply, 2 launches)."""
+    assert content.size() == style.size()
+    assert content.dim() == 4
+    _check(content, style)
+    content, style = _c(content), _c(style)
+    N, C = content.shape[:2]
+    hw = content.numel() // (N * C)
+    if out is None:
+        out = torch.empty_like(content)
+    nbytes = _lib.load().rpst_adain_workspace_size(N, C)
+    ws = torch.empty(nbytes, device=content.device, dtype=torch.uint8)
+    with _traced(f"adain C{C} {hw}px N{N}", 0.0, 3.0 * 4 * N * C * hw):
+        _lib.call("rpst_adain", content.data_ptr(), style.data_ptr(), out.data_ptr(), N, C, hw,
+                  eps, ws.data_ptr(), nbytes, _stream(content))
+    return out
+
+
+def mean_variance_norm(feat: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    """network/sanet.py:20-24 on the GPU."""
+    assert feat.dim() == 4
+    _check(feat)
+    feat = _c(feat)
+    N, C = feat.shape[:2]
+    hw = feat.numel() // (N * C)
+    out = torch.empty_like(feat)
+    nbytes = _lib.load().rpst_adain_workspace_size(N, C)
+    ws = torch.empty(nbytes, device=feat.device, dtype=torch.uint8)
+    _lib.call("rpst_mean_variance_norm", feat.data_ptr(), out.data_ptr(), N, C, hw, eps,
+              ws.data_ptr(), nbytes, _stream(feat))
+    return out
+
+
+def pack_conv_weight(weight: torch.Tensor) -> torch.Tensor:
+    """Repack (Cout,Cin,k,k) fp32 weights into the conv kernel's K-major layout."""
+    _check(weight)
+    weight = _c(weight.detach())
+    cout, cin, kh, kw = weight.shape
+    assert kh == kw and kh in (1, 3), "rpst conv supports 1x1 and 3x3 kernels"
+    nbytes = _lib.load().rpst_conv2d_packed_size(cout, cin, kh)
+    packed = torch.empty(nbytes // 4, device=weight.device, dtype=torch.float32)
+    _lib.call("rpst_conv2d_pack", weight.data_ptr(), packed.data_ptr(), cout, cin, kh,
+              _stream(weight))
+    return packed
+
+
+def conv_out_hw(h: int, w: int, in_op: int) -> Tuple[int, int]:
+    if in_op == IN_MAXPOOL2:
+        return (h + 1) // 2, (w + 1) // 2
+    if in_op == IN_UPSAMPLE2:
+        return 2 * h, 2 * w
+    return h, w
+
+
+def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], cout: int,
+           ksize: int, pad: int = PAD_ZERO, in_op: int = IN_NONE, relu: bool = False,
+           aux: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = [relu](conv_k(in_op(x)) + bias) [+ residual]; see include/rpst.h."""
+    assert x.dim() == 4
+    _check(x, packed, bias, aux, residual)
+    x = _c(x)
+    n, cin, hs, ws = x.shape
+    h, w = conv_out_hw(hs, ws, in_op)
+    if out is None:
+        out = torch.empty((n, cout, h, w), device=x.device, dtype=torch.float32)
+    if residual is not None:
+        residual = _c(residual)
+        assert tuple(residual.shape) == (n, cout, h, w)
+    if aux is not None:
+        aux = _c(aux)
+        assert tuple(aux.shape) == (n, cin, h // 2, w // 2)
+    name = f"conv{ksize}x{ksize} {cin}->{cout} {h}x{w} N{n} op{in_op}"
+    with _traced(name, 2.0 * n * cout * h * w * cin * ksize * ksize,
+                 4.0 * (x.numel() + n * cout * h * w)):
+        _lib.call("rpst_conv2d", x.data_ptr(), _ptr(aux), packed.data_ptr(),
+                  _ptr(None if bias is None else _c(bias.detach())), _ptr(residual),
+                  out.data_ptr(), n, cin, hs, ws, cout, ksize, pad, in_op, int(bool(relu)),
+                  _stream(x))
+    return out
+
+
+def maxpool2x2_ceil(x: torch.Tensor) -> torch.Tensor:
+    _check(x)
+    x = _c(x)
+    n, c, h, w = x.shape
+    out = torch.empty((n, c, (h + 1) // 2, (w + 1) // 2), device=x.device, dtype=x.dtype)
+    _lib.call("rpst_maxpool2x2_ceil", x.data_ptr(), out.data_ptr(), n, c, h, w, _stream(x))
+    return out
+
+
+def upsample_nearest2x(x: torch.Tensor) -> torch.Tensor:
+    _check(x)
+    x = _c(x)
+    n, c, h, w = x.shape
+    out = torch.empty((n, c, 2 * h, 2 * w), device=x.device, dtype=x.dtype)
+    _lib.call("rpst_upsample_nearest2x", x.data_ptr(), out.data_ptr(), n, c, h, w, _stream(x))
+    return out

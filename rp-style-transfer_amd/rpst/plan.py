@@ -1,0 +1,138 @@
+"""Compile an nn.Sequential conv stack into fused rpst conv launches and run it.
+
+The reference builds its stacks from plain layers (network/base.py:25-111,363-396,
+sanet.py:162-192): [MaxPool2d | Upsample] -> [ReflectionPad2d] -> Conv2d -> [ReLU].
+Each such group becomes ONE rpst_conv2d launch: the pool/upsample and the padding are
+applied by the conv kernel's tile loader and ReLU by its epilogue, so no intermediate
+(padded, pooled or upsampled) tensor is ever written to HBM.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Iterable, List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+@dataclass
+class ConvStep:
+    conv: nn.Conv2d
+    pad: int
+    in_op: int
+    relu: bool
+
+
+@dataclass
+class OpStep:
+    in_op: int  # stand-alone MAXPOOL2 / UPSAMPLE2 with no conv after it
+
+
+def _is_pad1(m: nn.Module) -> bool:
+    return isinstance(m, nn.ReflectionPad2d) and tuple(m.padding) == (1, 1, 1, 1)
+
+
+def compile_layers(layers: Iterable[nn.Module]) -> List[object]:
+    steps: List[object] = []
+    in_op = ops.IN_NONE
+    reflect = False
+    last_conv: Optional[ConvStep] = None
+    for m in layers:
+        if isinstance(m, nn.ReLU):
+            if last_conv is None or last_conv.relu:
+                raise NotImplementedError("rpst plan: ReLU must directly follow a Conv2d")
+            last_conv.relu = True
+            continue
+        last_conv = None
+        if isinstance(m, nn.MaxPool2d):
+            k = m.kernel_size if isinstance(m.kernel_size, tuple) else (m.kernel_size,) * 2
+            s = m.stride if isinstance(m.stride, tuple) else (m.stride,) * 2
+            p = m.padding if isinstance(m.padding, tuple) else (m.padding,) * 2
+            if tuple(k) != (2, 2) or tuple(s) != (2, 2) or tuple(p) != (0, 0) or not m.ceil_mode:
+                raise NotImplementedError(f"rpst plan: unsupported {m}")
+            if in_op != ops.IN_NONE or reflect:
+                raise NotImplementedError("rpst plan: pool after pad/op")
+            in_op = ops.IN_MAXPOOL2
+        elif isinstance(m, nn.Upsample):
+            if m.mode != "nearest" or float(m.scale_factor) != 2.0:
+                raise NotImplementedError(f"rpst plan: unsupported {m}")
+            if in_op != ops.IN_NONE or reflect:
+                raise NotImplementedError("rpst plan: upsample after pad/op")
+            in_op = ops.IN_UPSAMPLE2
+        elif isinstance(m, nn.ReflectionPad2d):
+            if not _is_pad1(m) or reflect:
+                raise NotImplementedError(f"rpst plan: unsupported {m}")
+            reflect = True
+        elif isinstance(m, nn.Conv2d):
+            k = tuple(m.kernel_size)
+            if (tuple(m.stride) != (1, 1) or tuple(m.dilation) != (1, 1) or m.groups != 1
+                    or k not in ((1, 1), (3, 3))):
+                raise NotImplementedError(f"rpst plan: unsupported {m}")
+            pad_t = tuple(m.padding)
+            if k == (3, 3):
+                if reflect and pad_t == (0, 0):
+                    pad = ops.PAD_REFLECT
+                elif not reflect and pad_t == (1, 1) and m.padding_mode == "zeros":
+                    pad = ops.PAD_ZERO
+                else:
+                    raise NotImplementedError(f"rpst plan: unsupported padding for {m}")
+            else:
+                if reflect or pad_t != (0, 0) or in_op != ops.IN_NONE:
+                    raise NotImplementedError(f"rpst plan: unsupported 1x1 conv {m}")
+                pad = ops.PAD_ZERO
+            step = ConvStep(m, pad, in_op, False)
+            steps.append(step)
+            last_conv = step
+            in_op, reflect = ops.IN_NONE, False
+        else:
+            raise NotImplementedError(f"rpst plan: unsupported layer {type(m).__name__}")
+    if reflect:
+        raise NotImplementedError("rpst plan: trailing ReflectionPad2d")
+    if in_op != ops.IN_NONE:
+        steps.append(OpStep(in_op))
+    return steps
+
+
+def packed_weight(conv: nn.Conv2d) -> torch.Tensor:
+    """K-major packed copy of conv.weight, cached on the module and refreshed whenever
+    the parameter is replaced or modified in place (load_state_dict, optimizer step)."""
+    w = conv.weight
+    key = (w.device, w.data_ptr(), w._version)
+    cached = getattr(conv, "_rpst_packed", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    with torch.no_grad():
+        packed = ops.pack_conv_weight(w.detach())
+    conv._rpst_packed = (key, packed)
+    return packed
+
+
+def run_conv_step(step: ConvStep, x: torch.Tensor, aux=None, residual=None) -> torch.Tensor:
+    c = step.conv
+    return ops.conv2d(x, packed_weight(c), c.bias, c.out_channels, c.kernel_size[0],
+                      pad=step.pad, in_op=step.in_op, relu=step.relu, aux=aux,
+                      residual=residual)
+
+
+def run(steps: List[object], x: torch.Tensor) -> torch.Tensor:
+    for s in steps:
+        if isinstance(s, ConvStep):
+            x = run_conv_step(s, x)
+        elif s.in_op == ops.IN_MAXPOOL2:
+            x = ops.maxpool2x2_ceil(x)
+        else:
+            x = ops.upsample_nearest2x(x)
+    return x
+
+
+class KernelSequential(nn.Sequential):
+    """nn.Sequential whose forward runs the fused rpst conv plan on the GPU.
+
+    Children, indexing and state_dict keys are those of nn.Sequential, so reference
+    checkpoints load unchanged; only the execution differs. CPU inputs raise.
+    """
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:  # noqa: D401
+        return run(compile_layers(self.children()), x)

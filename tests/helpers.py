@@ -1,0 +1,38 @@
+"""Shared test helpers: model construction with synthetic weights, tolerances."""
+import numpy as np
+import torch
+
+# Tolerances; measured fp32-vs-fp64 noise floor of the reference:
+# AdaIN-RP rel-L2 1.8e-6, SANet 4.8e-6.
+TOL_STATS = 1e-5       # stats / AdaIN, rel-L2
+TOL_WCT = 1e-5         # WCT on the fp32 output, rel-L2
+TOL_NET = 1e-4         # full networks in fp32, rel-L2
+TOL_NET_MAXABS = 5e-4  # full networks: max-abs <= TOL_NET_MAXABS * max|ref|
+
+
+def rel_l2(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-300))
+
+
+def max_abs_ratio(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-300))
+
+
+def synth_(model, seed):
+    from rpst import synth
+    synth.synth_module_(model, seed)
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    return np.array(synth.checksum(sd))
+
+
+def state_dict_of(model):
+    return {k: v.detach().cpu() for k, v in model.state_dict().items()}
+
+
+def rp_config(hidden, blocks=5):
+    return {"rp_blocks": blocks, "hidden_dim": hidden, "content_weight": 1.0,
+            "style_weight": 10.0, "resume": False, "use_mask": False}

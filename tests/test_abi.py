@@ -1,0 +1,82 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol the header
+declares, the ctypes table matches the header, and argument validation reports errors
+through status codes + rpst_last_error() without touching the device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from rpst import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rpst.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rpst_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_functions():
+    fns = header_functions()
+    assert "rpst_conv2d" in fns and "rpst_adain" in fns and len(fns) >= 10
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    for name in header_functions():
+        assert hasattr(lib, name), f"{name} declared in rpst.h but not exported"
+
+
+def test_ctypes_table_matches_header():
+    assert sorted(_lib.SIGNATURES) == header_functions()
+
+
+def test_version_and_error_string():
+    lib = _lib.load()
+    assert lib.rpst_version() >= 100
+    assert isinstance(lib.rpst_last_error(), bytes)
+
+
+def test_size_queries_are_host_only():
+    lib = _lib.load()
+    assert lib.rpst_adain_workspace_size(2, 3) == 4 * 4 * 6
+    # 3x3, Cin=3 -> one chunk of 8 channels, Cout=16 padded to 32
+    assert lib.rpst_conv2d_packed_size(16, 3, 3) == 1 * 9 * 8 * 32 * 4
+    assert lib.rpst_conv2d_packed_size(16, 3, 2) == 0
+
+
+@pytest.mark.parametrize("args,msg", [
+    ((None, None, None, None, None, None, 1, 3, 8, 8, 16, 3, 0, 0, 1, None), "null pointer"),
+    ((1, None, 1, None, None, 1, 1, 3, 8, 8, 16, 5, 0, 0, 1, None), "ksize"),
+    ((1, None, 1, None, None, 1, 1, 3, 8, 8, 16, 3, 7, 0, 1, None), "bad pad"),
+    ((1, None, 1, None, None, 1, 1, 3, 1, 8, 16, 3, 1, 0, 1, None), "reflect padding"),
+    ((1, None, 1, None, None, 1, 1, 3, 8, 8, 16, 3, 0, 3, 1, None), "aux"),
+])
+def test_conv2d_argument_errors(args, msg):
+    lib = _lib.load()
+    st = lib.rpst_conv2d(*args)
+    assert st == -1
+    assert msg in lib.rpst_last_error().decode()
+    with pytest.raises(_lib.RpstError, match=msg):
+        _lib.call("rpst_conv2d", *args)
+
+
+def test_adain_workspace_error():
+    lib = _lib.load()
+    st = lib.rpst_adain(1, 1, 1, 2, 3, 16, ctypes.c_float(1e-5), 1, 8, None)
+    assert st == -3
+    assert "workspace" in lib.rpst_last_error().decode()
+
+
+def test_cpu_tensors_raise_no_fallback():
+    import torch
+    import network as net
+    x = torch.rand(1, 4, 8, 8)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        net.calc_mean_std(x)
+    m = net.AdaINRPNet({"rp_blocks": 3, "hidden_dim": 2}, net.vgg)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        m.test(torch.rand(1, 3, 8, 8), torch.rand(1, 3, 8, 8))

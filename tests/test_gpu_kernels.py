@@ -1,0 +1,266 @@
+"""GPU parity: each HIP kernel (through the C ABI) against the CPU oracle and goldens.
+
+Tolerances: stats/AdaIN rel-L2 <= 1e-5; conv (one layer) <= 1e-5;
+networks rel-L2 <= 1e-4 and max-abs <= 5e-4*max|ref|.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import TOL_NET, TOL_NET_MAXABS, TOL_STATS, max_abs_ratio, rel_l2, rp_config, synth_
+from oracle import restate as R
+
+pytestmark = pytest.mark.gpu
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def gen(seed, shape, scale=1.0, offset=0.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(shape, generator=g) * 2 - 1) * scale + offset
+
+
+# ---- a1/a2/a10 ----------------------------------------------------------------------
+def test_calc_mean_std_golden(cuda, golden):
+    from rpst import ops
+    g = golden("stats")
+    for i in range(int(g["n"])):
+        c = t(g[f"c{i}"]).to(cuda)
+        m, s = ops.calc_mean_std(c)
+        assert rel_l2(m, g[f"cmean{i}"]) < 1e-6
+        sd = g[f"cstd{i}"]
+        if np.isnan(sd).any():  # HW == 1 -> NaN like torch.var
+            assert torch.isnan(s).all()
+        else:
+            assert rel_l2(s, sd) < 1e-6
+
+
+def test_adain_golden(cuda, golden):
+    import network as net
+    g = golden("stats")
+    for i in range(int(g["n"])):
+        ref = g[f"adain{i}"]
+        if np.isnan(ref).any():
+            continue
+        out = net.adaptive_instance_normalization(t(g[f"c{i}"]).to(cuda), t(g[f"s{i}"]).to(cuda))
+        assert rel_l2(out, ref) < TOL_STATS, i
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1, 2), (2, 3, 5, 7), (4, 64, 33, 17), (2, 256, 64, 64),
+                                   (1, 8, 512, 512)])
+def test_adain_vs_oracle(cuda, shape):
+    import network as net
+    c = gen(1, shape, 3.0, 1.0)
+    s = gen(2, shape, 0.5, -2.0)
+    out = net.adaptive_instance_normalization(c.to(cuda), s.to(cuda))
+    assert rel_l2(out, R.adain(c, s)) < TOL_STATS
+
+
+def test_adain_large_offset_variance(cuda):
+    """A mean 1e3x the spread: shifted fp64 accumulation keeps the variance exact."""
+    from rpst import ops
+    x = gen(3, (2, 4, 128, 128), 1.0, 1000.0)
+    m, s = ops.calc_mean_std(x.to(cuda))
+    xd = x.double().reshape(2, 4, -1)
+    ref_s = (xd.var(dim=2) + 1e-5).sqrt()
+    assert rel_l2(s.reshape(2, 4), ref_s) < 1e-6
+    assert rel_l2(m.reshape(2, 4), xd.mean(dim=2)) < 1e-7
+
+
+def test_mean_variance_norm(cuda, golden):
+    import network as net
+    g = golden("sanet")
+    for i in range(2):
+        out = net.mean_variance_norm(t(g[f"sa_c{i}"]).to(cuda))
+        assert rel_l2(out, g[f"sa_mvn{i}"]) < TOL_STATS
+
+
+def test_stats_deterministic(cuda):
+    from rpst import ops
+    x = gen(4, (2, 32, 96, 96)).to(cuda)
+    a = ops.calc_mean_std(x)
+    b = ops.calc_mean_std(x)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+# ---- conv kernel ----------------------------------------------------------------------
+def _conv_ref(x, w, b, pad, in_op, relu, aux=None, res=None):
+    import torch.nn.functional as F
+    if in_op == 1:
+        x = F.max_pool2d(x, 2, 2, 0, ceil_mode=True)
+    elif in_op == 2:
+        x = F.interpolate(x, scale_factor=2, mode="nearest")
+    elif in_op == 3:
+        x = x + F.interpolate(aux, scale_factor=2, mode="nearest")
+    k = w.shape[-1]
+    if k == 3:
+        if pad == 1:
+            y = F.conv2d(F.pad(x, (1, 1, 1, 1), mode="reflect"), w, b)
+        else:
+            y = F.conv2d(x, w, b, padding=1)
+    else:
+        y = F.conv2d(x, w, b)
+    if relu:
+        y = F.relu(y)
+    if res is not None:
+        y = y + res
+    return y
+
+
+CONV_CASES = [
+    # (N, Cin, Hs, Ws, Cout, k, pad, in_op, relu)
+    (2, 3, 32, 32, 16, 3, 0, 0, True),      # RP encoder first layer
+    (1, 16, 20, 28, 32, 3, 0, 0, True),     # ragged spatial
+    (2, 32, 17, 40, 64, 3, 0, 0, True),
+    (1, 64, 24, 36, 128, 3, 0, 0, True),
+    (1, 128, 16, 48, 256, 3, 0, 0, True),
+    (1, 256, 16, 16, 128, 3, 0, 0, True),
+    (1, 16, 13, 9, 3, 3, 0, 0, True),       # RP decoder last layer
+    (1, 3, 40, 40, 64, 3, 1, 0, True),      # VGG reflect
+    (1, 64, 40, 40, 128, 3, 1, 1, True),    # VGG pool (even)
+    (1, 64, 21, 19, 128, 3, 1, 1, True),    # VGG pool ceil-mode (odd)
+    (2, 512, 5, 6, 256, 3, 1, 0, True),     # decoder first
+    (1, 256, 5, 6, 256, 3, 1, 2, True),     # decoder upsample
+    (1, 64, 12, 10, 3, 3, 1, 0, False),     # decoder last, no relu
+    (2, 32, 8, 8, 32, 3, 1, 3, False),      # merge conv a + up2(b)
+    (1, 3, 40, 40, 3, 1, 0, 0, False),      # VGG 1x1 pre-conv
+    (2, 64, 5, 7, 64, 1, 0, 0, False),      # SANet 1x1
+    (1, 512, 16, 16, 512, 1, 0, 0, False),
+    (1, 40, 7, 33, 72, 3, 0, 0, True),      # odd channel counts
+    (1, 8, 2, 2, 8, 3, 1, 0, True),         # tiny reflect
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d_vs_torch(cuda, case):
+    from rpst import ops
+    n, cin, hs, ws, cout, k, pad, in_op, relu = case
+    x = gen(10, (n, cin, hs, ws), 1.0, 0.2)
+    w = gen(11, (cout, cin, k, k), (2.0 / (cin * k * k)) ** 0.5)
+    b = gen(12, (cout,), 0.05)
+    aux = gen(13, (n, cin, hs // 2, ws // 2)) if in_op == 3 else None
+    ref = _conv_ref(x.double(), w.double(), b.double(), pad, in_op, relu,
+                    None if aux is None else aux.double())
+    packed = ops.pack_conv_weight(w.to(cuda))
+    out = ops.conv2d(x.to(cuda), packed, b.to(cuda), cout, k, pad=pad, in_op=in_op, relu=relu,
+                     aux=None if aux is None else aux.to(cuda))
+    assert out.shape == ref.shape
+    assert rel_l2(out, ref) < 1e-5, rel_l2(out, ref)
+
+
+def test_conv2d_residual(cuda):
+    from rpst import ops
+    x = gen(20, (2, 64, 9, 11))
+    w = gen(21, (64, 64, 1, 1), 0.1)
+    b = gen(22, (64,), 0.05)
+    r = gen(23, (2, 64, 9, 11))
+    ref = _conv_ref(x.double(), w.double(), b.double(), 0, 0, False, res=r.double())
+    out = ops.conv2d(x.to(cuda), ops.pack_conv_weight(w.to(cuda)), b.to(cuda), 64, 1,
+                     residual=r.to(cuda))
+    assert rel_l2(out, ref) < 1e-5
+
+
+def test_conv2d_deterministic(cuda):
+    from rpst import ops
+    x = gen(30, (2, 128, 32, 64)).to(cuda)
+    w = gen(31, (256, 128, 3, 3), 0.03).to(cuda)
+    p = ops.pack_conv_weight(w)
+    a = ops.conv2d(x, p, None, 256, 3, relu=True)
+    b = ops.conv2d(x, p, None, 256, 3, relu=True)
+    assert torch.equal(a, b)
+
+
+def test_pool_upsample_standalone(cuda):
+    import torch.nn.functional as F
+    from rpst import ops
+    x = gen(40, (2, 5, 9, 14))
+    assert torch.equal(ops.maxpool2x2_ceil(x.to(cuda)).cpu(),
+                       F.max_pool2d(x, 2, 2, 0, ceil_mode=True))
+    assert torch.equal(ops.upsample_nearest2x(x.to(cuda)).cpu(),
+                       F.interpolate(x, scale_factor=2, mode="nearest"))
+
+
+# ---- a3/a4: AdaIN-RP ------------------------------------------------------------------
+def test_adain_rp_test_golden(cuda, golden):
+    import network as net
+    g = golden("adain_rp")
+    for i in range(int(g["n"])):
+        m = net.AdaINRPNet(rp_config(int(g[f"hidden{i}"])), copy.deepcopy(net.vgg))
+        synth_(m, int(g[f"seed{i}"]))
+        m = m.to(cuda)
+        out = m.test(t(g[f"content{i}"]).to(cuda), t(g[f"style{i}"]).to(cuda))
+        ref = g[f"out{i}"]
+        assert rel_l2(out, ref) < TOL_NET, (i, rel_l2(out, ref))
+        assert max_abs_ratio(out, ref) < TOL_NET_MAXABS
+
+
+def test_adain_rp_intermediates_golden(cuda, golden):
+    import network as net
+    g = golden("adain_rp")
+    m = net.AdaINRPNet(rp_config(int(g["hidden0"])), copy.deepcopy(net.vgg))
+    synth_(m, int(g["seed0"]))
+    m = m.to(cuda)
+    with torch.no_grad():
+        cf = m.rp_shared_encoder(t(g["content0"]).to(cuda))
+        sf = m.rp_shared_encoder(t(g["style0"]).to(cuda))
+        fu = net.adaptive_instance_normalization(cf, sf)
+    assert rel_l2(cf, g["enc_c0"]) < 1e-5
+    assert rel_l2(sf, g["enc_s0"]) < 1e-5
+    assert rel_l2(fu, g["fused0"]) < 1e-5
+
+
+def test_adain_rp_forward_losses(cuda, golden):
+    import network as net
+    g = golden("forward")
+    m = net.AdaINRPNet(rp_config(4), copy.deepcopy(net.vgg))
+    synth_(m, 21)
+    m = m.to(cuda)
+    with torch.no_grad():
+        d, tot = m(t(g["content"]).to(cuda), t(g["style"]).to(cuda))
+    for k in ("style_loss", "content_loss", "total_loss"):
+        np.testing.assert_allclose(d[k].item(), g[k], rtol=1e-4)
+
+
+def test_adain_rp_vs_oracle_hidden16(cuda):
+    """Full-width RP net (hidden 16 -> 256 channels) on a 64x96 pair vs the oracle."""
+    import network as net
+    m = net.AdaINRPNet(rp_config(16), copy.deepcopy(net.vgg))
+    synth_(m, 5)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    from rpst import synth
+    c = torch.from_numpy(synth.image(1, (2, 3, 64, 96)))
+    s = torch.from_numpy(synth.image(2, (2, 3, 64, 96)))
+    ref = R.adain_rp_test(c, s, sd, 5)
+    out = m.to(cuda).test(c.to(cuda), s.to(cuda))
+    assert rel_l2(out, ref) < TOL_NET
+    assert max_abs_ratio(out, ref) < TOL_NET_MAXABS
+
+
+def test_grad_enabled_raises(cuda):
+    import network as net
+    m = net.AdaINRPNet(rp_config(2, 3), copy.deepcopy(net.vgg)).to(cuda)
+    x = torch.rand(1, 3, 8, 8, device=cuda)
+    with pytest.raises(NotImplementedError):
+        m(x, x)
+
+
+def test_vgg_and_decoder_golden(cuda, golden):
+    import network as net
+    g = golden("vgg")
+    vgg = copy.deepcopy(net.vgg)
+    synth_(vgg, 80)
+    vgg = vgg.to(cuda)
+    x = t(g["x"]).to(cuda)
+    with torch.no_grad():
+        for i, (lo, hi) in enumerate(R.ENC_SLICES):
+            from rpst.plan import KernelSequential
+            x = KernelSequential(*list(vgg.children())[lo:hi])(x)
+            assert rel_l2(x, g[f"relu{i + 1}_1"]) < 1e-5, i
+        dec = copy.deepcopy(net.decoder)
+        synth_(dec, 81)
+        out = dec.to(cuda)(t(g["z"]).to(cuda))
+    assert rel_l2(out, g["dec_out"]) < 1e-5

@@ -1,0 +1,147 @@
+"""Pin the CPU oracle (oracle/restate.py) to golden vectors produced by the reference.
+
+The goldens come from running the reference's own network/ package in the build
+container (tests/golden/gen_golden.py). Weights are regenerated here by rpst.synth and
+checked against the checksum recorded at generation time, so a generator drift fails
+loudly instead of silently comparing different models.
+"""
+import copy
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import rel_l2, rp_config, state_dict_of, synth_
+from oracle import restate as R
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def test_stats_bitwise(golden):
+    g = golden("stats")
+    for i in range(int(g["n"])):
+        c, s = t(g[f"c{i}"]), t(g[f"s{i}"])
+        m, sd = R.calc_mean_std(c)
+        np.testing.assert_array_equal(m.numpy(), g[f"cmean{i}"])
+        np.testing.assert_array_equal(sd.numpy(), g[f"cstd{i}"])
+        np.testing.assert_array_equal(R.adain(c, s).numpy(), g[f"adain{i}"])
+
+
+def _adain_model(hidden):
+    import network as net
+    return net.AdaINRPNet(rp_config(hidden), copy.deepcopy(net.vgg))
+
+
+def test_adain_rp_test(golden):
+    g = golden("adain_rp")
+    for i in range(int(g["n"])):
+        m = _adain_model(int(g[f"hidden{i}"]))
+        ck = synth_(m, int(g[f"seed{i}"]))
+        np.testing.assert_allclose(ck, g[f"checksum{i}"], rtol=1e-12)
+        sd = state_dict_of(m)
+        out = R.adain_rp_test(t(g[f"content{i}"]), t(g[f"style{i}"]), sd, 5)
+        assert rel_l2(out, g[f"out{i}"]) < 1e-6, i
+
+
+def test_adain_rp_forward_losses(golden):
+    g = golden("forward")
+    m = _adain_model(4)
+    np.testing.assert_allclose(synth_(m, 21), g["checksum"], rtol=1e-12)
+    sd = state_dict_of(m)
+    d = R.adain_rp_forward(t(g["content"]), t(g["style"]), sd, 5, 1.0, 10.0)
+    for k in ("style_loss", "content_loss", "total_loss"):
+        np.testing.assert_allclose(d[k].numpy(), g[k], rtol=1e-5)
+    feats = R.encode_with_intermediate(t(g["content"]), sd)
+    for i, f in enumerate(feats):
+        assert rel_l2(f, g[f"relu{i + 1}_1"]) < 1e-6
+
+
+def test_vgg_and_decoder(golden):
+    import network as net
+    g = golden("vgg")
+    vgg = copy.deepcopy(net.vgg)
+    np.testing.assert_allclose(synth_(vgg, 80), g["vgg_ck"], rtol=1e-12)
+    sd = state_dict_of(vgg)
+    x = t(g["x"])
+    for i, (lo, hi) in enumerate(R.ENC_SLICES):
+        x = R.vgg_slice(x, sd, "", lo, hi)
+        assert rel_l2(x, g[f"relu{i + 1}_1"]) < 1e-6
+    dec = copy.deepcopy(net.decoder)
+    np.testing.assert_allclose(synth_(dec, 81), g["dec_ck"], rtol=1e-12)
+    out = R.decoder(t(g["z"]), state_dict_of(dec), "")
+    assert rel_l2(out, g["dec_out"]) < 1e-6
+
+
+def test_wct_matrix_functions(golden):
+    g = golden("wct")
+    for i in range(int(g["nmat"])):
+        a = t(g[f"A{i}"])
+        assert rel_l2(R.matrix_sqrt(a), g[f"sqrt{i}"]) < 1e-12
+        assert rel_l2(R.matrix_inv_sqrt(a), g[f"isqrt{i}"]) < 1e-12
+
+
+def test_wct_whiten_and_color(golden):
+    g = golden("wct")
+    for i in range(int(g["ncase"])):
+        out = R.whiten_and_color(t(g[f"cF{i}"]), t(g[f"sF{i}"]))
+        assert rel_l2(out, g[f"wc{i}"]) < 1e-12
+
+
+def test_wct_rp_test(golden):
+    import network as net
+    g = golden("wct")
+    for i in range(int(g["nnet"])):
+        m = net.WCTRPNet(rp_config(int(g[f"net_hidden{i}"])), copy.deepcopy(net.vgg))
+        np.testing.assert_allclose(synth_(m, int(g[f"net_seed{i}"])), g[f"net_checksum{i}"],
+                                   rtol=1e-12)
+        out = R.wct_rp_test(t(g[f"net_content{i}"]), t(g[f"net_style{i}"]), state_dict_of(m), 5)
+        assert rel_l2(out, g[f"net_out{i}"]) < 1e-6
+
+
+def test_sanet_module_and_transform(golden):
+    import network as net
+    g = golden("sanet")
+    for i in range(2):
+        c = t(g[f"sa_c{i}"])
+        mod = net.SANet(c.shape[1])
+        np.testing.assert_allclose(synth_(mod, int(g[f"sa_seed{i}"])), g[f"sa_ck{i}"], rtol=1e-12)
+        out = R.sanet(c, t(g[f"sa_s{i}"]), state_dict_of(mod), "")
+        assert rel_l2(out, g[f"sa_out{i}"]) < 1e-6
+        np.testing.assert_array_equal(R.mean_variance_norm(c).numpy(), g[f"sa_mvn{i}"])
+    tr = net.Transform(32)
+    np.testing.assert_allclose(synth_(tr, 60), g["tr_ck"], rtol=1e-12)
+    out = R.transform(t(g["tr_c4"]), t(g["tr_s4"]), t(g["tr_c5"]), t(g["tr_s5"]),
+                      state_dict_of(tr), "")
+    assert rel_l2(out, g["tr_out"]) < 1e-6
+
+
+def test_samodel_test(golden):
+    import network as net
+    g = golden("sanet")
+    for i in range(2):
+        c = t(g[f"model_content{i}"])
+        m = net.SAModel({}, copy.deepcopy(net.vgg), 0, c.shape[-1])
+        np.testing.assert_allclose(synth_(m, int(g[f"model_seed{i}"])), g[f"model_ck{i}"],
+                                   rtol=1e-12)
+        out = R.samodel_test(c, t(g[f"model_style{i}"]), state_dict_of(m))
+        assert rel_l2(out, g[f"model_out{i}"]) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["AdaINRPNet", "WCTRPNet", "SAModel", "vgg", "decoder"])
+def test_state_dict_keys_match_reference(name):
+    """Checkpoint compatibility: same keys and shapes as the reference modules."""
+    import network as net
+    ref = json.load(open(os.path.join(GOLD, "keys.json")))[name]
+    vgg = copy.deepcopy(net.vgg)
+    mine = {"AdaINRPNet": lambda: net.AdaINRPNet(rp_config(16), vgg),
+            "WCTRPNet": lambda: net.WCTRPNet(rp_config(16), vgg),
+            "SAModel": lambda: net.SAModel({}, vgg, 0, 512),
+            "vgg": lambda: net.vgg, "decoder": lambda: net.decoder}[name]()
+    got = [[k, list(v.shape)] for k, v in mine.state_dict().items()]
+    assert got == ref
