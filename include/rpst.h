@@ -99,6 +99,40 @@ int rpst_maxpool2x2_ceil(const float* in, float* out, int N, int C, int H, int W
 int rpst_upsample_nearest2x(const float* in, float* out, int N, int C, int H, int W,
                             rpst_stream_t stream);
 
+/* ---- a11: SANet attention core  network/sanet.py:86-94 ------------------------------
+ * O[b] = H[b] softmax_rows(F[b]^T G[b])^T  for F, G, H, O of shape (B, C, HW):
+ *   S = F^T G (HW x HW, no 1/sqrt(C) scale), row softmax over keys, O = H S^T.
+ * The 1x1 convs f/g/h/out_conv and mean_variance_norm run through rpst_conv2d /
+ * rpst_mean_variance_norm. Workspace: rpst_sanet_attention_workspace_size(B, HW)
+ * (S is materialised: B*HW*HW floats). */
+size_t rpst_sanet_attention_workspace_size(int B, int HW);
+int rpst_sanet_attention(const float* F, const float* G, const float* H, float* O, int B,
+                         int C, int HW, void* workspace, size_t workspace_bytes,
+                         rpst_stream_t stream);
+
+/* ---- a7: matrix_sqrt / matrix_inv_sqrt  network/wct_rp.py:7-40 ----------------------
+ * out[b] = (A[b] + 1e-4 I)^(+1/2) (inverse = 0) or ^(-1/2) (inverse = 1) for symmetric PSD
+ * fp64 n x n matrices, batch of `batch`. Coupled Newton-Schulz (fixed 40 steps); equal to
+ * the reference's SVD form because its truncation (< 1e-5) cannot trigger after +1e-4.
+ * Workspace: rpst_matrix_power_workspace_size(n, batch). */
+size_t rpst_matrix_power_workspace_size(int n, int batch);
+int rpst_matrix_power_psd_f64(const double* A, double* out, int n, int batch, int inverse,
+                              void* workspace, size_t workspace_bytes, rpst_stream_t stream);
+
+/* ---- a8: WCTRPNet.whiten_and_color(cF, sF, 'closed-form')  network/wct_rp.py:82-114 ---
+ * cF, sF, out: (C, HW) fp64. out = T (cF - mu_c) + mu_s with the closed-form T.
+ * Workspace: rpst_wct_workspace_size(1, C, HW). */
+size_t rpst_wct_workspace_size(int n, int C, int64_t HW);
+int rpst_whiten_and_color_f64(const double* cF, const double* sF, double* out, int C,
+                              int64_t HW, void* workspace, size_t workspace_bytes,
+                              rpst_stream_t stream);
+
+/* ---- a9: WCTRPNet.fuse(content_feats, style_feats)  network/wct_rp.py:157-166 --------
+ * content, style, out: (n, C, HW) fp32. Per image: widen to fp64, whiten_and_color, round
+ * to fp32 — all n images in one set of launches. Workspace: rpst_wct_workspace_size(n,C,HW). */
+int rpst_wct_fuse(const float* content, const float* style, float* out, int n, int C,
+                  int64_t HW, void* workspace, size_t workspace_bytes, rpst_stream_t stream);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

@@ -35,6 +35,13 @@ SIGNATURES = {
     "rpst_conv2d": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_maxpool2x2_ceil": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "rpst_upsample_nearest2x": (_I, [_P, _P, _I, _I, _I, _I, _P]),
+    "rpst_sanet_attention_workspace_size": (_SZ, [_I, _I]),
+    "rpst_sanet_attention": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
+    "rpst_matrix_power_workspace_size": (_SZ, [_I, _I]),
+    "rpst_matrix_power_psd_f64": (_I, [_P, _P, _I, _I, _I, _P, _SZ, _P]),
+    "rpst_wct_workspace_size": (_SZ, [_I, _I, _I64]),
+    "rpst_whiten_and_color_f64": (_I, [_P, _P, _P, _I, _I64, _P, _SZ, _P]),
+    "rpst_wct_fuse": (_I, [_P, _P, _P, _I, _I, _I64, _P, _SZ, _P]),
 }
 
 _lib = None

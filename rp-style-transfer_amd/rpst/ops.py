@@ -59,7 +59,7 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def _check(*ts: torch.Tensor) -> None:
+def _check(*ts: torch.Tensor, dtype=torch.float32) -> None:
     dev = None
     for t in ts:
         if t is None:
@@ -68,8 +68,8 @@ def _check(*ts: torch.Tensor) -> None:
             raise RuntimeError(
                 "rpst kernels run on a ROCm GPU only; got a CPU tensor (the CPU reference "
                 "path is oracle/, which is test infrastructure, not a fallback)")
-        if t.dtype != torch.float32:
-            raise RuntimeError(f"rpst kernels take float32 tensors, got {t.dtype}")
+        if t.dtype != dtype:
+            raise RuntimeError(f"rpst kernel expects {dtype} tensors, got {t.dtype}")
         if dev is None:
             dev = t.device
         elif t.device != dev:
@@ -201,4 +201,76 @@ def upsample_nearest2x(x: torch.Tensor) -> torch.Tensor:
     n, c, h, w = x.shape
     out = torch.empty((n, c, 2 * h, 2 * w), device=x.device, dtype=x.dtype)
     _lib.call("rpst_upsample_nearest2x", x.data_ptr(), out.data_ptr(), n, c, h, w, _stream(x))
+    return out
+
+
+# Cap on the materialised attention matrix per launch; larger batches are chunked.
+SANET_WS_CAP = 8 << 30
+
+
+def sanet_attention(F: torch.Tensor, G: torch.Tensor, H: torch.Tensor) -> torch.Tensor:
+    """SANet core (sanet.py:86-94): O = H softmax(F^T G)^T per image, (B,C,h,w)."""
+    assert F.dim() == 4 and F.shape == G.shape == H.shape
+    _check(F, G, H)
+    F, G, H = _c(F), _c(G), _c(H)
+    B, C, h, w = F.shape
+    hw = h * w
+    out = torch.empty_like(F)
+    lib = _lib.load()
+    per_img = lib.rpst_sanet_attention_workspace_size(1, hw)
+    chunk = max(1, min(B, SANET_WS_CAP // max(per_img, 1)))
+    ws_bytes = lib.rpst_sanet_attention_workspace_size(chunk, hw)
+    ws = torch.empty(ws_bytes, device=F.device, dtype=torch.uint8)
+    for b0 in range(0, B, chunk):
+        nb = min(chunk, B - b0)
+        with _traced(f"sanet_attention C{C} HW{hw} N{nb}", 4.0 * nb * hw * hw * C, 0.0):
+            _lib.call("rpst_sanet_attention", F[b0].data_ptr(), G[b0].data_ptr(),
+                      H[b0].data_ptr(), out[b0].data_ptr(), nb, C, hw, ws.data_ptr(), ws_bytes,
+                      _stream(F))
+    return out
+
+
+def matrix_power_psd(A: torch.Tensor, p: float) -> torch.Tensor:
+    """(A + 1e-4 I)^p, p = +-1/2, for symmetric PSD fp64 (n,n) or (b,n,n) matrices
+    (wct_rp.py:7-40)."""
+    assert p in (0.5, -0.5)
+    _check(A, dtype=torch.float64)
+    A = _c(A)
+    n = A.shape[-1]
+    assert A.shape[-2] == n
+    batch = A.numel() // (n * n)
+    out = torch.empty_like(A)
+    nbytes = _lib.load().rpst_matrix_power_workspace_size(n, batch)
+    ws = torch.empty(nbytes, device=A.device, dtype=torch.uint8)
+    _lib.call("rpst_matrix_power_psd_f64", A.data_ptr(), out.data_ptr(), n, batch,
+              int(p < 0), ws.data_ptr(), nbytes, _stream(A))
+    return out
+
+
+def whiten_and_color(cF: torch.Tensor, sF: torch.Tensor) -> torch.Tensor:
+    """WCTRPNet.whiten_and_color closed-form (wct_rp.py:82-114): (C,HW) fp64 -> fp64."""
+    assert cF.dim() == 2 and cF.shape == sF.shape
+    _check(cF, sF, dtype=torch.float64)
+    cF, sF = _c(cF), _c(sF)
+    C, hw = cF.shape
+    out = torch.empty_like(cF)
+    nbytes = _lib.load().rpst_wct_workspace_size(1, C, hw)
+    ws = torch.empty(nbytes, device=cF.device, dtype=torch.uint8)
+    _lib.call("rpst_whiten_and_color_f64", cF.data_ptr(), sF.data_ptr(), out.data_ptr(), C, hw,
+              ws.data_ptr(), nbytes, _stream(cF))
+    return out
+
+
+def wct_fuse(content: torch.Tensor, style: torch.Tensor) -> torch.Tensor:
+    """WCTRPNet.fuse (wct_rp.py:157-166): (n,C,h,w) fp32 -> fp32, fp64 internals."""
+    assert content.dim() == 4 and content.shape == style.shape
+    _check(content, style)
+    content, style = _c(content), _c(style)
+    n, C, h, w = content.shape
+    out = torch.empty_like(content)
+    nbytes = _lib.load().rpst_wct_workspace_size(n, C, h * w)
+    ws = torch.empty(nbytes, device=content.device, dtype=torch.uint8)
+    with _traced(f"wct_fuse C{C} {h * w}px N{n}", 6.0 * n * C * C * h * w, 0.0):
+        _lib.call("rpst_wct_fuse", content.data_ptr(), style.data_ptr(), out.data_ptr(), n, C,
+                  h * w, ws.data_ptr(), nbytes, _stream(content))
     return out

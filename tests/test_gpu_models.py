@@ -1,0 +1,159 @@
+"""GPU parity for the SANet and WCT paths (kernels through the C ABI) against goldens
+produced by the reference and against the CPU oracle at larger sizes."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import (TOL_NET, TOL_NET_MAXABS, TOL_WCT, max_abs_ratio, rel_l2, rp_config,
+                     state_dict_of, synth_)
+from oracle import restate as R
+
+pytestmark = pytest.mark.gpu
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def gen(seed, shape, scale=1.0, offset=0.0, relu=False):
+    g = torch.Generator().manual_seed(seed)
+    x = (torch.rand(shape, generator=g) * 2 - 1) * scale + offset
+    return x.clamp_min(0) if relu else x
+
+
+# ---- a11/a12/a13: SANet ----------------------------------------------------------------
+def test_sanet_module_golden(cuda, golden):
+    import network as net
+    g = golden("sanet")
+    for i in range(2):
+        c = t(g[f"sa_c{i}"])
+        mod = net.SANet(c.shape[1])
+        synth_(mod, int(g[f"sa_seed{i}"]))
+        with torch.no_grad():
+            out = mod.to(cuda)(c.to(cuda), t(g[f"sa_s{i}"]).to(cuda))
+        assert rel_l2(out, g[f"sa_out{i}"]) < 1e-5, i
+
+
+def test_transform_golden(cuda, golden):
+    import network as net
+    g = golden("sanet")
+    tr = net.Transform(32)
+    synth_(tr, 60)
+    tr = tr.to(cuda)
+    with torch.no_grad():
+        out = tr(*(t(g[k]).to(cuda) for k in ("tr_c4", "tr_s4", "tr_c5", "tr_s5")))
+    assert rel_l2(out, g["tr_out"]) < 1e-5
+
+
+def test_samodel_test_golden(cuda, golden):
+    import network as net
+    g = golden("sanet")
+    for i in range(2):
+        c = t(g[f"model_content{i}"])
+        m = net.SAModel({}, copy.deepcopy(net.vgg), 0, c.shape[-1])
+        synth_(m, int(g[f"model_seed{i}"]))
+        out = m.to(cuda).test(c.to(cuda), t(g[f"model_style{i}"]).to(cuda))
+        ref = g[f"model_out{i}"]
+        assert rel_l2(out, ref) < TOL_NET, (i, rel_l2(out, ref))
+        assert max_abs_ratio(out, ref) < TOL_NET_MAXABS
+
+
+@pytest.mark.parametrize("shape", [(1, 512, 64, 64), (2, 512, 32, 32), (3, 48, 7, 9)])
+def test_sanet_attention_vs_oracle(cuda, shape):
+    """Attention core at the relu4_1 size of a 512x512 image (HW = 4096)."""
+    import network as net
+    mod = net.SANet(shape[1])
+    synth_(mod, 3)
+    sd = state_dict_of(mod)
+    c = gen(1, shape, 2.0, 0.5, relu=True)
+    s = gen(2, shape, 2.0, 0.5, relu=True)
+    ref = R.sanet(c, s, sd, "")
+    with torch.no_grad():
+        out = mod.to(cuda)(c.to(cuda), s.to(cuda))
+    assert rel_l2(out, ref) < 1e-5
+
+
+def test_sanet_attention_large_logits(cuda):
+    """Logits in the hundreds: exercises the max subtraction of the softmax."""
+    from rpst import ops
+    B, C, h, w = 1, 64, 16, 16
+    F = gen(5, (B, C, h, w), 3.0)
+    G = gen(6, (B, C, h, w), 3.0)
+    H = gen(7, (B, C, h, w), 1.0)
+    S = torch.bmm(F.view(B, C, -1).permute(0, 2, 1).double(), G.view(B, C, -1).double())
+    assert S.abs().max() > 100
+    ref = torch.bmm(H.view(B, C, -1).double(), torch.softmax(S, -1).permute(0, 2, 1)).view(B, C, h, w)
+    out = ops.sanet_attention(F.to(cuda), G.to(cuda), H.to(cuda))
+    assert rel_l2(out, ref) < 1e-5
+
+
+def test_samodel_vs_oracle_64(cuda):
+    import network as net
+    from rpst import synth
+    m = net.SAModel({}, copy.deepcopy(net.vgg), 0, 64)
+    synth_(m, 4)
+    sd = state_dict_of(m)
+    c = torch.from_numpy(synth.image(3, (2, 3, 64, 64)))
+    s = torch.from_numpy(synth.image(4, (2, 3, 64, 64)))
+    ref = R.samodel_test(c, s, sd)
+    out = m.to(cuda).test(c.to(cuda), s.to(cuda))
+    assert rel_l2(out, ref) < TOL_NET
+
+
+# ---- a7/a8/a9: WCT -----------------------------------------------------------------------
+def test_matrix_sqrt_golden(cuda, golden):
+    import network as net
+    g = golden("wct")
+    for i in range(int(g["nmat"])):
+        a = t(g[f"A{i}"]).to(cuda)
+        assert rel_l2(net.matrix_sqrt(a), g[f"sqrt{i}"]) < 1e-10, i
+        assert rel_l2(net.matrix_inv_sqrt(a), g[f"isqrt{i}"]) < 1e-10, i
+
+
+def test_whiten_and_color_golden(cuda, golden):
+    import network as net
+    g = golden("wct")
+    m = net.WCTRPNet(rp_config(2), copy.deepcopy(net.vgg))
+    for i in range(int(g["ncase"])):
+        out = m.whiten_and_color(t(g[f"cF{i}"]).to(cuda), t(g[f"sF{i}"]).to(cuda))
+        assert out.dtype == torch.float64
+        assert rel_l2(out, g[f"wc{i}"]) < 1e-10, (i, rel_l2(out, g[f"wc{i}"]))
+
+
+def test_wct_rp_test_golden(cuda, golden):
+    import network as net
+    g = golden("wct")
+    for i in range(int(g["nnet"])):
+        m = net.WCTRPNet(rp_config(int(g[f"net_hidden{i}"])), copy.deepcopy(net.vgg))
+        synth_(m, int(g[f"net_seed{i}"]))
+        out = m.to(cuda).test(t(g[f"net_content{i}"]).to(cuda), t(g[f"net_style{i}"]).to(cuda))
+        ref = g[f"net_out{i}"]
+        assert rel_l2(out, ref) < TOL_NET, (i, rel_l2(out, ref))
+
+
+@pytest.mark.parametrize("shape", [(2, 256, 64, 64), (1, 64, 33, 31), (3, 16, 5, 7)])
+def test_wct_fuse_vs_oracle(cuda, shape):
+    """fp64 WCT over fp32 features at the RP encoder width (C = 256)."""
+    from rpst import ops
+    c = gen(11, shape, 2.0, 0.3, relu=True)
+    s = gen(12, shape, 1.5, 0.5, relu=True)
+    s[:, 3] = 0.0  # a dead style channel: singular style covariance
+    ref = R.wct_fuse(c, s)
+    out = ops.wct_fuse(c.to(cuda), s.to(cuda))
+    assert rel_l2(out, ref) < TOL_WCT, rel_l2(out, ref)
+
+
+def test_wct_rp_vs_oracle_hidden16(cuda):
+    import network as net
+    from rpst import synth
+    m = net.WCTRPNet(rp_config(16), copy.deepcopy(net.vgg))
+    synth_(m, 6)
+    sd = state_dict_of(m)
+    c = torch.from_numpy(synth.image(5, (2, 3, 48, 64)))
+    s = torch.from_numpy(synth.image(6, (2, 3, 48, 64)))
+    ref = R.wct_rp_test(c, s, sd, 5)
+    out = m.to(cuda).test(c.to(cuda), s.to(cuda))
+    assert rel_l2(out, ref) < TOL_NET
+    assert max_abs_ratio(out, ref) < TOL_NET_MAXABS
