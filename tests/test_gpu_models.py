@@ -157,3 +157,19 @@ def test_wct_rp_vs_oracle_hidden16(cuda):
     out = m.to(cuda).test(c.to(cuda), s.to(cuda))
     assert rel_l2(out, ref) < TOL_NET
     assert max_abs_ratio(out, ref) < TOL_NET_MAXABS
+
+
+def test_sharded_model_bit_identical(cuda):
+    """Per-image split over 2 replicas (both on cuda:0 here; one per GPU on a node) must
+    reproduce the single-replica output bit for bit: every kernel is deterministic and
+    no kernel mixes images."""
+    import network as net
+    from rpst import synth
+    from rpst.shard import ShardedModel
+    m = net.AdaINRPNet(rp_config(4), copy.deepcopy(net.vgg))
+    synth_(m, 8)
+    c = torch.from_numpy(synth.image(7, (5, 3, 32, 32)))
+    s = torch.from_numpy(synth.image(8, (5, 3, 32, 32)))
+    ref = m.to(cuda).test(c.to(cuda), s.to(cuda)).cpu()
+    out = ShardedModel(m, [cuda, cuda])(c, s)
+    assert torch.equal(out, ref)
