@@ -26,6 +26,8 @@
 // Numerics: exact fp32 products, fp32 accumulation (MFMA = k-ordered fmaf chain).
 #include "rpst_common.h"
 
+#include <cstdlib>
+
 namespace rpst {
 
 constexpr int kConvThreads = 256;
@@ -64,31 +66,46 @@ __device__ __forceinline__ bool resolve(int& v, int n, int pad, bool padded) {
   return true;
 }
 
-// Input value at resolved logical (y, x) of one channel plane, applying the fused op.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// Byte offset the buffer unit treats as out of range (returns 0, no fault): every
+// descriptor below has num_records < 2^31.
+constexpr unsigned kOOB = 0x80000000u;
+
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+
+// One patch element: logical (post-in_op) resolved row yr / column xr of the plane whose
+// byte offset (within the image) is `pbyte`. ok == false -> zero (pad position).
 template <int INOP>
-__device__ __forceinline__ float fetch(const float* __restrict__ p,
-                                       const float* __restrict__ q, int y, int x,
+__device__ __forceinline__ float fetch(__amdgpu_buffer_rsrc_t rin, __amdgpu_buffer_rsrc_t raux,
+                                       unsigned pbyte, unsigned abyte, int yr, int xr, bool ok,
                                        const ConvArgs& a) {
   if (INOP == RPST_IN_MAXPOOL2) {
-    const int sy = 2 * y, sx = 2 * x;
-    const bool xr = sx + 1 < a.Ws, yd = sy + 1 < a.Hs;
-    const float* r0 = p + (int64_t)sy * a.Ws + sx;
-    float v = r0[0];
-    if (xr) v = fmaxf(v, r0[1]);
-    if (yd) v = fmaxf(v, r0[a.Ws]);
-    if (xr && yd) v = fmaxf(v, r0[a.Ws + 1]);
-    return v;
+    const int sy = 2 * yr, sx = 2 * xr;
+    const unsigned o = pbyte + (unsigned)(sy * a.Ws + sx) * 4u;
+    const bool xr1 = sx + 1 < a.Ws, yd = sy + 1 < a.Hs;
+    const float v00 = bload(rin, ok ? o : kOOB);
+    const float v01 = bload(rin, ok ? o + 4u : kOOB);
+    const float v10 = bload(rin, ok ? o + 4u * a.Ws : kOOB);
+    const float v11 = bload(rin, ok ? o + 4u * a.Ws + 4u : kOOB);
+    float v = fmaxf(v00, xr1 ? v01 : v00);
+    v = fmaxf(v, yd ? v10 : v00);
+    v = fmaxf(v, (xr1 && yd) ? v11 : v00);
+    return ok ? v : 0.f;
   } else if (INOP == RPST_IN_UPSAMPLE2) {
-    return p[(int64_t)(y >> 1) * a.Ws + (x >> 1)];
+    return bload(rin, ok ? pbyte + (unsigned)((yr >> 1) * a.Ws + (xr >> 1)) * 4u : kOOB);
   } else if (INOP == RPST_IN_ADD_UPSAMPLE2) {
-    return p[(int64_t)y * a.W + x] + q[(int64_t)(y >> 1) * (a.W >> 1) + (x >> 1)];
+    const float v = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
+    const float u = bload(raux, ok ? abyte + (unsigned)((yr >> 1) * (a.W >> 1) + (xr >> 1)) * 4u : kOOB);
+    return v + u;
   } else {
-    return p[(int64_t)y * a.W + x];
+    return bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
   }
 }
 
-template <int KS, int BM, int TH, int WM, int WN, int INOP>
-__global__ __launch_bounds__(kConvThreads, 2) void conv_mfma_kernel(ConvArgs a) {
+template <int KS, int BM, int TH, int WM, int WN, int INOP, int NTH>
+__global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
   using K = ConvK<KS>;
   constexpr int CK = K::CK, TAPS = K::TAPS, KCH = K::KCH;
   constexpr int OFF = (KS == 3) ? 1 : 0;
@@ -96,12 +113,21 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_mfma_kernel(ConvArgs a) 
   constexpr int WTM = BM / WM;       // co per wave
   constexpr int MT = WTM / 32;       // 32-row M sub-tiles per wave
   constexpr int NT = TH / WN;        // rows (32-px N sub-tiles) per wave
-  static_assert(WM * WN == kConvThreads / kWave, "4 waves");
+  static_assert(WM * WN == NTH / kWave, "one wave per sub-tile");
   static_assert(MT >= 1 && NT >= 1 && (CK % 8) == 0, "tile");
   constexpr int NW4 = KCH * BM / 4;  // float4 weight loads per chunk
-  constexpr int WLD = (NW4 + kConvThreads - 1) / kConvThreads;
-  constexpr int CPT = CK / 8;        // patch channels per thread (8 channel groups)
-  constexpr int HALO = (KS == 3) ? (2 * PH + 31) / 32 : 0;  // halo loads per lane
+  constexpr int WLD = (NW4 + NTH - 1) / NTH;
+  constexpr bool WFULL = (NW4 % NTH) == 0;
+  // patch loader: NTH/32 groups of 32 lanes; a group owns CPT channels and 1/RS of
+  // their rows (RS > 1 when there are more groups than channels in a chunk)
+  constexpr int GROUPS = NTH / 32;
+  constexpr int CPT = CK > GROUPS ? CK / GROUPS : 1;
+  constexpr int RS = GROUPS > CK ? GROUPS / CK : 1;
+  constexpr int CGS = GROUPS / RS;                 // distinct channel groups
+  constexpr int RPT = (PH + RS - 1) / RS;          // rows per thread
+  constexpr int HALO = (KS == 3) ? (2 * PH + 32 * RS - 1) / (32 * RS) : 0;  // halo loads per lane
+  constexpr int XN = RPT + HALO;
+  static_assert(CPT * CGS == CK, "channel split");
 
   __shared__ float Ws[KCH * BM];
   __shared__ float Xs[CK * PH * PW];
@@ -123,17 +149,33 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_mfma_kernel(ConvArgs a) 
   const int wm = wave / WN, wn = wave % WN;
   const int h = lane >> 5, j = lane & 31;
 
-  // patch loader geometry: thread -> (channel group cg, column jc); rows are uniform
-  const int cg = tid >> 5, jc = tid & 31;
-  int bx = x0 + jc;  // body column (logical)
+  // ---- buffer descriptors (wave-uniform) -------------------------------------------
+  const bool pooled = (INOP == RPST_IN_MAXPOOL2 || INOP == RPST_IN_UPSAMPLE2);
+  const unsigned in_plane = pooled ? (unsigned)(a.Hs * a.Ws) : (unsigned)(a.H * a.W);
+  const unsigned aux_plane = (unsigned)((a.H >> 1) * (a.W >> 1));
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.in + (int64_t)n * a.Cin * in_plane), (short)0, (int)(a.Cin * in_plane * 4u),
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t raux = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(INOP == RPST_IN_ADD_UPSAMPLE2 ? a.aux + (int64_t)n * a.Cin * aux_plane : a.in),
+      (short)0, (int)(a.Cin * aux_plane * 4u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.wpk + co0), (short)0, 0x7fffffff, 0x00020000);
+
+  // weights: thread -> row tid/(BM/4) (+ u*NTH/(BM/4)), float4 column tid%(BM/4)
+  const unsigned w_voff = ((unsigned)(tid / (BM / 4)) * a.Cout_pad + (tid % (BM / 4)) * 4) * 4u;
+  const unsigned w_ustride = (unsigned)(NTH / (BM / 4)) * a.Cout_pad * 4u;
+  const unsigned w_cstride = (unsigned)KCH * a.Cout_pad * 4u;
+
+  // patch: thread -> (channel group cg, row slice rs, column jc); row math is uniform
+  const int cg = (tid >> 5) % CGS, rs = (tid >> 5) / CGS, jc = tid & 31;
+  int bx = x0 + jc;
   const bool bx_ok = resolve(bx, a.W, a.pad, KS == 3);
-  // halo element e of this lane: hi = jc + 32e < 2*PH covers patch column 0 / PW-1 of
-  // row hi>>1
-  int hy[HALO > 0 ? HALO : 1], hx[HALO > 0 ? HALO : 1];
+  int hy[HALO > 0 ? HALO : 1], hx[HALO > 0 ? HALO : 1];  // (HALO == 0: unused)
   bool h_ok[HALO > 0 ? HALO : 1], has_halo[HALO > 0 ? HALO : 1];
 #pragma unroll
   for (int e = 0; e < HALO; ++e) {
-    const int hi = jc + 32 * e;
+    const int hi = jc + 32 * (rs + RS * e);
     has_halo[e] = hi < 2 * PH;
     hy[e] = y0 - OFF + (hi >> 1);
     hx[e] = (hi & 1) ? x0 + kTW : x0 - 1;
@@ -141,10 +183,6 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_mfma_kernel(ConvArgs a) 
     const bool ok2 = resolve(hx[e], a.W, a.pad, true);
     h_ok[e] = has_halo[e] && ok1 && ok2;
   }
-  const int64_t in_plane = (INOP == RPST_IN_MAXPOOL2 || INOP == RPST_IN_UPSAMPLE2)
-                               ? (int64_t)a.Hs * a.Ws
-                               : (int64_t)a.H * a.W;
-  const int64_t aux_plane = (int64_t)(a.H >> 1) * (a.W >> 1);
 
   floatx16 acc[MT][NT];
 #pragma unroll
@@ -154,65 +192,56 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_mfma_kernel(ConvArgs a) 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
 
-  float4 wreg[WLD];
-  float xreg[CPT][PH + HALO];
+  u32x4 wreg[WLD];
+  float xreg[CPT][XN];
 
-  auto load_chunk = [&](int c) {
-    const float4* wsrc = reinterpret_cast<const float4*>(
-        a.wpk + (int64_t)c * KCH * a.Cout_pad + co0);
-#pragma unroll
-    for (int u = 0; u < WLD; ++u) {
-      const int i = tid + u * kConvThreads;
-      if (i < NW4) {
-        const int row = i / (BM / 4), col4 = i % (BM / 4);
-        wreg[u] = wsrc[(int64_t)row * (a.Cout_pad / 4) + col4];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-      const int ci = c * CK + cg + 8 * q;
-      const bool cok = ci < a.Cin;
-      const int64_t pl = (int64_t)n * a.Cin + ci;
-      const float* p = a.in + pl * in_plane;
-      const float* qa = a.aux + pl * aux_plane;
-#pragma unroll
-      for (int py = 0; py < PH; ++py) {
-        int y = y0 - OFF + py;
-        const bool yok = resolve(y, a.H, a.pad, KS == 3);
-        xreg[q][py] = (cok && yok && bx_ok) ? fetch<INOP>(p, qa, y, bx, a) : 0.f;
-      }
-#pragma unroll
-      for (int e = 0; e < HALO; ++e)
-        xreg[q][PH + e] = (cok && h_ok[e]) ? fetch<INOP>(p, qa, hy[e], hx[e], a) : 0.f;
-    }
-  };
-  auto store_chunk = [&]() {
-#pragma unroll
-    for (int u = 0; u < WLD; ++u) {
-      const int i = tid + u * kConvThreads;
-      if (i < NW4) reinterpret_cast<float4*>(Ws)[i] = wreg[u];
-    }
-#pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-      float* xs = Xs + (cg + 8 * q) * PH * PW;
-#pragma unroll
-      for (int py = 0; py < PH; ++py) xs[py * PW + jc + OFF] = xreg[q][py];
-#pragma unroll
-      for (int e = 0; e < HALO; ++e) {
-        const int hi = jc + 32 * e;
-        if (has_halo[e]) xs[(hi >> 1) * PW + ((hi & 1) ? PW - 1 : 0)] = xreg[q][PH + e];
-      }
-    }
-  };
+#define RPST_CONV_LOAD(c)                                                                   \
+  {                                                                                         \
+    const unsigned wc = (unsigned)(c) * w_cstride;                                          \
+    _Pragma("unroll") for (int u = 0; u < WLD; ++u) {                                       \
+      const bool wv = WFULL || tid + u * NTH < NW4;                                         \
+      wreg[u] = __builtin_amdgcn_raw_buffer_load_b128(                                      \
+          rw, (int)(wv ? w_voff + wc + u * w_ustride : kOOB), 0, 0);                        \
+    }                                                                                       \
+    _Pragma("unroll") for (int q = 0; q < CPT; ++q) {                                       \
+      const unsigned ch = (unsigned)((c) * CK + cg + CGS * q);                              \
+      const unsigned pb = ch * in_plane * 4u, ab = ch * aux_plane * 4u;                     \
+      _Pragma("unroll") for (int i = 0; i < RPT; ++i) {                                     \
+        const int py = rs * RPT + i;                                                        \
+        int y = y0 - OFF + py;                                                              \
+        const bool yok = resolve(y, a.H, a.pad, KS == 3) && py < PH;                        \
+        xreg[q][i] = fetch<INOP>(rin, raux, pb, ab, y, bx, yok && bx_ok, a);                \
+      }                                                                                     \
+      _Pragma("unroll") for (int e = 0; e < HALO; ++e) xreg[q][RPT + e] =                   \
+          fetch<INOP>(rin, raux, pb, ab, hy[e], hx[e], h_ok[e], a);                         \
+    }                                                                                       \
+  }
 
   const int aoff = h * BM + wm * WTM + j;
   const int boff = h * PH * PW + (wn * NT) * PW + j;
 
-  load_chunk(0);
+  RPST_CONV_LOAD(0)
   for (int c = 0; c < a.nchunks; ++c) {
-    store_chunk();
+#pragma unroll
+    for (int u = 0; u < WLD; ++u)
+      if (WFULL || tid + u * NTH < NW4)
+        *reinterpret_cast<u32x4*>(Ws + 4 * (tid + u * NTH)) = wreg[u];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      float* xs = Xs + (cg + CGS * q) * PH * PW;
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int py = rs * RPT + i;
+        if ((PH % RS) == 0 || py < PH) xs[py * PW + jc + OFF] = xreg[q][i];
+      }
+#pragma unroll
+      for (int e = 0; e < HALO; ++e) {
+        const int hi = jc + 32 * (rs + RS * e);
+        if (has_halo[e]) xs[(hi >> 1) * PW + ((hi & 1) ? PW - 1 : 0)] = xreg[q][RPT + e];
+      }
+    }
     __syncthreads();
-    if (c + 1 < a.nchunks) load_chunk(c + 1);
+    if (c + 1 < a.nchunks) RPST_CONV_LOAD(c + 1)
 #pragma unroll
     for (int t = 0; t < TAPS; ++t) {
       const int kh = t / KS, kw = t % KS;
@@ -234,6 +263,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv_mfma_kernel(ConvArgs a) 
     }
     __syncthreads();
   }
+#undef RPST_CONV_LOAD
 
   // epilogue: bias, ReLU, residual, predicated coalesced stores (128 B per half-wave)
   const int x = x0 + j;
@@ -296,15 +326,46 @@ static int pad_cout(int Cout) {
 
 static int ck_of(int ksize) { return ksize == 3 ? ConvK<3>::CK : ConvK<1>::CK; }
 
+// Tile variants per BM (selected by RPST_CONV_VARIANT for tuning; index 0 = default).
+// <BM, TH, WM, WN, NTH>: block tile BM x (TH x 32 px), WM x WN waves of NTH/64.
 template <int KS, int INOP>
-static void launch_conv(const ConvArgs& a, int BM, hipStream_t st) {
+static void launch_conv(const ConvArgs& a, int BM, int variant, hipStream_t st) {
   const int blocks = a.tiles_x * a.tiles_y * a.N * a.co_tiles;
-  if (BM == 128)
-    conv_mfma_kernel<KS, 128, 8, 2, 2, INOP><<<blocks, kConvThreads, 0, st>>>(a);
-  else if (BM == 64)
-    conv_mfma_kernel<KS, 64, 8, 2, 2, INOP><<<blocks, kConvThreads, 0, st>>>(a);
-  else
-    conv_mfma_kernel<KS, 32, 16, 1, 4, INOP><<<blocks, kConvThreads, 0, st>>>(a);
+#define RPST_LAUNCH(BM_, TH_, WM_, WN_, NTH_) \
+  conv_mfma_kernel<KS, BM_, TH_, WM_, WN_, INOP, NTH_><<<blocks, NTH_, 0, st>>>(a)
+  if (BM == 128) {
+    switch (variant) {
+      case 1: RPST_LAUNCH(128, 8, 2, 2, 256); break;
+      case 2: RPST_LAUNCH(128, 4, 2, 2, 256); break;
+      case 3: RPST_LAUNCH(128, 16, 2, 4, 512); break;
+      default: RPST_LAUNCH(128, 8, 2, 4, 512);
+    }
+  } else if (BM == 64) {
+    switch (variant) {
+      case 1: RPST_LAUNCH(64, 16, 1, 8, 512); break;
+      case 2: RPST_LAUNCH(64, 8, 1, 8, 512); break;
+      default: RPST_LAUNCH(64, 8, 1, 4, 256);
+    }
+  } else {
+    switch (variant) {
+      case 1: RPST_LAUNCH(32, 16, 1, 8, 512); break;
+      case 2: RPST_LAUNCH(32, 8, 1, 4, 256); break;
+      default: RPST_LAUNCH(32, 16, 1, 4, 256);
+    }
+  }
+#undef RPST_LAUNCH
+}
+
+// TH of a variant (the host needs it for the grid)
+static int variant_th(int BM, int variant) {
+  if (BM == 128) return variant == 2 ? 4 : (variant == 3 ? 16 : 8);
+  if (BM == 64) return variant == 1 ? 16 : 8;
+  return variant == 2 ? 8 : 16;
+}
+
+static int conv_variant() {
+  const char* e = getenv("RPST_CONV_VARIANT");
+  return e ? atoi(e) : 0;
 }
 
 }  // namespace rpst
@@ -376,28 +437,34 @@ extern "C" int rpst_conv2d(const float* input, const float* aux, const float* pa
   if (ksize == 3 && pad_mode == RPST_PAD_REFLECT)
     RPST_REQUIRE(a.H >= 2 && a.W >= 2, "conv2d: reflect padding needs H,W >= 2");
   const TileCfg cfg = pick_cfg(Cout);
+  const int variant = conv_variant();
+  const int th = variant_th(cfg.BM, variant);
   const int ck = ck_of(ksize);
   a.Cout_pad = pad_cout(Cout);
   a.nchunks = (Cin + ck - 1) / ck;
   a.tiles_x = (a.W + kTW - 1) / kTW;
-  a.tiles_y = (a.H + cfg.TH - 1) / cfg.TH;
+  a.tiles_y = (a.H + th - 1) / th;
   a.co_tiles = a.Cout_pad / cfg.BM;
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * N * a.co_tiles;
   RPST_REQUIRE(blocks <= 0x7fffffffLL, "conv2d: grid too large");
   RPST_REQUIRE((int64_t)N * (Cout > Cin ? Cout : Cin) * a.H * a.W < (1LL << 40),
                "conv2d: tensor too large");
+  // per-image input (plus one chunk of channel padding) must be addressable by a 31-bit
+  // buffer offset
+  RPST_REQUIRE(((int64_t)Cin + 16) * Hs * Ws * 4 < (1LL << 31),
+               "conv2d: one image's input exceeds 2 GiB");
   hipStream_t st = as_stream(stream);
   if (ksize == 1) {
     RPST_REQUIRE(in_op == RPST_IN_NONE, "conv2d: 1x1 conv supports in_op NONE only");
-    launch_conv<1, RPST_IN_NONE>(a, cfg.BM, st);
+    launch_conv<1, RPST_IN_NONE>(a, cfg.BM, variant, st);
   } else if (in_op == RPST_IN_MAXPOOL2) {
-    launch_conv<3, RPST_IN_MAXPOOL2>(a, cfg.BM, st);
+    launch_conv<3, RPST_IN_MAXPOOL2>(a, cfg.BM, variant, st);
   } else if (in_op == RPST_IN_UPSAMPLE2) {
-    launch_conv<3, RPST_IN_UPSAMPLE2>(a, cfg.BM, st);
+    launch_conv<3, RPST_IN_UPSAMPLE2>(a, cfg.BM, variant, st);
   } else if (in_op == RPST_IN_ADD_UPSAMPLE2) {
-    launch_conv<3, RPST_IN_ADD_UPSAMPLE2>(a, cfg.BM, st);
+    launch_conv<3, RPST_IN_ADD_UPSAMPLE2>(a, cfg.BM, variant, st);
   } else {
-    launch_conv<3, RPST_IN_NONE>(a, cfg.BM, st);
+    launch_conv<3, RPST_IN_NONE>(a, cfg.BM, variant, st);
   }
   return launch_status("conv_mfma_kernel");
 }

@@ -1,0 +1,88 @@
+"""Conv tile-variant micro-benchmark (interleaved rounds in one process).
+
+For each conv layer shape of the benchmark workloads, times every tile variant of
+rpst_conv2d (RPST_CONV_VARIANT) with HIP events on the launch stream, checks that all
+variants produce bit-identical output (same per-output K order), and prints TF/s.
+
+    python tools/bench_conv.py [--layers adain|vgg|all] [--rounds 3]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rp-style-transfer_amd"))
+import torch  # noqa: E402
+
+from rpst import ops  # noqa: E402
+
+ADAIN = [  # (N, Cin, Hs, Ws, Cout, k, pad, in_op)
+    (64, 3, 512, 512, 16, 3, 0, 0), (64, 16, 512, 512, 32, 3, 0, 0),
+    (64, 32, 512, 512, 64, 3, 0, 0), (64, 64, 512, 512, 128, 3, 0, 0),
+    (64, 128, 512, 512, 256, 3, 0, 0), (32, 256, 512, 512, 128, 3, 0, 0),
+    (32, 128, 512, 512, 64, 3, 0, 0), (32, 64, 512, 512, 32, 3, 0, 0),
+    (32, 32, 512, 512, 16, 3, 0, 0), (32, 16, 512, 512, 3, 3, 0, 0),
+]
+VGG = [
+    (64, 64, 512, 512, 64, 3, 1, 0), (64, 64, 512, 512, 128, 3, 1, 1),
+    (64, 128, 256, 256, 128, 3, 1, 0), (64, 128, 256, 256, 256, 3, 1, 1),
+    (64, 256, 128, 128, 256, 3, 1, 0), (64, 256, 128, 128, 512, 3, 1, 1),
+    (64, 512, 64, 64, 512, 3, 1, 0), (32, 512, 64, 64, 512, 1, 0, 0),
+]
+VARIANTS = {128: [0, 1, 2, 3], 64: [0, 1, 2], 32: [0, 1, 2]}
+
+
+def bm_of(cout):
+    return 128 if cout > 64 else (64 if cout > 32 else 32)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", default="all")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    layers = {"adain": ADAIN, "vgg": VGG, "all": ADAIN + VGG}[args.layers]
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    results = []
+    for (n, cin, hs, ws, cout, k, pad, in_op) in layers:
+        x = torch.rand((n, cin, hs, ws), device=dev, generator=g)
+        w = (torch.rand((cout, cin, k, k), device=dev, generator=g) - 0.5) * 0.1
+        b = torch.rand((cout,), device=dev, generator=g) * 0.1
+        p = ops.pack_conv_weight(w)
+        h, wd = ops.conv_out_hw(hs, ws, in_op)
+        flops = 2.0 * n * cout * h * wd * cin * k * k
+        times = {v: [] for v in VARIANTS[bm_of(cout)]}
+        ref = None
+        for rnd in range(args.rounds):
+            for v in times:
+                os.environ["RPST_CONV_VARIANT"] = str(v)
+                out = ops.conv2d(x, p, b, cout, k, pad=pad, in_op=in_op, relu=True)
+                if ref is None:
+                    ref = out.clone()
+                elif rnd == 0:
+                    assert torch.equal(out, ref), f"variant {v} differs"
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.reps):
+                    ops.conv2d(x, p, b, cout, k, pad=pad, in_op=in_op, relu=True, out=out)
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) / args.reps)
+        os.environ.pop("RPST_CONV_VARIANT", None)
+        row = {"layer": f"{cin}->{cout} k{k} {h}x{wd} N{n} pad{pad} op{in_op}"}
+        for v, ts in times.items():
+            ms = min(ts)
+            row[f"v{v}_ms"] = round(ms, 3)
+            row[f"v{v}_tf"] = round(flops / ms / 1e9, 1)
+        results.append(row)
+        print(json.dumps(row), flush=True)
+        del x, w, p, ref
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
