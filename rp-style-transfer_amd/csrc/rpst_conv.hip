@@ -104,17 +104,21 @@ __device__ __forceinline__ float fetch(__amdgpu_buffer_rsrc_t rin, __amdgpu_buff
   }
 }
 
-template <int KS, int BM, int TH, int WM, int WN, int INOP, int NTH>
+// CKK = input channels per kernel chunk (divides the packing chunk K::CK);
+// DB = double-buffered LDS (one barrier per chunk instead of two).
+template <int KS, int BM, int TH, int WM, int WN, int INOP, int NTH, int CKK, bool DB>
 __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
   using K = ConvK<KS>;
-  constexpr int CK = K::CK, TAPS = K::TAPS, KCH = K::KCH;
+  constexpr int PCK = K::CK, TAPS = K::TAPS;
+  constexpr int CK = CKK, KCH = TAPS * CK;
+  static_assert(PCK % CK == 0, "kernel chunk must divide the packing chunk");
   constexpr int OFF = (KS == 3) ? 1 : 0;
   constexpr int PH = TH + KS - 1, PW = kTW + KS - 1;
   constexpr int WTM = BM / WM;       // co per wave
   constexpr int MT = WTM / 32;       // 32-row M sub-tiles per wave
   constexpr int NT = TH / WN;        // rows (32-px N sub-tiles) per wave
   static_assert(WM * WN == NTH / kWave, "one wave per sub-tile");
-  static_assert(MT >= 1 && NT >= 1 && (CK % 8) == 0, "tile");
+  static_assert(MT >= 1 && NT >= 1 && (CK % 2) == 0, "tile");
   constexpr int NW4 = KCH * BM / 4;  // float4 weight loads per chunk
   constexpr int WLD = (NW4 + NTH - 1) / NTH;
   constexpr bool WFULL = (NW4 % NTH) == 0;
@@ -129,8 +133,9 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
   constexpr int XN = RPT + HALO;
   static_assert(CPT * CGS == CK, "channel split");
 
-  __shared__ float Ws[KCH * BM];
-  __shared__ float Xs[CK * PH * PW];
+  constexpr int NBUF = DB ? 2 : 1;
+  __shared__ float Wsb[NBUF][KCH * BM];
+  __shared__ float Xsb[NBUF][CK * PH * PW];
 
   // block -> (co tile, image, tile row, tile col); co tile slowest so resident blocks
   // share one weight slice in L2
@@ -162,10 +167,26 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.wpk + co0), (short)0, 0x7fffffff, 0x00020000);
 
-  // weights: thread -> row tid/(BM/4) (+ u*NTH/(BM/4)), float4 column tid%(BM/4)
-  const unsigned w_voff = ((unsigned)(tid / (BM / 4)) * a.Cout_pad + (tid % (BM / 4)) * 4) * 4u;
-  const unsigned w_ustride = (unsigned)(NTH / (BM / 4)) * a.Cout_pad * 4u;
-  const unsigned w_cstride = (unsigned)KCH * a.Cout_pad * 4u;
+  // weights: thread -> kernel row r = tid/(BM/4) + u*NTH/(BM/4) = (tap, cl), float4
+  // column tid%(BM/4). Packed row of (tap, channel c*CK+cl) = pchunk*TAPS*PCK + tap*PCK + ci%PCK.
+  // When the per-u row step RU is a multiple of CK the packed row is linear in u.
+  constexpr int RU = NTH / (BM / 4);
+  constexpr bool WLIN = (RU % CK) == 0;
+  unsigned w_voff[WLIN ? 1 : WLD];
+  unsigned w_ustride = 0;
+  {
+    const int r0 = tid / (BM / 4);
+    if (WLIN) {
+      w_voff[0] = ((unsigned)((r0 / CK) * PCK + r0 % CK) * a.Cout_pad + (tid % (BM / 4)) * 4) * 4u;
+      w_ustride = (unsigned)(RU / CK) * PCK * a.Cout_pad * 4u;
+    } else {
+#pragma unroll
+      for (int u = 0; u < (WLIN ? 1 : WLD); ++u) {
+        const int r = r0 + u * RU;
+        w_voff[u] = ((unsigned)((r / CK) * PCK + r % CK) * a.Cout_pad + (tid % (BM / 4)) * 4) * 4u;
+      }
+    }
+  }
 
   // patch: thread -> (channel group cg, row slice rs, column jc); row math is uniform
   const int cg = (tid >> 5) % CGS, rs = (tid >> 5) / CGS, jc = tid & 31;
@@ -197,11 +218,13 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
 
 #define RPST_CONV_LOAD(c)                                                                   \
   {                                                                                         \
-    const unsigned wc = (unsigned)(c) * w_cstride;                                          \
+    const unsigned c0 = (unsigned)(c) * CK;                                                 \
+    const unsigned wc = ((c0 / PCK) * TAPS * PCK + c0 % PCK) * a.Cout_pad * 4u;            \
     _Pragma("unroll") for (int u = 0; u < WLD; ++u) {                                       \
       const bool wv = WFULL || tid + u * NTH < NW4;                                         \
       wreg[u] = __builtin_amdgcn_raw_buffer_load_b128(                                      \
-          rw, (int)(wv ? w_voff + wc + u * w_ustride : kOOB), 0, 0);                        \
+          rw, (int)(wv ? (WLIN ? w_voff[0] + u * w_ustride : w_voff[WLIN ? 0 : u]) + wc    \
+                       : kOOB), 0, 0);                                                      \
     }                                                                                       \
     _Pragma("unroll") for (int q = 0; q < CPT; ++q) {                                       \
       const unsigned ch = (unsigned)((c) * CK + cg + CGS * q);                              \
@@ -221,7 +244,10 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
   const int boff = h * PH * PW + (wn * NT) * PW + j;
 
   RPST_CONV_LOAD(0)
-  for (int c = 0; c < a.nchunks; ++c) {
+  const int nchunks = (a.Cin + CK - 1) / CK;
+  for (int c = 0; c < nchunks; ++c) {
+    float* Ws = Wsb[DB ? (c & 1) : 0];
+    float* Xs = Xsb[DB ? (c & 1) : 0];
 #pragma unroll
     for (int u = 0; u < WLD; ++u)
       if (WFULL || tid + u * NTH < NW4)
@@ -241,7 +267,7 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
       }
     }
     __syncthreads();
-    if (c + 1 < a.nchunks) RPST_CONV_LOAD(c + 1)
+    if (c + 1 < nchunks) RPST_CONV_LOAD(c + 1)
 #pragma unroll
     for (int t = 0; t < TAPS; ++t) {
       const int kh = t / KS, kw = t % KS;
@@ -261,7 +287,7 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
                                                                0, 0, 0);
       }
     }
-    __syncthreads();
+    if (!DB) __syncthreads();  // double-buffered: the next chunk's barrier suffices
   }
 #undef RPST_CONV_LOAD
 
@@ -326,46 +352,57 @@ static int pad_cout(int Cout) {
 
 static int ck_of(int ksize) { return ksize == 3 ? ConvK<3>::CK : ConvK<1>::CK; }
 
-// Tile variants per BM (selected by RPST_CONV_VARIANT for tuning; index 0 = default).
-// <BM, TH, WM, WN, NTH>: block tile BM x (TH x 32 px), WM x WN waves of NTH/64.
+// Tile variants per BM. RPST_CONV_VARIANT (tools/bench_conv.py) forces one for tuning;
+// otherwise pick_variant() chooses from the measured table (profiles/r01_bench_conv.log):
+//   BM=128: 3x3 -> v1 (128 co x 8x32 px, 8 accumulators/wave, 134-143 TF/s);
+//           max-pool input or 1x1 -> v2 (128 x 4x32, lighter loader, 113-128 TF/s);
+//   BM=64 / BM=32 -> v1 (4-channel chunks, double-buffered LDS, 1 barrier per chunk).
+// <BM, TH, WM, WN, NTH, CK, DB>: block tile BM x (TH x 32 px), WM x WN waves of NTH/64.
 template <int KS, int INOP>
 static void launch_conv(const ConvArgs& a, int BM, int variant, hipStream_t st) {
   const int blocks = a.tiles_x * a.tiles_y * a.N * a.co_tiles;
-#define RPST_LAUNCH(BM_, TH_, WM_, WN_, NTH_) \
-  conv_mfma_kernel<KS, BM_, TH_, WM_, WN_, INOP, NTH_><<<blocks, NTH_, 0, st>>>(a)
+#define RPST_LAUNCH(BM_, TH_, WM_, WN_, NTH_, CK_, DB_) \
+  conv_mfma_kernel<KS, BM_, TH_, WM_, WN_, INOP, NTH_, CK_, DB_><<<blocks, NTH_, 0, st>>>(a)
+  constexpr int C8 = ConvK<KS>::CK, C4 = ConvK<KS>::CK / 2;
   if (BM == 128) {
     switch (variant) {
-      case 1: RPST_LAUNCH(128, 8, 2, 2, 256); break;
-      case 2: RPST_LAUNCH(128, 4, 2, 2, 256); break;
-      case 3: RPST_LAUNCH(128, 16, 2, 4, 512); break;
-      default: RPST_LAUNCH(128, 8, 2, 4, 512);
+      case 0: RPST_LAUNCH(128, 8, 2, 4, 512, C8, false); break;
+      case 2: RPST_LAUNCH(128, 4, 2, 2, 256, C8, false); break;
+      case 3: RPST_LAUNCH(128, 8, 2, 2, 256, C4, true); break;
+      case 4: RPST_LAUNCH(128, 4, 2, 2, 256, C4, true); break;
+      default: RPST_LAUNCH(128, 8, 2, 2, 256, C8, false);
     }
   } else if (BM == 64) {
     switch (variant) {
-      case 1: RPST_LAUNCH(64, 16, 1, 8, 512); break;
-      case 2: RPST_LAUNCH(64, 8, 1, 8, 512); break;
-      default: RPST_LAUNCH(64, 8, 1, 4, 256);
+      case 0: RPST_LAUNCH(64, 8, 1, 4, 256, C8, false); break;
+      case 2: RPST_LAUNCH(64, 8, 1, 8, 512, C8, false); break;
+      default: RPST_LAUNCH(64, 8, 1, 4, 256, C4, true);
     }
   } else {
     switch (variant) {
-      case 1: RPST_LAUNCH(32, 16, 1, 8, 512); break;
-      case 2: RPST_LAUNCH(32, 8, 1, 4, 256); break;
-      default: RPST_LAUNCH(32, 16, 1, 4, 256);
+      case 0: RPST_LAUNCH(32, 16, 1, 4, 256, C8, false); break;
+      case 2: RPST_LAUNCH(32, 8, 1, 4, 256, C8, false); break;
+      default: RPST_LAUNCH(32, 8, 1, 4, 256, C4, true);
     }
   }
 #undef RPST_LAUNCH
 }
 
-// TH of a variant (the host needs it for the grid)
-static int variant_th(int BM, int variant) {
-  if (BM == 128) return variant == 2 ? 4 : (variant == 3 ? 16 : 8);
-  if (BM == 64) return variant == 1 ? 16 : 8;
-  return variant == 2 ? 8 : 16;
+static int pick_variant(int BM, int ksize, int in_op) {
+  if (BM == 128 && (in_op == RPST_IN_MAXPOOL2 || ksize == 1)) return 2;
+  return 1;
 }
 
-static int conv_variant() {
+// TH of a variant (the host needs it for the grid)
+static int variant_th(int BM, int variant) {
+  if (BM == 128) return (variant == 2 || variant == 4) ? 4 : 8;
+  if (BM == 64) return 8;
+  return variant == 0 ? 16 : 8;
+}
+
+static int conv_variant(int BM, int ksize, int in_op) {
   const char* e = getenv("RPST_CONV_VARIANT");
-  return e ? atoi(e) : 0;
+  return (e && *e) ? atoi(e) : pick_variant(BM, ksize, in_op);
 }
 
 }  // namespace rpst
@@ -437,7 +474,7 @@ extern "C" int rpst_conv2d(const float* input, const float* aux, const float* pa
   if (ksize == 3 && pad_mode == RPST_PAD_REFLECT)
     RPST_REQUIRE(a.H >= 2 && a.W >= 2, "conv2d: reflect padding needs H,W >= 2");
   const TileCfg cfg = pick_cfg(Cout);
-  const int variant = conv_variant();
+  const int variant = conv_variant(cfg.BM, ksize, in_op);
   const int th = variant_th(cfg.BM, variant);
   const int ck = ck_of(ksize);
   a.Cout_pad = pad_cout(Cout);

@@ -19,6 +19,8 @@
 // staged k-major in LDS with a 16-double pad (conflict-free ds_read_b64 halves).
 #include "rpst_common.h"
 
+#include <cstdlib>
+
 namespace rpst {
 
 enum { SRC_F64 = 0, SRC_F64C = 1, SRC_F32C = 2 };  // plain fp64 / centered fp64 / centered fp32
@@ -41,13 +43,56 @@ struct G64Args {
   int tiles_n;
 };
 
-template <int SRC>
-__device__ __forceinline__ double ld_src(const void* p, int64_t i) {
-  if (SRC == SRC_F32C) return (double)static_cast<const float*>(p)[i];
-  return static_cast<const double*>(p)[i];
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+constexpr unsigned kOOB = 0x80000000u;  // out-of-range buffer offset: loads return 0
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-template <int BT, int SRCA, int SRCB, int BLAY, int OUT>
+// Load N consecutive elements (contiguous dim) starting at element index e of a SRC-typed
+// buffer, widened to fp64. VEC: 16-B loads whose validity is all-or-nothing (host checks
+// the alignment of sizes / leading dims); else one load per element. ok(i) -> element i
+// is inside the logical operand; invalid elements read 0 (buffer out-of-range).
+template <int SRC, int N, bool VEC, typename OK>
+__device__ __forceinline__ void load_run(double (&v)[N], __amdgpu_buffer_rsrc_t r, unsigned e,
+                                         OK ok) {
+  if (SRC == SRC_F32C) {
+    if (VEC) {
+#pragma unroll
+      for (int q = 0; q < N / 4; ++q) {
+        const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(
+            r, (int)(ok(4 * q) ? (e + 4 * q) * 4u : kOOB), 0, 0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[4 * q + t] = (double)__uint_as_float(w[t]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        v[i] = (double)__uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(r, (int)(ok(i) ? (e + i) * 4u : kOOB), 0, 0));
+    }
+  } else {
+    if (VEC) {
+#pragma unroll
+      for (int q = 0; q < N / 2; ++q) {
+        const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(
+            r, (int)(ok(2 * q) ? (e + 2 * q) * 8u : kOOB), 0, 0);
+        v[2 * q] = __hiloint2double((int)w[1], (int)w[0]);
+        v[2 * q + 1] = __hiloint2double((int)w[3], (int)w[2]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(ok(i) ? (e + i) * 8u : kOOB), 0, 0);
+        v[i] = __hiloint2double((int)w[1], (int)w[0]);
+      }
+    }
+  }
+}
+
+template <int BT, int SRCA, int SRCB, int BLAY, int OUT, bool VEC>
 __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
   constexpr int BK = 16, LD = BT + 16, WT = BT / 2, MT = WT / 16;
   constexpr int EPT = BT * BK / 256;  // elements staged per thread per operand
@@ -71,14 +116,19 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
   const int z = blockIdx.z;
   const int b = z / g.ksplit, split = z - b * g.ksplit;
   const int m0 = ti * BT, n0 = tj * BT;
-  const int64_t kper = ((int64_t)g.K + g.ksplit - 1) / g.ksplit;
-  const int64_t kbeg = split * kper;
-  const int64_t kend = min((int64_t)g.K, kbeg + kper);
+  // split-K ranges are whole BK tiles
+  const int kper = ((g.K + g.ksplit - 1) / g.ksplit + BK - 1) / BK * BK;
+  const int kbeg = split * kper;
+  const int kend = min(g.K, kbeg + kper);
 
-  const char* A = static_cast<const char*>(g.A) + b * g.sA * (SRCA == SRC_F32C ? 4 : 8);
-  const char* B = static_cast<const char*>(g.B) + b * g.sB * (SRCB == SRC_F32C ? 4 : 8);
-  const double* amean = g.amean ? g.amean + b * g.sMean : nullptr;
-  const double* bmean = g.bmean ? g.bmean + b * g.sMean : nullptr;
+  constexpr unsigned ESA = SRCA == SRC_F32C ? 4u : 8u, ESB = SRCB == SRC_F32C ? 4u : 8u;
+  const char* Ab = static_cast<const char*>(g.A) + (int64_t)b * g.sA * ESA;
+  const char* Bb = static_cast<const char*>(g.B) + (int64_t)b * g.sB * ESB;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(Ab, (unsigned)g.M * g.lda * ESA);
+  const __amdgpu_buffer_rsrc_t rb =
+      rsrc(Bb, BLAY == B_NK ? (unsigned)g.N * g.ldb * ESB : (unsigned)g.K * g.ldb * ESB);
+  const double* amean = g.amean ? g.amean + (int64_t)b * g.sMean : nullptr;
+  const double* bmean = g.bmean ? g.bmean + (int64_t)b * g.sMean : nullptr;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -90,56 +140,61 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
 #pragma unroll
     for (int jn = 0; jn < MT; ++jn) acc[i][jn] = doublex4{0.0, 0.0, 0.0, 0.0};
 
-  // row-major [r][k] staging: thread -> (row r = tid / TPR, k-run of EPT)
+  // row-major [r][k] staging: thread -> (row sr = tid / TPR, k-run sk .. sk+EPT)
   constexpr int TPR = BK / EPT;
   const int sr = tid / TPR, sk = (tid % TPR) * EPT;
-  // [k][n] staging: thread -> (k = tid / (BT/EPT), n-run of EPT)
+  // [k][n] staging: thread -> (k = kk_, n-run sn .. sn+EPT)
   constexpr int TPK = BT / EPT;
   const int kk_ = tid / TPK, sn = (tid % TPK) * EPT;
 
   const int am = m0 + sr;
-  const double amu = (SRCA != SRC_F64 && am < g.M) ? amean[am] : 0.0;
+  const bool am_ok = am < g.M;
+  const double amu = (SRCA != SRC_F64 && am_ok) ? amean[am] : 0.0;
   const int bn = n0 + sr;  // B_NK row
-  const double bmu_nk = (BLAY == B_NK && SRCB != SRC_F64 && bn < g.N) ? bmean[bn] : 0.0;
+  const bool bn_ok = bn < g.N;
+  const double bmu_nk = (BLAY == B_NK && SRCB != SRC_F64 && bn_ok) ? bmean[bn] : 0.0;
 
-  double ra[EPT], rb[EPT];
-  auto load = [&](int64_t k0) {
+  double ra_[EPT], rb_[EPT];
+  auto load = [&](int k0) {
+    {
+      const int k = k0 + sk;
+      load_run<SRCA, EPT, VEC>(ra_, ra, (unsigned)(am * g.lda + k),
+                               [&](int i) { return am_ok && k + i < kend; });
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      const int64_t k = k0 + sk + e;
-      ra[e] = (am < g.M && k < kend) ? ld_src<SRCA>(A, (int64_t)am * g.lda + k) - amu : 0.0;
+      for (int i = 0; i < EPT; ++i) ra_[i] = (am_ok && k + i < kend) ? ra_[i] - amu : 0.0;
     }
     if (BLAY == B_NK) {
+      const int k = k0 + sk;
+      load_run<SRCB, EPT, VEC>(rb_, rb, (unsigned)(bn * g.ldb + k),
+                               [&](int i) { return bn_ok && k + i < kend; });
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) {
-        const int64_t k = k0 + sk + e;
-        rb[e] = (bn < g.N && k < kend) ? ld_src<SRCB>(B, (int64_t)bn * g.ldb + k) - bmu_nk : 0.0;
-      }
+      for (int i = 0; i < EPT; ++i) rb_[i] = (bn_ok && k + i < kend) ? rb_[i] - bmu_nk : 0.0;
     } else {
-      const int64_t k = k0 + kk_;
-      const double mu = (SRCB != SRC_F64 && k < kend) ? bmean[k] : 0.0;
+      const int k = k0 + kk_;
+      const bool kok = k < kend;
+      const double mu = (SRCB != SRC_F64 && kok) ? bmean[k] : 0.0;
+      const int n = n0 + sn;
+      load_run<SRCB, EPT, VEC>(rb_, rb, (unsigned)(k * g.ldb + n),
+                               [&](int i) { return kok && n + i < g.N; });
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) {
-        const int n = n0 + sn + e;
-        rb[e] = (n < g.N && k < kend) ? ld_src<SRCB>(B, k * g.ldb + n) - mu : 0.0;
-      }
+      for (int i = 0; i < EPT; ++i) rb_[i] = (kok && n + i < g.N) ? rb_[i] - mu : 0.0;
     }
   };
   auto store = [&]() {
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) As[(sk + e) * LD + sr] = ra[e];
+    for (int e = 0; e < EPT; ++e) As[(sk + e) * LD + sr] = ra_[e];
     if (BLAY == B_NK) {
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) Bs[(sk + e) * LD + sr] = rb[e];
+      for (int e = 0; e < EPT; ++e) Bs[(sk + e) * LD + sr] = rb_[e];
     } else {
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) Bs[kk_ * LD + sn + e] = rb[e];
+      for (int e = 0; e < EPT; ++e) Bs[kk_ * LD + sn + e] = rb_[e];
     }
   };
 
-  const int64_t ktiles = (kend - kbeg + BK - 1) / BK;
+  const int ktiles = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   if (ktiles > 0) load(kbeg);
-  for (int64_t kt = 0; kt < ktiles; ++kt) {
+  for (int kt = 0; kt < ktiles; ++kt) {
     store();
     __syncthreads();
     if (kt + 1 < ktiles) load(kbeg + (kt + 1) * BK);
@@ -196,7 +251,26 @@ __global__ __launch_bounds__(256) void rowmean_kernel(const T* __restrict__ x0,
   const int r = blockIdx.x;
   const T* x = (r < rows0 ? x0 + (int64_t)r * L : x1 + (int64_t)(r - rows0) * L);
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < L; i += 256) s += (double)x[i];
+  constexpr int V = 16 / sizeof(T);
+  if ((L % V) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const int64_t nv = L / V;
+    int64_t i = threadIdx.x;
+    for (; i + 256 < nv; i += 512) {  // two 16-B loads in flight per lane
+      T a[V], c[V];
+      *reinterpret_cast<u32x4*>(a) = reinterpret_cast<const u32x4*>(x)[i];
+      *reinterpret_cast<u32x4*>(c) = reinterpret_cast<const u32x4*>(x)[i + 256];
+#pragma unroll
+      for (int t = 0; t < V; ++t) s += (double)a[t] + (double)c[t];
+    }
+    for (; i < nv; i += 256) {
+      T a[V];
+      *reinterpret_cast<u32x4*>(a) = reinterpret_cast<const u32x4*>(x)[i];
+#pragma unroll
+      for (int t = 0; t < V; ++t) s += (double)a[t];
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < L; i += 256) s += (double)x[i];
+  }
   s = wave_sum(s);
   __shared__ double red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -265,7 +339,18 @@ __global__ void scale_pow_kernel(const double* __restrict__ in, double* __restri
 // ---- host-side pipeline ------------------------------------------------------------
 template <int BT, int SRCA, int SRCB, int BLAY, int OUT>
 static void gemm64(const G64Args& g, dim3 grid, hipStream_t st) {
-  gemm_f64_kernel<BT, SRCA, SRCB, BLAY, OUT><<<grid, 256, 0, st>>>(g);
+  // 16-B loads need every contiguous run to start on a 16-B boundary: sizes and leading
+  // dims in whole vectors (4 floats / 2 doubles), split-K ranges are whole BK tiles.
+  const int va = SRCA == SRC_F32C ? 4 : 2, vb = SRCB == SRC_F32C ? 4 : 2;
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  bool vec = al(g.A) && al(g.B) && g.lda % va == 0 && g.ldb % vb == 0 && g.K % va == 0 &&
+             g.sA % va == 0 && g.sB % vb == 0;
+  if (BLAY == B_NK) vec = vec && g.K % vb == 0;
+  else vec = vec && g.N % vb == 0;
+  if (vec)
+    gemm_f64_kernel<BT, SRCA, SRCB, BLAY, OUT, true><<<grid, 256, 0, st>>>(g);
+  else
+    gemm_f64_kernel<BT, SRCA, SRCB, BLAY, OUT, false><<<grid, 256, 0, st>>>(g);
 }
 
 // C[b] = alpha*avec[b]*A[b]B[b] + beta_diag*I for batched n x n fp64 matrices.
@@ -317,9 +402,15 @@ static void ns_power(const double* A, double add, double* sqrt_out, double* isqr
 
 static size_t ns_work_doubles(int n, int batch) { return 5 * (size_t)n * n * batch + batch; }
 
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e && *e) ? atoi(e) : dflt;
+}
+
 static int pick_ksplit(int batch, int tiles, int64_t K) {
   // aim for ~2048 workgroups, each with >= 4096 K values
-  int s = (int)((2048 + (int64_t)batch * tiles - 1) / ((int64_t)batch * tiles));
+  const int64_t target = env_int("RPST_WCT_BLOCKS", 4096);
+  int s = (int)((target + (int64_t)batch * tiles - 1) / ((int64_t)batch * tiles));
   const int64_t maxs = K / 4096 > 1 ? K / 4096 : 1;
   if (s > maxs) s = (int)maxs;
   return s < 1 ? 1 : (s > 64 ? 64 : s);
@@ -338,7 +429,7 @@ static WctLayout wct_layout(int n, int C, int64_t HW) {
   L.n = n;
   L.C = C;
   L.HW = HW;
-  L.BT = C >= 128 ? 128 : 64;
+  L.BT = (C >= 128 && env_int("RPST_WCT_COV_BT", 128) == 128) ? 128 : 64;
   L.tiles = (C + L.BT - 1) / L.BT;
   L.symtiles = L.tiles * (L.tiles + 1) / 2;
   L.ksplit = pick_ksplit(2 * n, L.symtiles, HW);
@@ -439,8 +530,13 @@ static int wct_run(const void* cF, const void* sF, void* out, int n, int C, int6
   g.sB = (int64_t)C * HW;
   g.sC = (int64_t)C * HW;
   g.ksplit = 1;
-  dim3 grid((unsigned)((HW + 127) / 128), (C + 127) / 128, n);
-  gemm64<128, SRC_F64, SRC, B_KN, OUTM>(g, grid, st);
+  if (env_int("RPST_WCT_T_BT", 64) == 128) {
+    dim3 grid((unsigned)((HW + 127) / 128), (C + 127) / 128, n);
+    gemm64<128, SRC_F64, SRC, B_KN, OUTM>(g, grid, st);
+  } else {
+    dim3 grid((unsigned)((HW + 63) / 64), (C + 63) / 64, n);
+    gemm64<64, SRC_F64, SRC, B_KN, OUTM>(g, grid, st);
+  }
   return launch_status("gemm_f64_kernel(transform)");
 }
 

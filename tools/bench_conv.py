@@ -30,7 +30,7 @@ VGG = [
     (64, 256, 128, 128, 256, 3, 1, 0), (64, 256, 128, 128, 512, 3, 1, 1),
     (64, 512, 64, 64, 512, 3, 1, 0), (32, 512, 64, 64, 512, 1, 0, 0),
 ]
-VARIANTS = {128: [0, 1, 2, 3], 64: [0, 1, 2], 32: [0, 1, 2]}
+VARIANTS = {128: [0, 1, 2, 3, 4], 64: [0, 1, 2], 32: [0, 1, 2]}
 
 
 def bm_of(cout):
@@ -62,8 +62,9 @@ def main():
                 out = ops.conv2d(x, p, b, cout, k, pad=pad, in_op=in_op, relu=True)
                 if ref is None:
                     ref = out.clone()
-                elif rnd == 0:
-                    assert torch.equal(out, ref), f"variant {v} differs"
+                elif rnd == 0:  # chunk size changes the K summation order: tolerance
+                    err = float((out - ref).norm() / ref.norm().clamp_min(1e-30))
+                    assert err < 1e-5, f"variant {v} differs: {err}"
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
