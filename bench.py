@@ -96,7 +96,27 @@ def cpu_baseline(kind, size, budget_s=12.0):
                       f"{threads} threads, {dt:.1f}s"}
 
 
-def roofline_from_trace(summary, flops_key=True):
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def pmc_lookup(kernel_substr, grid=None):
+    """HBM bytes per launch from the committed rocprofv3 PMC table (tools/pmc_traffic.py);
+    None if the kernel/grid was not profiled."""
+    if not os.path.exists(PMC_TRAFFIC):
+        return None
+    table = json.load(open(PMC_TRAFFIC))
+    tot = 0.0
+    found = False
+    for k, v in table.items():
+        name, g = k.rsplit("|", 1)
+        if kernel_substr in name and (grid is None or int(g) == grid):
+            tot += v["traffic_bytes"]
+            found = True
+    return tot if found else None
+
+
+def roofline_from_trace(summary):
+    from rpst import _lib
     best = None
     for name, a in summary.items():
         if not name.startswith("conv"):
@@ -108,10 +128,19 @@ def roofline_from_trace(summary, flops_key=True):
     name, a = best
     avg_ms = a["ms"] / a["launches"]
     achieved = a["flops"] / (avg_ms * 1e-3) / 1e12
+    # "conv3x3 128->256 512x512 N64 op0" -> launch geometry -> PMC record
+    k, chans, hw, nn, op = name.split()
+    cin, cout = (int(v) for v in chans.split("->"))
+    h, w = (int(v) for v in hw.split("x"))
+    n, in_op, ks = int(nn[1:]), int(op[2:]), int(k[4])
+    hs, ws = ((h * 2, w * 2) if in_op == 1 else ((h // 2, w // 2) if in_op == 2 else (h, w)))
+    grid = _lib.load().rpst_conv2d_grid_threads(n, hs, ws, cout, ks, in_op)
+    traffic = pmc_lookup("conv_mfma_kernel", grid)
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
-            "kernel": f"conv_mfma_kernel [{name}]", "launch_ms": round(avg_ms, 4),
-            "flop_per_launch": a["flops"]}
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+            "traffic": traffic, "kernel": f"conv_mfma_kernel [{name}]",
+            "launch_ms": round(avg_ms, 4), "flop_per_launch": a["flops"],
+            "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None}
 
 
 def adain_roofline(summary):
@@ -119,10 +148,14 @@ def adain_roofline(summary):
         if name.startswith("adain"):
             avg_ms = a["ms"] / a["launches"]
             gbs = a["bytes"] / (avg_ms * 1e-3) / 1e9
+            st = pmc_lookup("plane_stats_kernel")
+            ap = pmc_lookup("plane_apply_kernel<true>")
+            traffic = (st + ap) if (st is not None and ap is not None) else None
             return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
                     "kernel": f"plane_stats_kernel+plane_apply_kernel [{name}]",
-                    "launch_ms": round(avg_ms, 4), "bytes_per_launch": a["bytes"]}
+                    "launch_ms": round(avg_ms, 4), "bytes_per_launch": a["bytes"],
+                    "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None}
     return None
 
 

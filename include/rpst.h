@@ -93,6 +93,10 @@ int rpst_conv2d(const float* input, const float* aux, const float* packed_weight
                 int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
                 rpst_stream_t stream);
 
+/* Launch geometry (total threads) rpst_conv2d would use for this shape — host-only; lets
+ * profilers match rocprofv3 per-dispatch records (Grid_Size) to a layer. */
+int64_t rpst_conv2d_grid_threads(int N, int Hs, int Ws, int Cout, int ksize, int in_op);
+
 /* ---- stand-alone pool / upsample (same semantics as the conv input operators) ----- */
 int rpst_maxpool2x2_ceil(const float* in, float* out, int N, int C, int H, int W,
                          rpst_stream_t stream);

@@ -416,6 +416,26 @@ extern "C" size_t rpst_conv2d_packed_size(int Cout, int Cin, int ksize) {
   return nch * ksize * ksize * ck * (size_t)pad_cout(Cout) * sizeof(float);
 }
 
+extern "C" int64_t rpst_conv2d_grid_threads(int N, int Hs, int Ws, int Cout, int ksize,
+                                            int in_op) {
+  if (N <= 0 || Hs <= 0 || Ws <= 0 || Cout <= 0 || (ksize != 1 && ksize != 3)) return 0;
+  int H = Hs, W = Ws;
+  if (in_op == RPST_IN_MAXPOOL2) {
+    H = (Hs + 1) / 2;
+    W = (Ws + 1) / 2;
+  } else if (in_op == RPST_IN_UPSAMPLE2) {
+    H = 2 * Hs;
+    W = 2 * Ws;
+  }
+  const TileCfg cfg = pick_cfg(Cout);
+  const int variant = conv_variant(cfg.BM, ksize, in_op);
+  const int th = variant_th(cfg.BM, variant);
+  const int nth = (cfg.BM == 128 && variant == 0) ? 512 : 256;
+  const int64_t blocks = (int64_t)((W + kTW - 1) / kTW) * ((H + th - 1) / th) * N *
+                         (pad_cout(Cout) / cfg.BM);
+  return blocks * nth;
+}
+
 extern "C" int rpst_conv2d_pack(const float* weight, float* packed, int Cout, int Cin,
                                 int ksize, rpst_stream_t stream) {
   RPST_REQUIRE(weight && packed, "conv2d_pack: null pointer");
