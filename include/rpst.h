@@ -44,6 +44,8 @@ typedef void* rpst_stream_t;
 #define RPST_IN_MAXPOOL2 1 /* nn.MaxPool2d((2,2),(2,2),(0,0),ceil_mode=True) base.py:65,72,85,98 */
 #define RPST_IN_UPSAMPLE2 2 /* nn.Upsample(scale_factor=2, mode='nearest') base.py:29,42,49     */
 #define RPST_IN_ADD_UPSAMPLE2 3 /* x + Upsample2(y)   sanet.py:149 (Transform merge input)   */
+#define RPST_IN_ADAIN 4 /* ((x-mean_c)/std_c)*std_s+mean_s per (n,ci): AdaIN base.py:416-418 fused
+                           into the consumer conv; aux = [mean_c|mean_s|std_c|std_s], N*Cin each */
 
 /* Library version (major*10000 + minor*100 + patch). */
 int rpst_version(void);
@@ -81,6 +83,7 @@ int rpst_mean_variance_norm(const float* feat, float* out, int N, int C, int64_t
  *   RPST_IN_MAXPOOL2:     input (N,Cin,Hs,Ws), conv runs at H=ceil(Hs/2), W=ceil(Ws/2)
  *   RPST_IN_UPSAMPLE2:    input (N,Cin,Hs,Ws), conv runs at H=2Hs, W=2Ws
  *   RPST_IN_ADD_UPSAMPLE2: input (N,Cin,H,W) + aux (N,Cin,H/2,W/2) upsampled
+ *   RPST_IN_ADAIN:        input (N,Cin,H,W) normalised on load with aux statistics
  *   RPST_IN_NONE:         input (N,Cin,H,W)
  * (Hs, Ws) are the dims of `input`. out (N,Cout,H,W):
  *   out = [relu](conv(in_op(input)) + bias) [+ residual]   (residual (N,Cout,H,W) or NULL)
@@ -92,6 +95,17 @@ int rpst_conv2d(const float* input, const float* aux, const float* packed_weight
                 const float* bias, const float* residual, float* out, int N, int Cin,
                 int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
                 rpst_stream_t stream);
+
+/* Same conv, additionally returning calc_mean_std (base.py:399-407) of its OUTPUT per
+ * (n, co): the statistics are reduced in the conv epilogue from registers and merged in
+ * fp64, so an AdaIN consumer never re-reads the feature. mean/std_out: N*Cout floats.
+ * Workspace: rpst_conv2d_stats_workspace_size(N, Hs, Ws, Cout, ksize, in_op). */
+size_t rpst_conv2d_stats_workspace_size(int N, int Hs, int Ws, int Cout, int ksize, int in_op);
+int rpst_conv2d_stats(const float* input, const float* aux, const float* packed_weight,
+                      const float* bias, const float* residual, float* out, int N, int Cin,
+                      int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
+                      float* mean, float* std_out, float eps, void* workspace,
+                      size_t workspace_bytes, rpst_stream_t stream);
 
 /* Launch geometry (total threads) rpst_conv2d would use for this shape — host-only; lets
  * profilers match rocprofv3 per-dispatch records (Grid_Size) to a layer. */

@@ -43,6 +43,8 @@ struct ConvArgs {
   int N, Cin, Hs, Ws, H, W, Cout, Cout_pad, nchunks;
   int tiles_x, tiles_y, co_tiles;
   int pad, relu;
+  float2* stat_part;  // optional: per-(n, co, wave tile) (mean, M2) of the output
+  int stat_P;         // partials per (n, co) = tiles_x * tiles_y * WN
 };
 
 template <int KS>
@@ -99,9 +101,25 @@ __device__ __forceinline__ float fetch(__amdgpu_buffer_rsrc_t rin, __amdgpu_buff
     const float v = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
     const float u = bload(raux, ok ? abyte + (unsigned)((yr >> 1) * (a.W >> 1) + (xr >> 1)) * 4u : kOOB);
     return v + u;
-  } else {
+  } else {  // RPST_IN_NONE and RPST_IN_ADAIN (affine applied by the caller)
     return bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
   }
+}
+
+// AdaIN on load (RPST_IN_ADAIN): ((v - mean_c) / std_c) * std_s + mean_s, rounded like the
+// stand-alone apply kernel (no contraction). aux = [mean_c | mean_s | std_c | std_s], each
+// N*Cin floats.
+struct AdainP {
+  float mc, ms, sc, ss;
+};
+__device__ __forceinline__ AdainP adain_params(const float* __restrict__ aux, int n, int ci,
+                                               const ConvArgs& a) {
+  const int64_t nc = (int64_t)a.N * a.Cin;
+  const int64_t i = (int64_t)n * a.Cin + (ci < a.Cin ? ci : 0);
+  return {aux[i], aux[nc + i], aux[2 * nc + i], aux[3 * nc + i]};
+}
+__device__ __forceinline__ float adain_apply(float v, const AdainP& p) {
+  return __fadd_rn(__fmul_rn(__fdiv_rn(__fsub_rn(v, p.mc), p.sc), p.ss), p.ms);
 }
 
 // CKK = input channels per kernel chunk (divides the packing chunk K::CK);
@@ -229,14 +247,22 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
     _Pragma("unroll") for (int q = 0; q < CPT; ++q) {                                       \
       const unsigned ch = (unsigned)((c) * CK + cg + CGS * q);                              \
       const unsigned pb = ch * in_plane * 4u, ab = ch * aux_plane * 4u;                     \
+      const bool chok = (int)ch < a.Cin;                                                    \
+      AdainP ap{0.f, 0.f, 1.f, 1.f};                                                        \
+      if (INOP == RPST_IN_ADAIN) ap = adain_params(a.aux, n, (int)ch, a);                   \
       _Pragma("unroll") for (int i = 0; i < RPT; ++i) {                                     \
         const int py = rs * RPT + i;                                                        \
         int y = y0 - OFF + py;                                                              \
         const bool yok = resolve(y, a.H, a.pad, KS == 3) && py < PH;                        \
-        xreg[q][i] = fetch<INOP>(rin, raux, pb, ab, y, bx, yok && bx_ok, a);                \
+        float v = fetch<INOP>(rin, raux, pb, ab, y, bx, yok && bx_ok, a);                   \
+        if (INOP == RPST_IN_ADAIN) v = (yok && bx_ok && chok) ? adain_apply(v, ap) : 0.f;   \
+        xreg[q][i] = v;                                                                     \
       }                                                                                     \
-      _Pragma("unroll") for (int e = 0; e < HALO; ++e) xreg[q][RPT + e] =                   \
-          fetch<INOP>(rin, raux, pb, ab, hy[e], hx[e], h_ok[e], a);                         \
+      _Pragma("unroll") for (int e = 0; e < HALO; ++e) {                                    \
+        float v = fetch<INOP>(rin, raux, pb, ab, hy[e], hx[e], h_ok[e], a);                 \
+        if (INOP == RPST_IN_ADAIN) v = (h_ok[e] && chok) ? adain_apply(v, ap) : 0.f;        \
+        xreg[q][RPT + e] = v;                                                               \
+      }                                                                                     \
     }                                                                                       \
   }
 
@@ -304,15 +330,94 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int y = y0 + wn * NT + nt;
+        float v = acc[mt][nt][r] + b;
+        if (a.relu) v = fmaxf(v, 0.f);
         if (y < a.H && x < a.W) {
-          float v = acc[mt][nt][r] + b;
-          if (a.relu) v = fmaxf(v, 0.f);
           const int64_t o = pbase + (int64_t)y * a.W + x;
           if (a.res) v += a.res[o];
           a.out[o] = v;
         }
+        acc[mt][nt][r] = v;
       }
     }
+  }
+
+  // optional output statistics (AdaIN / calc_mean_std of this layer's output, fused):
+  // each half-wave holds one output channel's 32 x NT pixels of this tile -> (mean, M2)
+  // over the valid ones; merged in fp64 by stat_merge_kernel.
+  if (a.stat_part) {
+    const int rows = max(0, min(NT, a.H - (y0 + wn * NT)));
+    const int cols = max(0, min(kTW, a.W - x0));
+    const int cnt = rows * cols;
+    const float inv = cnt > 0 ? 1.f / (float)cnt : 0.f;
+    const bool xv = x < a.W;
+    const int pidx = (ty * a.tiles_x + tx) * WN + wn;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wm * WTM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float s1 = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          s1 += (xv && nt < rows) ? acc[mt][nt][r] : 0.f;
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) s1 += __shfl_xor(s1, o, 64);  // within the half-wave
+        const float mean = s1 * inv;
+        float s2 = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const float d = acc[mt][nt][r] - mean;
+          s2 += (xv && nt < rows) ? d * d : 0.f;
+        }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+        if (j == 0 && co < a.Cout)
+          a.stat_part[((int64_t)n * a.Cout + co) * a.stat_P + pidx] = make_float2(mean, s2);
+      }
+    }
+  }
+}
+
+// Merge the (mean, M2) partials of one (n, c) plane in fp64 (Chan et al.), fixed order:
+// lane l folds partials l, l+64, ...; then a butterfly over lanes. Writes calc_mean_std.
+__global__ __launch_bounds__(256) void stat_merge_kernel(const float2* __restrict__ part,
+                                                         float* __restrict__ mean,
+                                                         float* __restrict__ stdv, int planes,
+                                                         int P, int tiles_x, int WN, int NT,
+                                                         int H, int W, float eps) {
+  const int plane = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (plane >= planes) return;
+  double cn = 0.0, cm = 0.0, c2 = 0.0;
+  for (int p = lane; p < P; p += 64) {
+    const int tile = p / WN, wn = p - tile * WN;
+    const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+    const int rows = max(0, min(NT, H - (ty * NT * WN + wn * NT)));
+    const int cols = max(0, min(kTW, W - tx * kTW));
+    const double nb = (double)(rows * cols);
+    if (nb == 0.0) continue;
+    const float2 v = part[(int64_t)plane * P + p];
+    const double n2 = cn + nb, d = (double)v.x - cm;
+    cm += d * nb / n2;
+    c2 += (double)v.y + d * d * cn * nb / n2;
+    cn = n2;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double on = __shfl_xor(cn, o, 64), om = __shfl_xor(cm, o, 64), o2 = __shfl_xor(c2, o, 64);
+    const double n2 = cn + on;
+    if (n2 > 0.0) {
+      const double d = om - cm;
+      cm += d * on / n2;
+      c2 += o2 + d * d * cn * on / n2;
+    }
+    cn = n2;
+  }
+  if (lane == 0) {
+    float varf = (float)(cn > 1.0 ? c2 / (cn - 1.0) : __builtin_nan(""));
+    mean[plane] = (float)cm;
+    stdv[plane] = __fsqrt_rn(__fadd_rn(varf, eps));
   }
 }
 
@@ -400,6 +505,18 @@ static int variant_th(int BM, int variant) {
   return variant == 0 ? 16 : 8;
 }
 
+// threads per workgroup of a variant
+static int variant_nth(int BM, int variant) {
+  return ((BM == 128 && variant == 0) || (BM == 64 && variant == 2)) ? 512 : 256;
+}
+
+// WN (waves along the pixel rows) of a variant: rows per wave = TH / WN
+static int variant_wn(int BM, int variant) {
+  if (BM == 128) return variant == 0 ? 4 : 2;
+  if (BM == 64) return variant == 2 ? 8 : 4;
+  return 4;
+}
+
 static int conv_variant(int BM, int ksize, int in_op) {
   const char* e = getenv("RPST_CONV_VARIANT");
   return (e && *e) ? atoi(e) : pick_variant(BM, ksize, in_op);
@@ -430,7 +547,7 @@ extern "C" int64_t rpst_conv2d_grid_threads(int N, int Hs, int Ws, int Cout, int
   const TileCfg cfg = pick_cfg(Cout);
   const int variant = conv_variant(cfg.BM, ksize, in_op);
   const int th = variant_th(cfg.BM, variant);
-  const int nth = (cfg.BM == 128 && variant == 0) ? 512 : 256;
+  const int nth = variant_nth(cfg.BM, variant);
   const int64_t blocks = (int64_t)((W + kTW - 1) / kTW) * ((H + th - 1) / th) * N *
                          (pad_cout(Cout) / cfg.BM);
   return blocks * nth;
@@ -449,15 +566,15 @@ extern "C" int rpst_conv2d_pack(const float* weight, float* packed, int Cout, in
   return launch_status("conv_pack_kernel");
 }
 
-extern "C" int rpst_conv2d(const float* input, const float* aux, const float* packed_weight,
-                           const float* bias, const float* residual, float* out, int N,
-                           int Cin, int Hs, int Ws, int Cout, int ksize, int pad_mode,
-                           int in_op, int relu, rpst_stream_t stream) {
+static int conv_common(const float* input, const float* aux, const float* packed_weight,
+                       const float* bias, const float* residual, float* out, int N, int Cin,
+                       int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
+                       float2* stat_part, int* stat_P, ConvArgs* args_out, hipStream_t st) {
   RPST_REQUIRE(input && packed_weight && out, "conv2d: null pointer");
   RPST_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && Hs > 0 && Ws > 0, "conv2d: bad shape");
   RPST_REQUIRE(ksize == 1 || ksize == 3, "conv2d: ksize must be 1 or 3, got %d", ksize);
   RPST_REQUIRE(pad_mode == RPST_PAD_ZERO || pad_mode == RPST_PAD_REFLECT, "conv2d: bad pad");
-  RPST_REQUIRE(in_op >= RPST_IN_NONE && in_op <= RPST_IN_ADD_UPSAMPLE2, "conv2d: bad in_op");
+  RPST_REQUIRE(in_op >= RPST_IN_NONE && in_op <= RPST_IN_ADAIN, "conv2d: bad in_op");
   ConvArgs a{};
   a.in = input;
   a.aux = aux;
@@ -487,6 +604,11 @@ extern "C" int rpst_conv2d(const float* input, const float* aux, const float* pa
       a.H = Hs;
       a.W = Ws;
       break;
+    case RPST_IN_ADAIN:
+      RPST_REQUIRE(aux != nullptr, "conv2d: ADAIN needs aux (AdaIN statistics)");
+      a.H = Hs;
+      a.W = Ws;
+      break;
     default:
       a.H = Hs;
       a.W = Ws;
@@ -502,6 +624,10 @@ extern "C" int rpst_conv2d(const float* input, const float* aux, const float* pa
   a.tiles_x = (a.W + kTW - 1) / kTW;
   a.tiles_y = (a.H + th - 1) / th;
   a.co_tiles = a.Cout_pad / cfg.BM;
+  const int wn = variant_wn(cfg.BM, variant);
+  a.stat_P = a.tiles_x * a.tiles_y * wn;
+  a.stat_part = stat_part;
+  if (stat_P) *stat_P = a.stat_P;
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * N * a.co_tiles;
   RPST_REQUIRE(blocks <= 0x7fffffffLL, "conv2d: grid too large");
   RPST_REQUIRE((int64_t)N * (Cout > Cin ? Cout : Cin) * a.H * a.W < (1LL << 40),
@@ -510,7 +636,7 @@ extern "C" int rpst_conv2d(const float* input, const float* aux, const float* pa
   // buffer offset
   RPST_REQUIRE(((int64_t)Cin + 16) * Hs * Ws * 4 < (1LL << 31),
                "conv2d: one image's input exceeds 2 GiB");
-  hipStream_t st = as_stream(stream);
+  if (args_out) *args_out = a;
   if (ksize == 1) {
     RPST_REQUIRE(in_op == RPST_IN_NONE, "conv2d: 1x1 conv supports in_op NONE only");
     launch_conv<1, RPST_IN_NONE>(a, cfg.BM, variant, st);
@@ -520,10 +646,69 @@ extern "C" int rpst_conv2d(const float* input, const float* aux, const float* pa
     launch_conv<3, RPST_IN_UPSAMPLE2>(a, cfg.BM, variant, st);
   } else if (in_op == RPST_IN_ADD_UPSAMPLE2) {
     launch_conv<3, RPST_IN_ADD_UPSAMPLE2>(a, cfg.BM, variant, st);
+  } else if (in_op == RPST_IN_ADAIN) {
+    launch_conv<3, RPST_IN_ADAIN>(a, cfg.BM, variant, st);
   } else {
     launch_conv<3, RPST_IN_NONE>(a, cfg.BM, variant, st);
   }
   return launch_status("conv_mfma_kernel");
+}
+
+extern "C" int rpst_conv2d(const float* input, const float* aux, const float* packed_weight,
+                           const float* bias, const float* residual, float* out, int N,
+                           int Cin, int Hs, int Ws, int Cout, int ksize, int pad_mode,
+                           int in_op, int relu, rpst_stream_t stream) {
+  return conv_common(input, aux, packed_weight, bias, residual, out, N, Cin, Hs, Ws, Cout,
+                     ksize, pad_mode, in_op, relu, nullptr, nullptr, nullptr, as_stream(stream));
+}
+
+extern "C" size_t rpst_conv2d_stats_workspace_size(int N, int Hs, int Ws, int Cout, int ksize,
+                                                   int in_op) {
+  const int64_t thr = rpst_conv2d_grid_threads(N, Hs, Ws, Cout, ksize, in_op);
+  if (thr <= 0) return 0;
+  int H = Hs, W = Ws;
+  if (in_op == RPST_IN_MAXPOOL2) {
+    H = (Hs + 1) / 2;
+    W = (Ws + 1) / 2;
+  } else if (in_op == RPST_IN_UPSAMPLE2) {
+    H = 2 * Hs;
+    W = 2 * Ws;
+  }
+  const TileCfg cfg = pick_cfg(Cout);
+  const int variant = conv_variant(cfg.BM, ksize, in_op);
+  const int64_t P = (int64_t)((W + kTW - 1) / kTW) * ((H + variant_th(cfg.BM, variant) - 1) /
+                                                      variant_th(cfg.BM, variant)) *
+                    variant_wn(cfg.BM, variant);
+  return (size_t)N * Cout * P * sizeof(float2);
+}
+
+extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
+                                 const float* packed_weight, const float* bias,
+                                 const float* residual, float* out, int N, int Cin, int Hs,
+                                 int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
+                                 float* mean, float* std_out, float eps, void* workspace,
+                                 size_t workspace_bytes, rpst_stream_t stream) {
+  RPST_REQUIRE(mean && std_out, "conv2d_stats: null statistics pointer");
+  const size_t need = rpst_conv2d_stats_workspace_size(N, Hs, Ws, Cout, ksize, in_op);
+  if (!workspace || workspace_bytes < need) {
+    set_error("conv2d_stats: workspace %zu < %zu bytes", workspace_bytes, need);
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  ConvArgs a{};
+  int P = 0;
+  if (int e = conv_common(input, aux, packed_weight, bias, residual, out, N, Cin, Hs, Ws, Cout,
+                          ksize, pad_mode, in_op, relu, static_cast<float2*>(workspace), &P,
+                          &a, st))
+    return e;
+  const int planes = N * Cout;
+  const TileCfg cfg = pick_cfg(Cout);
+  const int variant = conv_variant(cfg.BM, ksize, in_op);
+  const int wn = variant_wn(cfg.BM, variant), th = variant_th(cfg.BM, variant);
+  stat_merge_kernel<<<(planes + 3) / 4, 256, 0, st>>>(static_cast<const float2*>(workspace), mean,
+                                                      std_out, planes, P, a.tiles_x, wn, th / wn,
+                                                      a.H, a.W, eps);
+  return launch_status("stat_merge_kernel");
 }
 
 // ---- stand-alone max-pool / upsample (used where no conv follows directly) ----------

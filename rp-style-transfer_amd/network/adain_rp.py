@@ -7,14 +7,35 @@ adain_rp.py:96-97), AdaIN with the HIP statistics kernels, then the RP decoder.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
+from rpst import ops, plan
 from rpst.plan import KernelSequential
 
 from .base import (BaseNet, adaptive_instance_normalization, build_decrease_depth_rp_blocks,
                    build_increase_depth_rp_blocks, calc_mean_std, mse)
 from .base import adaptive_instance_normalization as AdaIN  # noqa: F401 (reference alias)
+
+
+# RPST_FUSE_ADAIN=0 disables the fused path (A/B measurements, debugging)
+FUSED_ADAIN = os.environ.get("RPST_FUSE_ADAIN", "1") != "0"
+
+
+def adain_rp_fused(encoder, decoder, content, style):
+    """enc -> AdaIN -> dec with AdaIN fused into its neighbours (adain_rp.py:94-101):
+    the encoder's last conv emits calc_mean_std of its output from its epilogue, and the
+    decoder's first conv applies ((c - mu_c)/sigma_c)*sigma_s + mu_s while loading its
+    input tile, so the AdaIN feature is never written to HBM."""
+    n = content.shape[0]
+    assert content.size() == style.size()
+    feats, mean, std = plan.run(plan.compile_layers(encoder.children()),
+                                torch.cat([content, style], dim=0), stats_last=True)
+    aux = ops.adain_params(mean[:n], std[:n], mean[n:], std[n:])
+    return plan.run(plan.compile_layers(decoder.children()), feats[:n],
+                    first_aux=aux, first_in_op=ops.IN_ADAIN)
 
 
 def encode_both(encoder, content, style):
@@ -70,6 +91,8 @@ class AdaINRPNet(BaseNet):
 
     def test(self, content, style, iterations=0, bid=0, c_mask_path=None, s_mask_path=None):
         with torch.no_grad():
+            if type(self).fuse is AdaINRPNet.fuse and FUSED_ADAIN:
+                return adain_rp_fused(self.rp_shared_encoder, self.rp_decoder, content, style)
             content_feat, style_feat = encode_both(self.rp_shared_encoder, content, style)
             fusion_feat = self.fuse(content_feat, style_feat)
             return self.rp_decoder(fusion_feat)

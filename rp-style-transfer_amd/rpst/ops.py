@@ -14,7 +14,7 @@ import torch
 from . import _lib
 
 PAD_ZERO, PAD_REFLECT = 0, 1
-IN_NONE, IN_MAXPOOL2, IN_UPSAMPLE2, IN_ADD_UPSAMPLE2 = 0, 1, 2, 3
+IN_NONE, IN_MAXPOOL2, IN_UPSAMPLE2, IN_ADD_UPSAMPLE2, IN_ADAIN = 0, 1, 2, 3, 4
 
 
 class Trace:
@@ -175,7 +175,10 @@ def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], 
         assert tuple(residual.shape) == (n, cout, h, w)
     if aux is not None:
         aux = _c(aux)
-        assert tuple(aux.shape) == (n, cin, h // 2, w // 2)
+        if in_op == IN_ADAIN:
+            assert aux.numel() == 4 * n * cin, "ADAIN aux = [mean_c|mean_s|std_c|std_s]"
+        else:
+            assert tuple(aux.shape) == (n, cin, h // 2, w // 2)
     name = f"conv{ksize}x{ksize} {cin}->{cout} {h}x{w} N{n} op{in_op}"
     with _traced(name, 2.0 * n * cout * h * w * cin * ksize * ksize,
                  4.0 * (x.numel() + n * cout * h * w)):
@@ -184,6 +187,38 @@ def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], 
                   out.data_ptr(), n, cin, hs, ws, cout, ksize, pad, in_op, int(bool(relu)),
                   _stream(x))
     return out
+
+
+def conv2d_stats(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], cout: int,
+                 ksize: int, pad: int = PAD_ZERO, in_op: int = IN_NONE, relu: bool = False,
+                 aux: Optional[torch.Tensor] = None, eps: float = 1e-5):
+    """conv2d plus calc_mean_std of its output, reduced in the conv epilogue:
+    returns (out, mean (N,Cout,1,1), std (N,Cout,1,1))."""
+    assert x.dim() == 4
+    _check(x, packed, bias, aux)
+    x = _c(x)
+    n, cin, hs, ws = x.shape
+    h, w = conv_out_hw(hs, ws, in_op)
+    out = torch.empty((n, cout, h, w), device=x.device, dtype=torch.float32)
+    mean = torch.empty((n, cout, 1, 1), device=x.device, dtype=torch.float32)
+    std = torch.empty_like(mean)
+    lib = _lib.load()
+    nbytes = lib.rpst_conv2d_stats_workspace_size(n, hs, ws, cout, ksize, in_op)
+    ws_t = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
+    name = f"conv{ksize}x{ksize} {cin}->{cout} {h}x{w} N{n} op{in_op}"
+    with _traced(name, 2.0 * n * cout * h * w * cin * ksize * ksize,
+                 4.0 * (x.numel() + n * cout * h * w)):
+        _lib.call("rpst_conv2d_stats", x.data_ptr(), _ptr(aux), packed.data_ptr(),
+                  _ptr(None if bias is None else _c(bias.detach())), None, out.data_ptr(), n,
+                  cin, hs, ws, cout, ksize, pad, in_op, int(bool(relu)), mean.data_ptr(),
+                  std.data_ptr(), eps, ws_t.data_ptr(), nbytes, _stream(x))
+    return out, mean, std
+
+
+def adain_params(mean_c, std_c, mean_s, std_s) -> torch.Tensor:
+    """aux vector of RPST_IN_ADAIN: [mean_c | mean_s | std_c | std_s] (N*C each)."""
+    return torch.cat([mean_c.reshape(-1), mean_s.reshape(-1), std_c.reshape(-1),
+                      std_s.reshape(-1)])
 
 
 def maxpool2x2_ceil(x: torch.Tensor) -> torch.Tensor:

@@ -116,14 +116,35 @@ def run_conv_step(step: ConvStep, x: torch.Tensor, aux=None, residual=None) -> t
                       residual=residual)
 
 
-def run(steps: List[object], x: torch.Tensor) -> torch.Tensor:
-    for s in steps:
+def run(steps: List[object], x: torch.Tensor, first_aux=None, first_in_op=None,
+        stats_last: bool = False):
+    """Run a compiled plan. first_in_op/first_aux override the first conv's input operator
+    (e.g. RPST_IN_ADAIN to fuse AdaIN into the decoder's first conv); stats_last makes the
+    last conv also return calc_mean_std of its output -> (x, mean, std)."""
+    mean = std = None
+    for i, s in enumerate(steps):
         if isinstance(s, ConvStep):
-            x = run_conv_step(s, x)
+            in_op, aux = s.in_op, None
+            if i == 0 and first_in_op is not None:
+                if s.in_op != ops.IN_NONE:
+                    raise NotImplementedError("rpst plan: first conv already has an input op")
+                in_op, aux = first_in_op, first_aux
+            c = s.conv
+            if stats_last and i == len(steps) - 1:
+                x, mean, std = ops.conv2d_stats(x, packed_weight(c), c.bias, c.out_channels,
+                                                c.kernel_size[0], pad=s.pad, in_op=in_op,
+                                                relu=s.relu, aux=aux)
+            else:
+                x = ops.conv2d(x, packed_weight(c), c.bias, c.out_channels, c.kernel_size[0],
+                               pad=s.pad, in_op=in_op, relu=s.relu, aux=aux)
         elif s.in_op == ops.IN_MAXPOOL2:
             x = ops.maxpool2x2_ceil(x)
         else:
             x = ops.upsample_nearest2x(x)
+    if stats_last:
+        if mean is None:
+            mean, std = ops.calc_mean_std(x)
+        return x, mean, std
     return x
 
 

@@ -264,3 +264,54 @@ def test_vgg_and_decoder_golden(cuda, golden):
         synth_(dec, 81)
         out = dec.to(cuda)(t(g["z"]).to(cuda))
     assert rel_l2(out, g["dec_out"]) < 1e-5
+
+
+# ---- fused AdaIN (statistics in the producing conv's epilogue, apply in the consumer's loader)
+@pytest.mark.parametrize("shape", [(2, 16, 64, 96, 256), (1, 8, 17, 45, 64), (3, 3, 9, 7, 32),
+                                   (2, 64, 40, 40, 128)])
+def test_conv2d_stats_equal_calc_mean_std(cuda, shape):
+    from rpst import ops
+    n, cin, h, w, cout = shape
+    x = gen(50, (n, cin, h, w), 1.0, 0.3).to(cuda)
+    wt = gen(51, (cout, cin, 3, 3), (2.0 / (cin * 9)) ** 0.5).to(cuda)
+    b = gen(52, (cout,), 0.05).to(cuda)
+    p = ops.pack_conv_weight(wt)
+    out, mean, std = ops.conv2d_stats(x, p, b, cout, 3, relu=True)
+    ref = ops.conv2d(x, p, b, cout, 3, relu=True)
+    assert torch.equal(out, ref)
+    m2, s2 = R.calc_mean_std(out.double().cpu())
+    assert rel_l2(mean, m2) < 1e-6
+    assert rel_l2(std, s2) < 1e-6
+
+
+def test_conv2d_adain_input_op(cuda):
+    from rpst import ops
+    c = gen(60, (2, 32, 24, 40), 2.0, 0.5).clamp_min(0)
+    s = gen(61, (2, 32, 24, 40), 1.0, 1.0).clamp_min(0)
+    wt = gen(62, (16, 32, 3, 3), 0.08)
+    b = gen(63, (16,), 0.05)
+    mc, sc = R.calc_mean_std(c)
+    ms, ss = R.calc_mean_std(s)
+    aux = ops.adain_params(mc, sc, ms, ss).to(cuda)
+    p = ops.pack_conv_weight(wt.to(cuda))
+    out = ops.conv2d(c.to(cuda), p, b.to(cuda), 16, 3, in_op=ops.IN_ADAIN, aux=aux, relu=True)
+    ref = _conv_ref(R.adain(c, s).double(), wt.double(), b.double(), 0, 0, True)
+    assert rel_l2(out, ref) < 1e-5
+
+
+def test_adain_rp_fused_equals_unfused(cuda):
+    import network as net
+    import network.adain_rp as arp
+    from rpst import synth
+    m = net.AdaINRPNet(rp_config(16), copy.deepcopy(net.vgg))
+    synth_(m, 9)
+    m = m.to(cuda)
+    c = torch.from_numpy(synth.image(1, (2, 3, 48, 64))).to(cuda)
+    s = torch.from_numpy(synth.image(2, (2, 3, 48, 64))).to(cuda)
+    fused = m.test(c, s)
+    arp.FUSED_ADAIN = False
+    try:
+        plain = m.test(c, s)
+    finally:
+        arp.FUSED_ADAIN = True
+    assert rel_l2(fused, plain) < 1e-5
