@@ -30,7 +30,6 @@
 
 namespace rpst {
 
-constexpr int kConvThreads = 256;
 constexpr int kTW = 32;  // pixels per N sub-tile = one row segment
 
 struct ConvArgs {
@@ -345,7 +344,9 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
   // optional output statistics (AdaIN / calc_mean_std of this layer's output, fused):
   // each half-wave holds one output channel's 32 x NT pixels of this tile -> (mean, M2)
   // over the valid ones; merged in fp64 by stat_merge_kernel.
-  if (a.stat_part) {
+  // (compiled only for tiles with >= 4 rows per wave: with NT <= 2 hipcc keeps the
+  // accumulators dynamically indexed and spills thousands of VGPRs)
+  if constexpr (NT >= 4) if (a.stat_part) {
     const int rows = max(0, min(NT, a.H - (y0 + wn * NT)));
     const int cols = max(0, min(kTW, a.W - x0));
     const int cnt = rows * cols;
@@ -697,14 +698,20 @@ extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
   hipStream_t st = as_stream(stream);
   ConvArgs a{};
   int P = 0;
+  const TileCfg cfg = pick_cfg(Cout);
+  const int variant = conv_variant(cfg.BM, ksize, in_op);
+  const int wn = variant_wn(cfg.BM, variant), th = variant_th(cfg.BM, variant);
+  const int planes = N * Cout;
+  if (th / wn < 4) {  // tile without the fused statistics epilogue: separate pass
+    if (int e = conv_common(input, aux, packed_weight, bias, residual, out, N, Cin, Hs, Ws,
+                            Cout, ksize, pad_mode, in_op, relu, nullptr, &P, &a, st))
+      return e;
+    return rpst_calc_mean_std(out, mean, std_out, N, Cout, (int64_t)a.H * a.W, eps, stream);
+  }
   if (int e = conv_common(input, aux, packed_weight, bias, residual, out, N, Cin, Hs, Ws, Cout,
                           ksize, pad_mode, in_op, relu, static_cast<float2*>(workspace), &P,
                           &a, st))
     return e;
-  const int planes = N * Cout;
-  const TileCfg cfg = pick_cfg(Cout);
-  const int variant = conv_variant(cfg.BM, ksize, in_op);
-  const int wn = variant_wn(cfg.BM, variant), th = variant_th(cfg.BM, variant);
   stat_merge_kernel<<<(planes + 3) / 4, 256, 0, st>>>(static_cast<const float2*>(workspace), mean,
                                                       std_out, planes, P, a.tiles_x, wn, th / wn,
                                                       a.H, a.W, eps);
