@@ -76,49 +76,62 @@ __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
 
-// One patch element: logical (post-in_op) resolved row yr / column xr of the plane whose
-// byte offset (within the image) is `pbyte`. ok == false -> zero (pad position).
+// Raw global loads per patch element for each input operator; they are combined into
+// the element value only when the chunk is written to LDS (after the current chunk's
+// MFMAs), so no wait for the loads sits in front of the compute phase.
 template <int INOP>
-__device__ __forceinline__ float fetch(__amdgpu_buffer_rsrc_t rin, __amdgpu_buffer_rsrc_t raux,
-                                       unsigned pbyte, unsigned abyte, int yr, int xr, bool ok,
-                                       const ConvArgs& a) {
-  if (INOP == RPST_IN_MAXPOOL2) {
+struct RawN {
+  static constexpr int R = INOP == RPST_IN_MAXPOOL2 ? 4 : (INOP == RPST_IN_ADD_UPSAMPLE2 ? 2 : 1);
+};
+
+// Issue the loads of one element: logical (post-in_op) resolved row yr / column xr of the
+// plane at byte offset `pbyte` (image-relative). ok == false -> zero (pad position /
+// padded channel): every load goes out of range and returns 0.
+template <int INOP>
+__device__ __forceinline__ void fetch_raw(float (&r)[RawN<INOP>::R], __amdgpu_buffer_rsrc_t rin,
+                                          __amdgpu_buffer_rsrc_t raux, unsigned pbyte,
+                                          unsigned abyte, int yr, int xr, bool ok,
+                                          const ConvArgs& a) {
+  if constexpr (INOP == RPST_IN_MAXPOOL2) {
+    // 2x2 window of the source; missing right/bottom neighbours (ceil mode) re-read the
+    // top-left element so the max is unaffected
     const int sy = 2 * yr, sx = 2 * xr;
     const unsigned o = pbyte + (unsigned)(sy * a.Ws + sx) * 4u;
-    const bool xr1 = sx + 1 < a.Ws, yd = sy + 1 < a.Hs;
-    const float v00 = bload(rin, ok ? o : kOOB);
-    const float v01 = bload(rin, ok ? o + 4u : kOOB);
-    const float v10 = bload(rin, ok ? o + 4u * a.Ws : kOOB);
-    const float v11 = bload(rin, ok ? o + 4u * a.Ws + 4u : kOOB);
-    float v = fmaxf(v00, xr1 ? v01 : v00);
-    v = fmaxf(v, yd ? v10 : v00);
-    v = fmaxf(v, (xr1 && yd) ? v11 : v00);
-    return ok ? v : 0.f;
-  } else if (INOP == RPST_IN_UPSAMPLE2) {
-    return bload(rin, ok ? pbyte + (unsigned)((yr >> 1) * a.Ws + (xr >> 1)) * 4u : kOOB);
-  } else if (INOP == RPST_IN_ADD_UPSAMPLE2) {
-    const float v = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
-    const float u = bload(raux, ok ? abyte + (unsigned)((yr >> 1) * (a.W >> 1) + (xr >> 1)) * 4u : kOOB);
-    return v + u;
-  } else {  // RPST_IN_NONE and RPST_IN_ADAIN (affine applied by the caller)
-    return bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
+    const unsigned dx = sx + 1 < a.Ws ? 4u : 0u, dy = sy + 1 < a.Hs ? 4u * a.Ws : 0u;
+    r[0] = bload(rin, ok ? o : kOOB);
+    r[1] = bload(rin, ok ? o + dx : kOOB);
+    r[2] = bload(rin, ok ? o + dy : kOOB);
+    r[3] = bload(rin, ok ? o + dx + dy : kOOB);
+  } else if constexpr (INOP == RPST_IN_UPSAMPLE2) {
+    r[0] = bload(rin, ok ? pbyte + (unsigned)((yr >> 1) * a.Ws + (xr >> 1)) * 4u : kOOB);
+  } else if constexpr (INOP == RPST_IN_ADD_UPSAMPLE2) {
+    r[0] = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
+    r[1] = bload(raux, ok ? abyte + (unsigned)((yr >> 1) * (a.W >> 1) + (xr >> 1)) * 4u : kOOB);
+  } else {  // RPST_IN_NONE and RPST_IN_ADAIN
+    r[0] = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
   }
 }
 
-// AdaIN on load (RPST_IN_ADAIN): ((v - mean_c) / std_c) * std_s + mean_s, rounded like the
-// stand-alone apply kernel (no contraction). aux = [mean_c | mean_s | std_c | std_s], each
-// N*Cin floats.
+// AdaIN on load (RPST_IN_ADAIN): ((v - mean_c) / std_c) * std_s + mean_s per (n, ci),
+// evaluated as fma(v - mean_c, std_s / std_c, mean_s). aux = [mean_c|mean_s|std_c|std_s],
+// each N*Cin floats.
 struct AdainP {
-  float mc, ms, sc, ss;
+  float mc, scale, ms;
 };
 __device__ __forceinline__ AdainP adain_params(const float* __restrict__ aux, int n, int ci,
                                                const ConvArgs& a) {
   const int64_t nc = (int64_t)a.N * a.Cin;
   const int64_t i = (int64_t)n * a.Cin + (ci < a.Cin ? ci : 0);
-  return {aux[i], aux[nc + i], aux[2 * nc + i], aux[3 * nc + i]};
+  return {aux[i], aux[3 * nc + i] / aux[2 * nc + i], aux[nc + i]};
 }
-__device__ __forceinline__ float adain_apply(float v, const AdainP& p) {
-  return __fadd_rn(__fmul_rn(__fdiv_rn(__fsub_rn(v, p.mc), p.sc), p.ss), p.ms);
+
+template <int INOP>
+__device__ __forceinline__ float combine(const float (&r)[RawN<INOP>::R], bool ok,
+                                         const AdainP& p) {
+  if constexpr (INOP == RPST_IN_MAXPOOL2) return fmaxf(fmaxf(r[0], r[1]), fmaxf(r[2], r[3]));
+  else if constexpr (INOP == RPST_IN_ADD_UPSAMPLE2) return r[0] + r[1];
+  else if constexpr (INOP == RPST_IN_ADAIN) return ok ? fmaf(r[0] - p.mc, p.scale, p.ms) : 0.f;
+  else return r[0];
 }
 
 // CKK = input channels per kernel chunk (divides the packing chunk K::CK);
@@ -230,8 +243,10 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
 
+  constexpr int R = RawN<INOP>::R;
   u32x4 wreg[WLD];
-  float xreg[CPT][XN];
+  float xraw[CPT][XN][R];
+  AdainP ap[CPT];
 
 #define RPST_CONV_LOAD(c)                                                                   \
   {                                                                                         \
@@ -246,22 +261,15 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
     _Pragma("unroll") for (int q = 0; q < CPT; ++q) {                                       \
       const unsigned ch = (unsigned)((c) * CK + cg + CGS * q);                              \
       const unsigned pb = ch * in_plane * 4u, ab = ch * aux_plane * 4u;                     \
-      const bool chok = (int)ch < a.Cin;                                                    \
-      AdainP ap{0.f, 0.f, 1.f, 1.f};                                                        \
-      if (INOP == RPST_IN_ADAIN) ap = adain_params(a.aux, n, (int)ch, a);                   \
+      if (INOP == RPST_IN_ADAIN) ap[q] = adain_params(a.aux, n, (int)ch, a);                \
       _Pragma("unroll") for (int i = 0; i < RPT; ++i) {                                     \
         const int py = rs * RPT + i;                                                        \
         int y = y0 - OFF + py;                                                              \
         const bool yok = resolve(y, a.H, a.pad, KS == 3) && py < PH;                        \
-        float v = fetch<INOP>(rin, raux, pb, ab, y, bx, yok && bx_ok, a);                   \
-        if (INOP == RPST_IN_ADAIN) v = (yok && bx_ok && chok) ? adain_apply(v, ap) : 0.f;   \
-        xreg[q][i] = v;                                                                     \
+        fetch_raw<INOP>(xraw[q][i], rin, raux, pb, ab, y, bx, yok && bx_ok, a);             \
       }                                                                                     \
-      _Pragma("unroll") for (int e = 0; e < HALO; ++e) {                                    \
-        float v = fetch<INOP>(rin, raux, pb, ab, hy[e], hx[e], h_ok[e], a);                 \
-        if (INOP == RPST_IN_ADAIN) v = (h_ok[e] && chok) ? adain_apply(v, ap) : 0.f;        \
-        xreg[q][RPT + e] = v;                                                               \
-      }                                                                                     \
+      _Pragma("unroll") for (int e = 0; e < HALO; ++e)                                      \
+        fetch_raw<INOP>(xraw[q][RPT + e], rin, raux, pb, ab, hy[e], hx[e], h_ok[e], a);     \
     }                                                                                       \
   }
 
@@ -280,15 +288,23 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
     for (int q = 0; q < CPT; ++q) {
       float* xs = Xs + (cg + CGS * q) * PH * PW;
+      const bool chok = (int)(c * CK + cg + CGS * q) < a.Cin;
 #pragma unroll
       for (int i = 0; i < RPT; ++i) {
         const int py = rs * RPT + i;
-        if ((PH % RS) == 0 || py < PH) xs[py * PW + jc + OFF] = xreg[q][i];
+        bool ok = chok && bx_ok;
+        if (INOP == RPST_IN_ADAIN) {
+          int y = y0 - OFF + py;
+          ok = ok && resolve(y, a.H, a.pad, KS == 3);
+        }
+        const float v = combine<INOP>(xraw[q][i], ok, ap[q]);
+        if ((PH % RS) == 0 || py < PH) xs[py * PW + jc + OFF] = v;
       }
 #pragma unroll
       for (int e = 0; e < HALO; ++e) {
         const int hi = jc + 32 * (rs + RS * e);
-        if (has_halo[e]) xs[(hi >> 1) * PW + ((hi & 1) ? PW - 1 : 0)] = xreg[q][RPT + e];
+        const float v = combine<INOP>(xraw[q][RPT + e], chok && h_ok[e], ap[q]);
+        if (has_halo[e]) xs[(hi >> 1) * PW + ((hi & 1) ? PW - 1 : 0)] = v;
       }
     }
     __syncthreads();
@@ -470,7 +486,21 @@ static void launch_conv(const ConvArgs& a, int BM, int variant, hipStream_t st) 
 #define RPST_LAUNCH(BM_, TH_, WM_, WN_, NTH_, CK_, DB_) \
   conv_mfma_kernel<KS, BM_, TH_, WM_, WN_, INOP, NTH_, CK_, DB_><<<blocks, NTH_, 0, st>>>(a)
   constexpr int C8 = ConvK<KS>::CK, C4 = ConvK<KS>::CK / 2;
-  if (BM == 128) {
+  // loaders with 2-4 raw loads per element only get the short-tile variants (the tall
+  // ones run out of registers)
+  constexpr bool HEAVY = INOP == RPST_IN_MAXPOOL2 || INOP == RPST_IN_ADD_UPSAMPLE2;
+  if (HEAVY) {
+    if (BM == 128) {
+      if (variant == 4) RPST_LAUNCH(128, 4, 2, 2, 256, C4, true);
+      else RPST_LAUNCH(128, 4, 2, 2, 256, C8, false);
+    } else if (BM == 64) {
+      if (variant == 0) RPST_LAUNCH(64, 8, 1, 4, 256, C8, false);
+      else RPST_LAUNCH(64, 8, 1, 4, 256, C4, true);
+    } else {
+      if (variant == 2) RPST_LAUNCH(32, 8, 1, 4, 256, C8, false);
+      else RPST_LAUNCH(32, 8, 1, 4, 256, C4, true);
+    }
+  } else if (BM == 128) {
     switch (variant) {
       case 0: RPST_LAUNCH(128, 8, 2, 4, 512, C8, false); break;
       case 2: RPST_LAUNCH(128, 4, 2, 2, 256, C8, false); break;
@@ -494,8 +524,12 @@ static void launch_conv(const ConvArgs& a, int BM, int variant, hipStream_t st) 
 #undef RPST_LAUNCH
 }
 
+static bool heavy_loader(int in_op) {
+  return in_op == RPST_IN_MAXPOOL2 || in_op == RPST_IN_ADD_UPSAMPLE2;
+}
+
 static int pick_variant(int BM, int ksize, int in_op) {
-  if (BM == 128 && (in_op == RPST_IN_MAXPOOL2 || ksize == 1)) return 2;
+  if (BM == 128 && (heavy_loader(in_op) || ksize == 1)) return 2;
   return 1;
 }
 
@@ -520,7 +554,13 @@ static int variant_wn(int BM, int variant) {
 
 static int conv_variant(int BM, int ksize, int in_op) {
   const char* e = getenv("RPST_CONV_VARIANT");
-  return (e && *e) ? atoi(e) : pick_variant(BM, ksize, in_op);
+  int v = (e && *e) ? atoi(e) : pick_variant(BM, ksize, in_op);
+  if (heavy_loader(in_op)) {  // the variants launch_conv instantiates for heavy loaders
+    if (BM == 128) v = (v == 4) ? 4 : 2;
+    else if (BM == 64) v = (v == 0) ? 0 : 1;
+    else v = (v == 2) ? 2 : 1;
+  }
+  return v;
 }
 
 }  // namespace rpst

@@ -24,6 +24,9 @@ ADAIN = [  # (N, Cin, Hs, Ws, Cout, k, pad, in_op)
     (32, 128, 512, 512, 64, 3, 0, 0), (32, 64, 512, 512, 32, 3, 0, 0),
     (32, 32, 512, 512, 16, 3, 0, 0), (32, 16, 512, 512, 3, 3, 0, 0),
 ]
+FUSED = [  # AdaIN-in-loader decoder conv (in_op 4) of the fused AdaIN-RP path
+    (32, 256, 512, 512, 128, 3, 0, 4),
+]
 VGG = [
     (64, 64, 512, 512, 64, 3, 1, 0), (64, 64, 512, 512, 128, 3, 1, 1),
     (64, 128, 256, 256, 128, 3, 1, 0), (64, 128, 256, 256, 256, 3, 1, 1),
@@ -43,7 +46,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
-    layers = {"adain": ADAIN, "vgg": VGG, "all": ADAIN + VGG}[args.layers]
+    layers = {"adain": ADAIN, "vgg": VGG, "fused": FUSED, "all": ADAIN + FUSED + VGG}[args.layers]
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     results = []
@@ -52,6 +55,10 @@ def main():
         w = (torch.rand((cout, cin, k, k), device=dev, generator=g) - 0.5) * 0.1
         b = torch.rand((cout,), device=dev, generator=g) * 0.1
         p = ops.pack_conv_weight(w)
+        aux = None
+        if in_op == 4:
+            aux = torch.cat([torch.rand(2 * n * cin, device=dev, generator=g),
+                             torch.rand(2 * n * cin, device=dev, generator=g) + 0.5])
         h, wd = ops.conv_out_hw(hs, ws, in_op)
         flops = 2.0 * n * cout * h * wd * cin * k * k
         times = {v: [] for v in VARIANTS[bm_of(cout)]}
@@ -59,7 +66,7 @@ def main():
         for rnd in range(args.rounds):
             for v in times:
                 os.environ["RPST_CONV_VARIANT"] = str(v)
-                out = ops.conv2d(x, p, b, cout, k, pad=pad, in_op=in_op, relu=True)
+                out = ops.conv2d(x, p, b, cout, k, pad=pad, in_op=in_op, relu=True, aux=aux)
                 if ref is None:
                     ref = out.clone()
                 elif rnd == 0:  # chunk size changes the K summation order: tolerance
@@ -69,7 +76,7 @@ def main():
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(args.reps):
-                    ops.conv2d(x, p, b, cout, k, pad=pad, in_op=in_op, relu=True, out=out)
+                    ops.conv2d(x, p, b, cout, k, pad=pad, in_op=in_op, relu=True, aux=aux, out=out)
                 e1.record()
                 torch.cuda.synchronize()
                 times[v].append(e0.elapsed_time(e1) / args.reps)
