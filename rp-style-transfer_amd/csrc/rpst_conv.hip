@@ -489,7 +489,7 @@ static void launch_conv(const ConvArgs& a, int BM, int variant, hipStream_t st) 
   // loaders with 2-4 raw loads per element only get the short-tile variants (the tall
   // ones run out of registers)
   constexpr bool HEAVY = INOP == RPST_IN_MAXPOOL2 || INOP == RPST_IN_ADD_UPSAMPLE2;
-  if (HEAVY) {
+  if constexpr (HEAVY) {
     if (BM == 128) {
       if (variant == 4) RPST_LAUNCH(128, 4, 2, 2, 256, C4, true);
       else RPST_LAUNCH(128, 4, 2, 2, 256, C8, false);
@@ -500,7 +500,8 @@ static void launch_conv(const ConvArgs& a, int BM, int variant, hipStream_t st) 
       if (variant == 2) RPST_LAUNCH(32, 8, 1, 4, 256, C8, false);
       else RPST_LAUNCH(32, 8, 1, 4, 256, C4, true);
     }
-  } else if (BM == 128) {
+  } else {
+  if (BM == 128) {
     switch (variant) {
       case 0: RPST_LAUNCH(128, 8, 2, 4, 512, C8, false); break;
       case 2: RPST_LAUNCH(128, 4, 2, 2, 256, C8, false); break;
@@ -520,6 +521,7 @@ static void launch_conv(const ConvArgs& a, int BM, int variant, hipStream_t st) 
       case 2: RPST_LAUNCH(32, 8, 1, 4, 256, C8, false); break;
       default: RPST_LAUNCH(32, 8, 1, 4, 256, C4, true);
     }
+  }
   }
 #undef RPST_LAUNCH
 }
