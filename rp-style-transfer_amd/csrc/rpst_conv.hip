@@ -134,6 +134,24 @@ __device__ __forceinline__ float combine(const float (&r)[RawN<INOP>::R], bool o
   else return r[0];
 }
 
+// Sum each of v[0..15] over the 32 lanes of a half-wave. Returns the total of element
+// e = (j >> 1) & 15 (lanes 2e and 2e+1 of the half hold it); 16 shuffles instead of 80.
+__device__ __forceinline__ float halfwave_reduce_scatter16(float (&v)[16], int j) {
+  float w[8], u[4], t[2];
+  bool b = (j & 16) != 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = (b ? v[i + 8] : v[i]) + __shfl_xor(b ? v[i] : v[i + 8], 16, 64);
+  b = (j & 8) != 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) u[i] = (b ? w[i + 4] : w[i]) + __shfl_xor(b ? w[i] : w[i + 4], 8, 64);
+  b = (j & 4) != 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) t[i] = (b ? u[i + 2] : u[i]) + __shfl_xor(b ? u[i] : u[i + 2], 4, 64);
+  b = (j & 2) != 0;
+  float s = (b ? t[1] : t[0]) + __shfl_xor(b ? t[0] : t[1], 2, 64);
+  return s + __shfl_xor(s, 1, 64);
+}
+
 // CKK = input channels per kernel chunk (divides the packing chunk K::CK);
 // DB = double-buffered LDS (one barrier per chunk instead of two).
 template <int KS, int BM, int TH, int WM, int WN, int INOP, int NTH, int CKK, bool DB>
@@ -358,8 +376,10 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
   }
 
   // optional output statistics (AdaIN / calc_mean_std of this layer's output, fused):
-  // each half-wave holds one output channel's 32 x NT pixels of this tile -> (mean, M2)
-  // over the valid ones; merged in fp64 by stat_merge_kernel.
+  // each half-wave holds 16 output channels (r) x NT rows x 32 columns of this tile per
+  // mt. Two-pass per channel: sums via a half-wave reduce-scatter (16 shuffles for 16
+  // values), means broadcast back, centred sums of squares the same way -> (mean, M2)
+  // per (channel, wave tile), merged in fp64 by stat_merge_kernel.
   // (compiled only for tiles with >= 4 rows per wave: with NT <= 2 hipcc keeps the
   // accumulators dynamically indexed and spills thousands of VGPRs)
   if constexpr (NT >= 4) if (a.stat_part) {
@@ -369,29 +389,33 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
     const float inv = cnt > 0 ? 1.f / (float)cnt : 0.f;
     const bool xv = x < a.W;
     const int pidx = (ty * a.tiles_x + tx) * WN + wn;
+    const int e = (j >> 1) & 15;  // channel index r this lane ends up holding
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
+      float v[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int co = co0 + wm * WTM + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        float s1 = 0.f;
+        float t = 0.f;
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-          s1 += (xv && nt < rows) ? acc[mt][nt][r] : 0.f;
+        for (int nt = 0; nt < NT; ++nt) t += (xv && nt < rows) ? acc[mt][nt][r] : 0.f;
+        v[r] = t;
+      }
+      const float mean = halfwave_reduce_scatter16(v, j) * inv;
 #pragma unroll
-        for (int o = 16; o > 0; o >>= 1) s1 += __shfl_xor(s1, o, 64);  // within the half-wave
-        const float mean = s1 * inv;
-        float s2 = 0.f;
+      for (int r = 0; r < 16; ++r) {
+        const float mr = __shfl(mean, (h << 5) + 2 * r, 64);
+        float t = 0.f;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
-          const float d = acc[mt][nt][r] - mean;
-          s2 += (xv && nt < rows) ? d * d : 0.f;
+          const float d = acc[mt][nt][r] - mr;
+          t += (xv && nt < rows) ? d * d : 0.f;
         }
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
-        if (j == 0 && co < a.Cout)
-          a.stat_part[((int64_t)n * a.Cout + co) * a.stat_P + pidx] = make_float2(mean, s2);
+        v[r] = t;
       }
+      const float m2 = halfwave_reduce_scatter16(v, j);
+      const int co = co0 + wm * WTM + mt * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if ((j & 1) == 0 && co < a.Cout)
+        a.stat_part[((int64_t)n * a.Cout + co) * a.stat_P + pidx] = make_float2(mean, m2);
     }
   }
 }
