@@ -119,7 +119,7 @@ def roofline_from_trace(summary):
     from rpst import _lib
     best = None
     for name, a in summary.items():
-        if not name.startswith("conv"):
+        if not name.startswith(("conv", "wino")):
             continue
         if best is None or a["ms"] > best[1]["ms"]:
             best = (name, a)
@@ -127,7 +127,13 @@ def roofline_from_trace(summary):
         return None
     name, a = best
     avg_ms = a["ms"] / a["launches"]
-    achieved = a["flops"] / (avg_ms * 1e-3) / 1e12
+    wino = name.startswith("wino")
+    # Winograd F(2x2,3x3) performs 16 instead of 36 multiply-adds per 2x2 output tile and
+    # (ci, co): its algorithmic FLOPs are 4/9 of the direct convolution's. "achieved" is
+    # priced on the algorithm that ran; "effective" on the direct-convolution FLOPs.
+    flop = a["flops"] * (4.0 / 9.0 if wino else 1.0)
+    achieved = flop / (avg_ms * 1e-3) / 1e12
+    effective = a["flops"] / (avg_ms * 1e-3) / 1e12
     # "conv3x3 128->256 512x512 N64 op0" -> launch geometry -> PMC record
     k, chans, hw, nn, op = name.split()
     cin, cout = (int(v) for v in chans.split("->"))
@@ -135,11 +141,14 @@ def roofline_from_trace(summary):
     n, in_op, ks = int(nn[1:]), int(op[2:]), int(k[4])
     hs, ws = ((h * 2, w * 2) if in_op == 1 else ((h // 2, w // 2) if in_op == 2 else (h, w)))
     grid = _lib.load().rpst_conv2d_grid_threads(n, hs, ws, cout, ks, in_op)
-    traffic = pmc_lookup("conv_mfma_kernel", grid)
+    kname = "wino_mfma_kernel" if wino else "conv_mfma_kernel"
+    traffic = pmc_lookup(kname, grid)
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-            "traffic": traffic, "kernel": f"conv_mfma_kernel [{name}]",
-            "launch_ms": round(avg_ms, 4), "flop_per_launch": a["flops"],
+            "traffic": traffic, "kernel": f"{kname} [{name}]",
+            "algorithm": "winograd F(2x2,3x3) fp32" if wino else "direct implicit GEMM fp32",
+            "effective_tflops": round(effective, 2),
+            "launch_ms": round(avg_ms, 4), "flop_per_launch": flop,
             "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None}
 
 

@@ -1,0 +1,159 @@
+// Shared pieces of the conv kernels (direct implicit GEMM in rpst_conv.hip, Winograd
+// F(2x2,3x3) in rpst_wino.hip): launch arguments, padding resolution, buffer loads and
+// the fused input operators of the tile loaders.
+#pragma once
+
+#include "rpst_common.h"
+
+namespace rpst {
+
+constexpr int kTW = 32;  // pixels per N sub-tile = one row segment
+
+struct ConvArgs {
+  const float* in;
+  const float* aux;
+  const float* wpk;
+  const float* bias;
+  const float* res;
+  float* out;
+  int N, Cin, Hs, Ws, H, W, Cout, Cout_pad, nchunks;
+  int tiles_x, tiles_y, co_tiles;
+  int pad, relu;
+  float2* stat_part;  // optional: per-(n, co, wave tile) (mean, M2) of the output
+  int stat_P;         // partials per (n, co) = tiles_x * tiles_y * WN
+};
+
+template <int KS>
+struct ConvK {
+  static constexpr int CK = (KS == 3) ? 8 : 16;  // input channels per chunk
+  static constexpr int TAPS = KS * KS;
+  static constexpr int KCH = TAPS * CK;  // K values per chunk
+};
+
+// Resolve a logical (post-in_op) coordinate against padding. Returns false for a zero
+// pad position. Tile overhang beyond the image is clamped (its results are discarded).
+__device__ __forceinline__ bool resolve(int& v, int n, int pad, bool padded) {
+  if (padded) {
+    if (pad == RPST_PAD_ZERO) {
+      if (v < 0 || v >= n) return false;
+    } else {
+      v = reflect1(v, n);
+    }
+  }
+  v = v < 0 ? 0 : (v >= n ? n - 1 : v);
+  return true;
+}
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// Byte offset the buffer unit treats as out of range (returns 0, no fault): every
+// descriptor below has num_records < 2^31.
+constexpr unsigned kOOB = 0x80000000u;
+
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+
+// Raw global loads per patch element for each input operator; they are combined into
+// the element value only when the chunk is written to LDS (after the current chunk's
+// MFMAs), so no wait for the loads sits in front of the compute phase.
+template <int INOP>
+struct RawN {
+  static constexpr int R = INOP == RPST_IN_MAXPOOL2 ? 4 : (INOP == RPST_IN_ADD_UPSAMPLE2 ? 2 : 1);
+};
+
+// Issue the loads of one element: logical (post-in_op) resolved row yr / column xr of the
+// plane at byte offset `pbyte` (image-relative). ok == false -> zero (pad position /
+// padded channel): every load goes out of range and returns 0.
+template <int INOP>
+__device__ __forceinline__ void fetch_raw(float (&r)[RawN<INOP>::R], __amdgpu_buffer_rsrc_t rin,
+                                          __amdgpu_buffer_rsrc_t raux, unsigned pbyte,
+                                          unsigned abyte, int yr, int xr, bool ok,
+                                          const ConvArgs& a) {
+  if constexpr (INOP == RPST_IN_MAXPOOL2) {
+    // 2x2 window of the source; missing right/bottom neighbours (ceil mode) re-read the
+    // top-left element so the max is unaffected
+    const int sy = 2 * yr, sx = 2 * xr;
+    const unsigned o = pbyte + (unsigned)(sy * a.Ws + sx) * 4u;
+    const unsigned dx = sx + 1 < a.Ws ? 4u : 0u, dy = sy + 1 < a.Hs ? 4u * a.Ws : 0u;
+    r[0] = bload(rin, ok ? o : kOOB);
+    r[1] = bload(rin, ok ? o + dx : kOOB);
+    r[2] = bload(rin, ok ? o + dy : kOOB);
+    r[3] = bload(rin, ok ? o + dx + dy : kOOB);
+  } else if constexpr (INOP == RPST_IN_UPSAMPLE2) {
+    r[0] = bload(rin, ok ? pbyte + (unsigned)((yr >> 1) * a.Ws + (xr >> 1)) * 4u : kOOB);
+  } else if constexpr (INOP == RPST_IN_ADD_UPSAMPLE2) {
+    r[0] = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
+    r[1] = bload(raux, ok ? abyte + (unsigned)((yr >> 1) * (a.W >> 1) + (xr >> 1)) * 4u : kOOB);
+  } else {  // RPST_IN_NONE and RPST_IN_ADAIN
+    r[0] = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
+  }
+}
+
+// AdaIN on load (RPST_IN_ADAIN): ((v - mean_c) / std_c) * std_s + mean_s per (n, ci),
+// evaluated as fma(v - mean_c, std_s / std_c, mean_s). aux = [mean_c|mean_s|std_c|std_s],
+// each N*Cin floats.
+struct AdainP {
+  float mc, scale, ms;
+};
+__device__ __forceinline__ AdainP adain_params(const float* __restrict__ aux, int n, int ci,
+                                               const ConvArgs& a) {
+  const int64_t nc = (int64_t)a.N * a.Cin;
+  const int64_t i = (int64_t)n * a.Cin + (ci < a.Cin ? ci : 0);
+  return {aux[i], aux[3 * nc + i] / aux[2 * nc + i], aux[nc + i]};
+}
+
+template <int INOP>
+__device__ __forceinline__ float combine(const float (&r)[RawN<INOP>::R], bool ok,
+                                         const AdainP& p) {
+  if constexpr (INOP == RPST_IN_MAXPOOL2) return fmaxf(fmaxf(r[0], r[1]), fmaxf(r[2], r[3]));
+  else if constexpr (INOP == RPST_IN_ADD_UPSAMPLE2) return r[0] + r[1];
+  else if constexpr (INOP == RPST_IN_ADAIN) return ok ? fmaf(r[0] - p.mc, p.scale, p.ms) : 0.f;
+  else return r[0];
+}
+
+// Sum each of v[0..15] over the 32 lanes of a half-wave. Returns the total of element
+// e = (j >> 1) & 15 (lanes 2e and 2e+1 of the half hold it); 16 shuffles instead of 80.
+__device__ __forceinline__ float halfwave_reduce_scatter16(float (&v)[16], int j) {
+  float w[8], u[4], t[2];
+  bool b = (j & 16) != 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = (b ? v[i + 8] : v[i]) + __shfl_xor(b ? v[i] : v[i + 8], 16, 64);
+  b = (j & 8) != 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) u[i] = (b ? w[i + 4] : w[i]) + __shfl_xor(b ? w[i] : w[i + 4], 8, 64);
+  b = (j & 4) != 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) t[i] = (b ? u[i + 2] : u[i]) + __shfl_xor(b ? u[i] : u[i + 2], 4, 64);
+  b = (j & 2) != 0;
+  float s = (b ? t[1] : t[0]) + __shfl_xor(b ? t[0] : t[1], 2, 64);
+  return s + __shfl_xor(s, 1, 64);
+}
+
+// Sum each of v[0..7] over the 32 lanes of a half-wave. Returns the total of element
+// e = (j >> 2) & 7 (lanes 4e..4e+3 of the half hold it).
+__device__ __forceinline__ float halfwave_reduce_scatter8(float (&v)[8], int j) {
+  float u[4], t[2];
+  bool b = (j & 16) != 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) u[i] = (b ? v[i + 4] : v[i]) + __shfl_xor(b ? v[i] : v[i + 4], 16, 64);
+  b = (j & 8) != 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) t[i] = (b ? u[i + 2] : u[i]) + __shfl_xor(b ? u[i] : u[i + 2], 8, 64);
+  b = (j & 4) != 0;
+  float s = (b ? t[1] : t[0]) + __shfl_xor(b ? t[0] : t[1], 4, 64);
+  s += __shfl_xor(s, 2, 64);
+  return s + __shfl_xor(s, 1, 64);
+}
+
+// ---- Winograd F(2x2,3x3) path (rpst_wino.hip) ----------------------------------------
+constexpr int kWinoBM = 64;    // output channels per block
+constexpr int kWinoTH = 4;     // output rows per block (x kTW columns)
+constexpr int kWinoNTH = 256;  // threads per block
+// floats of the Winograd weight image (stored after the direct image for 3x3 convs)
+size_t wino_packed_floats(int Cout, int Cin);
+int wino_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);
+// a: shape/operator fields filled in, a.wpk = the Winograd weight image. Sets the tiling
+// fields (Cout_pad, nchunks, tiles_*, co_tiles, stat_P) and launches.
+int wino_launch(ConvArgs& a, int in_op, hipStream_t st);
+
+}  // namespace rpst

@@ -24,133 +24,11 @@
 // Patch loader: thread -> (channel group tid>>5, column tid&31), so each half-wave reads
 // a 128-B row segment and all row index math is wave-uniform (scalar).
 // Numerics: exact fp32 products, fp32 accumulation (MFMA = k-ordered fmaf chain).
-#include "rpst_common.h"
+#include "rpst_conv.h"
 
 #include <cstdlib>
 
 namespace rpst {
-
-constexpr int kTW = 32;  // pixels per N sub-tile = one row segment
-
-struct ConvArgs {
-  const float* in;
-  const float* aux;
-  const float* wpk;
-  const float* bias;
-  const float* res;
-  float* out;
-  int N, Cin, Hs, Ws, H, W, Cout, Cout_pad, nchunks;
-  int tiles_x, tiles_y, co_tiles;
-  int pad, relu;
-  float2* stat_part;  // optional: per-(n, co, wave tile) (mean, M2) of the output
-  int stat_P;         // partials per (n, co) = tiles_x * tiles_y * WN
-};
-
-template <int KS>
-struct ConvK {
-  static constexpr int CK = (KS == 3) ? 8 : 16;  // input channels per chunk
-  static constexpr int TAPS = KS * KS;
-  static constexpr int KCH = TAPS * CK;  // K values per chunk
-};
-
-// Resolve a logical (post-in_op) coordinate against padding. Returns false for a zero
-// pad position. Tile overhang beyond the image is clamped (its results are discarded).
-__device__ __forceinline__ bool resolve(int& v, int n, int pad, bool padded) {
-  if (padded) {
-    if (pad == RPST_PAD_ZERO) {
-      if (v < 0 || v >= n) return false;
-    } else {
-      v = reflect1(v, n);
-    }
-  }
-  v = v < 0 ? 0 : (v >= n ? n - 1 : v);
-  return true;
-}
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-// Byte offset the buffer unit treats as out of range (returns 0, no fault): every
-// descriptor below has num_records < 2^31.
-constexpr unsigned kOOB = 0x80000000u;
-
-__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
-}
-
-// Raw global loads per patch element for each input operator; they are combined into
-// the element value only when the chunk is written to LDS (after the current chunk's
-// MFMAs), so no wait for the loads sits in front of the compute phase.
-template <int INOP>
-struct RawN {
-  static constexpr int R = INOP == RPST_IN_MAXPOOL2 ? 4 : (INOP == RPST_IN_ADD_UPSAMPLE2 ? 2 : 1);
-};
-
-// Issue the loads of one element: logical (post-in_op) resolved row yr / column xr of the
-// plane at byte offset `pbyte` (image-relative). ok == false -> zero (pad position /
-// padded channel): every load goes out of range and returns 0.
-template <int INOP>
-__device__ __forceinline__ void fetch_raw(float (&r)[RawN<INOP>::R], __amdgpu_buffer_rsrc_t rin,
-                                          __amdgpu_buffer_rsrc_t raux, unsigned pbyte,
-                                          unsigned abyte, int yr, int xr, bool ok,
-                                          const ConvArgs& a) {
-  if constexpr (INOP == RPST_IN_MAXPOOL2) {
-    // 2x2 window of the source; missing right/bottom neighbours (ceil mode) re-read the
-    // top-left element so the max is unaffected
-    const int sy = 2 * yr, sx = 2 * xr;
-    const unsigned o = pbyte + (unsigned)(sy * a.Ws + sx) * 4u;
-    const unsigned dx = sx + 1 < a.Ws ? 4u : 0u, dy = sy + 1 < a.Hs ? 4u * a.Ws : 0u;
-    r[0] = bload(rin, ok ? o : kOOB);
-    r[1] = bload(rin, ok ? o + dx : kOOB);
-    r[2] = bload(rin, ok ? o + dy : kOOB);
-    r[3] = bload(rin, ok ? o + dx + dy : kOOB);
-  } else if constexpr (INOP == RPST_IN_UPSAMPLE2) {
-    r[0] = bload(rin, ok ? pbyte + (unsigned)((yr >> 1) * a.Ws + (xr >> 1)) * 4u : kOOB);
-  } else if constexpr (INOP == RPST_IN_ADD_UPSAMPLE2) {
-    r[0] = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
-    r[1] = bload(raux, ok ? abyte + (unsigned)((yr >> 1) * (a.W >> 1) + (xr >> 1)) * 4u : kOOB);
-  } else {  // RPST_IN_NONE and RPST_IN_ADAIN
-    r[0] = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
-  }
-}
-
-// AdaIN on load (RPST_IN_ADAIN): ((v - mean_c) / std_c) * std_s + mean_s per (n, ci),
-// evaluated as fma(v - mean_c, std_s / std_c, mean_s). aux = [mean_c|mean_s|std_c|std_s],
-// each N*Cin floats.
-struct AdainP {
-  float mc, scale, ms;
-};
-__device__ __forceinline__ AdainP adain_params(const float* __restrict__ aux, int n, int ci,
-                                               const ConvArgs& a) {
-  const int64_t nc = (int64_t)a.N * a.Cin;
-  const int64_t i = (int64_t)n * a.Cin + (ci < a.Cin ? ci : 0);
-  return {aux[i], aux[3 * nc + i] / aux[2 * nc + i], aux[nc + i]};
-}
-
-template <int INOP>
-__device__ __forceinline__ float combine(const float (&r)[RawN<INOP>::R], bool ok,
-                                         const AdainP& p) {
-  if constexpr (INOP == RPST_IN_MAXPOOL2) return fmaxf(fmaxf(r[0], r[1]), fmaxf(r[2], r[3]));
-  else if constexpr (INOP == RPST_IN_ADD_UPSAMPLE2) return r[0] + r[1];
-  else if constexpr (INOP == RPST_IN_ADAIN) return ok ? fmaf(r[0] - p.mc, p.scale, p.ms) : 0.f;
-  else return r[0];
-}
-
-// Sum each of v[0..15] over the 32 lanes of a half-wave. Returns the total of element
-// e = (j >> 1) & 15 (lanes 2e and 2e+1 of the half hold it); 16 shuffles instead of 80.
-__device__ __forceinline__ float halfwave_reduce_scatter16(float (&v)[16], int j) {
-  float w[8], u[4], t[2];
-  bool b = (j & 16) != 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) w[i] = (b ? v[i + 8] : v[i]) + __shfl_xor(b ? v[i] : v[i + 8], 16, 64);
-  b = (j & 8) != 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) u[i] = (b ? w[i + 4] : w[i]) + __shfl_xor(b ? w[i] : w[i + 4], 8, 64);
-  b = (j & 4) != 0;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) t[i] = (b ? u[i + 2] : u[i]) + __shfl_xor(b ? u[i] : u[i + 2], 4, 64);
-  b = (j & 2) != 0;
-  float s = (b ? t[1] : t[0]) + __shfl_xor(b ? t[0] : t[1], 2, 64);
-  return s + __shfl_xor(s, 1, 64);
-}
 
 // CKK = input channels per kernel chunk (divides the packing chunk K::CK);
 // DB = double-buffered LDS (one barrier per chunk instead of two).
@@ -589,35 +467,93 @@ static int conv_variant(int BM, int ksize, int in_op) {
   return v;
 }
 
+// Algorithm for a 3x3 conv: Winograd F(2x2,3x3) (rpst_wino.hip) where it pays, else the
+// direct implicit GEMM. RPST_CONV_ALGO=direct|winograd overrides (tests, A/B benches).
+static bool use_winograd(int Cout, int ksize) {
+  if (ksize != 3) return false;
+  const char* e = getenv("RPST_CONV_ALGO");
+  if (e && *e) {
+    if (e[0] == 'd') return false;
+    if (e[0] == 'w') return true;
+  }
+  return Cout >= 64;
+}
+
+static void logical_hw(int Hs, int Ws, int in_op, int* H, int* W) {
+  *H = Hs;
+  *W = Ws;
+  if (in_op == RPST_IN_MAXPOOL2) {
+    *H = (Hs + 1) / 2;
+    *W = (Ws + 1) / 2;
+  } else if (in_op == RPST_IN_UPSAMPLE2) {
+    *H = 2 * Hs;
+    *W = 2 * Ws;
+  }
+}
+
+// Launch geometry shared by the entry points: blocks, threads per block, statistics
+// partials per plane and their (rows per partial, partials per tile row) layout.
+struct ConvGeom {
+  bool wino;
+  int64_t blocks;
+  int nth, stat_P, stat_nt, stat_wn, tiles_x;
+};
+
+static ConvGeom conv_geom(int N, int Hs, int Ws, int Cout, int ksize, int in_op) {
+  int H, W;
+  logical_hw(Hs, Ws, in_op, &H, &W);
+  ConvGeom g{};
+  g.tiles_x = (W + kTW - 1) / kTW;
+  if (use_winograd(Cout, ksize)) {
+    const int ty = (H + kWinoTH - 1) / kWinoTH;
+    g.wino = true;
+    g.blocks = (int64_t)g.tiles_x * ty * N * ((Cout + kWinoBM - 1) / kWinoBM);
+    g.nth = kWinoNTH;
+    g.stat_P = g.tiles_x * ty;
+    g.stat_nt = kWinoTH;
+    g.stat_wn = 1;
+    return g;
+  }
+  const TileCfg cfg = pick_cfg(Cout);
+  const int variant = conv_variant(cfg.BM, ksize, in_op);
+  const int th = variant_th(cfg.BM, variant), wn = variant_wn(cfg.BM, variant);
+  const int ty = (H + th - 1) / th;
+  g.blocks = (int64_t)g.tiles_x * ty * N * (pad_cout(Cout) / cfg.BM);
+  g.nth = variant_nth(cfg.BM, variant);
+  g.stat_P = g.tiles_x * ty * wn;
+  g.stat_nt = th / wn;
+  g.stat_wn = wn;
+  return g;
+}
+
+static size_t direct_packed_floats(int Cout, int Cin, int ksize) {
+  const int ck = ck_of(ksize);
+  const size_t nch = (size_t)(Cin + ck - 1) / ck;
+  return nch * ksize * ksize * ck * (size_t)pad_cout(Cout);
+}
+
 }  // namespace rpst
 
 using namespace rpst;
 
+// 3x3 weights are packed twice: the direct image followed by the Winograd image (the
+// algorithm is chosen per launch; both are small).
 extern "C" size_t rpst_conv2d_packed_size(int Cout, int Cin, int ksize) {
   if (Cout <= 0 || Cin <= 0 || (ksize != 1 && ksize != 3)) return 0;
-  const int ck = ck_of(ksize);
-  const size_t nch = (size_t)(Cin + ck - 1) / ck;
-  return nch * ksize * ksize * ck * (size_t)pad_cout(Cout) * sizeof(float);
+  size_t f = direct_packed_floats(Cout, Cin, ksize);
+  if (ksize == 3) f += wino_packed_floats(Cout, Cin);
+  return f * sizeof(float);
 }
 
 extern "C" int64_t rpst_conv2d_grid_threads(int N, int Hs, int Ws, int Cout, int ksize,
                                             int in_op) {
   if (N <= 0 || Hs <= 0 || Ws <= 0 || Cout <= 0 || (ksize != 1 && ksize != 3)) return 0;
-  int H = Hs, W = Ws;
-  if (in_op == RPST_IN_MAXPOOL2) {
-    H = (Hs + 1) / 2;
-    W = (Ws + 1) / 2;
-  } else if (in_op == RPST_IN_UPSAMPLE2) {
-    H = 2 * Hs;
-    W = 2 * Ws;
-  }
-  const TileCfg cfg = pick_cfg(Cout);
-  const int variant = conv_variant(cfg.BM, ksize, in_op);
-  const int th = variant_th(cfg.BM, variant);
-  const int nth = variant_nth(cfg.BM, variant);
-  const int64_t blocks = (int64_t)((W + kTW - 1) / kTW) * ((H + th - 1) / th) * N *
-                         (pad_cout(Cout) / cfg.BM);
-  return blocks * nth;
+  const ConvGeom g = conv_geom(N, Hs, Ws, Cout, ksize, in_op);
+  return g.blocks * g.nth;
+}
+
+extern "C" int rpst_conv2d_algorithm(int Cout, int ksize) {
+  return use_winograd(Cout, ksize) ? RPST_CONV_WINOGRAD : RPST_CONV_DIRECT;
 }
 
 extern "C" int rpst_conv2d_pack(const float* weight, float* packed, int Cout, int Cin,
@@ -625,12 +561,14 @@ extern "C" int rpst_conv2d_pack(const float* weight, float* packed, int Cout, in
   RPST_REQUIRE(weight && packed, "conv2d_pack: null pointer");
   RPST_REQUIRE(Cout > 0 && Cin > 0, "conv2d_pack: bad channels");
   RPST_REQUIRE(ksize == 1 || ksize == 3, "conv2d_pack: ksize must be 1 or 3, got %d", ksize);
-  const int64_t total = (int64_t)(rpst_conv2d_packed_size(Cout, Cin, ksize) / sizeof(float));
+  const int64_t total = (int64_t)direct_packed_floats(Cout, Cin, ksize);
   const int threads = 256;
   conv_pack_kernel<<<(unsigned)((total + threads - 1) / threads), threads, 0,
                      as_stream(stream)>>>(weight, packed, Cout, Cin, ksize, ck_of(ksize),
                                           pad_cout(Cout), total);
-  return launch_status("conv_pack_kernel");
+  if (int e = launch_status("conv_pack_kernel")) return e;
+  if (ksize == 3) return wino_pack(weight, packed + total, Cout, Cin, as_stream(stream));
+  return RPST_OK;
 }
 
 static int conv_common(const float* input, const float* aux, const float* packed_weight,
@@ -682,6 +620,20 @@ static int conv_common(const float* input, const float* aux, const float* packed
   }
   if (ksize == 3 && pad_mode == RPST_PAD_REFLECT)
     RPST_REQUIRE(a.H >= 2 && a.W >= 2, "conv2d: reflect padding needs H,W >= 2");
+  RPST_REQUIRE((int64_t)N * (Cout > Cin ? Cout : Cin) * a.H * a.W < (1LL << 40),
+               "conv2d: tensor too large");
+  // per-image input (plus one chunk of channel padding) must be addressable by a 31-bit
+  // buffer offset
+  RPST_REQUIRE(((int64_t)Cin + 16) * Hs * Ws * 4 < (1LL << 31),
+               "conv2d: one image's input exceeds 2 GiB");
+  if (use_winograd(Cout, ksize)) {
+    a.wpk = packed_weight + direct_packed_floats(Cout, Cin, ksize);
+    a.stat_part = stat_part;
+    if (int e = wino_launch(a, in_op, st)) return e;
+    if (stat_P) *stat_P = a.stat_P;
+    if (args_out) *args_out = a;
+    return RPST_OK;
+  }
   const TileCfg cfg = pick_cfg(Cout);
   const int variant = conv_variant(cfg.BM, ksize, in_op);
   const int th = variant_th(cfg.BM, variant);
@@ -697,12 +649,6 @@ static int conv_common(const float* input, const float* aux, const float* packed
   if (stat_P) *stat_P = a.stat_P;
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * N * a.co_tiles;
   RPST_REQUIRE(blocks <= 0x7fffffffLL, "conv2d: grid too large");
-  RPST_REQUIRE((int64_t)N * (Cout > Cin ? Cout : Cin) * a.H * a.W < (1LL << 40),
-               "conv2d: tensor too large");
-  // per-image input (plus one chunk of channel padding) must be addressable by a 31-bit
-  // buffer offset
-  RPST_REQUIRE(((int64_t)Cin + 16) * Hs * Ws * 4 < (1LL << 31),
-               "conv2d: one image's input exceeds 2 GiB");
   if (args_out) *args_out = a;
   if (ksize == 1) {
     RPST_REQUIRE(in_op == RPST_IN_NONE, "conv2d: 1x1 conv supports in_op NONE only");
@@ -731,22 +677,9 @@ extern "C" int rpst_conv2d(const float* input, const float* aux, const float* pa
 
 extern "C" size_t rpst_conv2d_stats_workspace_size(int N, int Hs, int Ws, int Cout, int ksize,
                                                    int in_op) {
-  const int64_t thr = rpst_conv2d_grid_threads(N, Hs, Ws, Cout, ksize, in_op);
-  if (thr <= 0) return 0;
-  int H = Hs, W = Ws;
-  if (in_op == RPST_IN_MAXPOOL2) {
-    H = (Hs + 1) / 2;
-    W = (Ws + 1) / 2;
-  } else if (in_op == RPST_IN_UPSAMPLE2) {
-    H = 2 * Hs;
-    W = 2 * Ws;
-  }
-  const TileCfg cfg = pick_cfg(Cout);
-  const int variant = conv_variant(cfg.BM, ksize, in_op);
-  const int64_t P = (int64_t)((W + kTW - 1) / kTW) * ((H + variant_th(cfg.BM, variant) - 1) /
-                                                      variant_th(cfg.BM, variant)) *
-                    variant_wn(cfg.BM, variant);
-  return (size_t)N * Cout * P * sizeof(float2);
+  if (N <= 0 || Hs <= 0 || Ws <= 0 || Cout <= 0 || (ksize != 1 && ksize != 3)) return 0;
+  const ConvGeom g = conv_geom(N, Hs, Ws, Cout, ksize, in_op);
+  return (size_t)N * Cout * g.stat_P * sizeof(float2);
 }
 
 extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
@@ -764,11 +697,9 @@ extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
   hipStream_t st = as_stream(stream);
   ConvArgs a{};
   int P = 0;
-  const TileCfg cfg = pick_cfg(Cout);
-  const int variant = conv_variant(cfg.BM, ksize, in_op);
-  const int wn = variant_wn(cfg.BM, variant), th = variant_th(cfg.BM, variant);
+  const ConvGeom g = conv_geom(N, Hs, Ws, Cout, ksize, in_op);
   const int planes = N * Cout;
-  if (th / wn < 4) {  // tile without the fused statistics epilogue: separate pass
+  if (!g.wino && g.stat_nt < 4) {  // tile without the fused statistics epilogue
     if (int e = conv_common(input, aux, packed_weight, bias, residual, out, N, Cin, Hs, Ws,
                             Cout, ksize, pad_mode, in_op, relu, nullptr, &P, &a, st))
       return e;
@@ -779,8 +710,8 @@ extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
                           &a, st))
     return e;
   stat_merge_kernel<<<(planes + 3) / 4, 256, 0, st>>>(static_cast<const float2*>(workspace), mean,
-                                                      std_out, planes, P, a.tiles_x, wn, th / wn,
-                                                      a.H, a.W, eps);
+                                                      std_out, planes, P, a.tiles_x, g.stat_wn,
+                                                      g.stat_nt, a.H, a.W, eps);
   return launch_status("stat_merge_kernel");
 }
 

@@ -158,6 +158,15 @@ def conv_out_hw(h: int, w: int, in_op: int) -> Tuple[int, int]:
     return h, w
 
 
+def _conv_name(ksize, cin, cout, h, w, n, in_op):
+    """Trace key of a conv launch; 'wino3x3' when the library runs it as Winograd
+    F(2x2,3x3) (the recorded FLOPs stay the direct-convolution count)."""
+    algo = "conv"
+    if TRACE is not None and _lib.load().rpst_conv2d_algorithm(cout, ksize) == 1:
+        algo = "wino"
+    return f"{algo}{ksize}x{ksize} {cin}->{cout} {h}x{w} N{n} op{in_op}"
+
+
 def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], cout: int,
            ksize: int, pad: int = PAD_ZERO, in_op: int = IN_NONE, relu: bool = False,
            aux: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
@@ -179,8 +188,8 @@ def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], 
             assert aux.numel() == 4 * n * cin, "ADAIN aux = [mean_c|mean_s|std_c|std_s]"
         else:
             assert tuple(aux.shape) == (n, cin, h // 2, w // 2)
-    name = f"conv{ksize}x{ksize} {cin}->{cout} {h}x{w} N{n} op{in_op}"
-    with _traced(name, 2.0 * n * cout * h * w * cin * ksize * ksize,
+    with _traced(_conv_name(ksize, cin, cout, h, w, n, in_op),
+                 2.0 * n * cout * h * w * cin * ksize * ksize,
                  4.0 * (x.numel() + n * cout * h * w)):
         _lib.call("rpst_conv2d", x.data_ptr(), _ptr(aux), packed.data_ptr(),
                   _ptr(None if bias is None else _c(bias.detach())), _ptr(residual),
@@ -205,8 +214,7 @@ def conv2d_stats(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Ten
     lib = _lib.load()
     nbytes = lib.rpst_conv2d_stats_workspace_size(n, hs, ws, cout, ksize, in_op)
     ws_t = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
-    name = f"conv{ksize}x{ksize} {cin}->{cout} {h}x{w} N{n} op{in_op}"
-    with _traced(name, 2.0 * n * cout * h * w * cin * ksize * ksize,
+    with _traced(_conv_name(ksize, cin, cout, h, w, n, in_op), 2.0 * n * cout * h * w * cin * ksize * ksize,
                  4.0 * (x.numel() + n * cout * h * w)):
         _lib.call("rpst_conv2d_stats", x.data_ptr(), _ptr(aux), packed.data_ptr(),
                   _ptr(None if bias is None else _c(bias.detach())), None, out.data_ptr(), n,

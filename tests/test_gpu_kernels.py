@@ -1,6 +1,7 @@
 """GPU parity: each HIP kernel (through the C ABI) against the CPU oracle and goldens.
 
-Tolerances: stats/AdaIN rel-L2 <= 1e-5; conv (one layer) <= 1e-5;
+Tolerances: stats/AdaIN rel-L2 <= 1e-5; conv (one layer) <= 1e-5 for
+both the direct and the Winograd F(2x2,3x3) algorithm (fp64 reference);
 networks rel-L2 <= 1e-4 and max-abs <= 5e-4*max|ref|.
 """
 import copy
@@ -135,8 +136,15 @@ CONV_CASES = [
 ]
 
 
+@pytest.fixture(params=["direct", "winograd"])
+def conv_algo(request, monkeypatch):
+    """Run a 3x3 conv test on both algorithms (librpst reads RPST_CONV_ALGO per launch)."""
+    monkeypatch.setenv("RPST_CONV_ALGO", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv2d_vs_torch(cuda, case):
+def test_conv2d_vs_torch(cuda, case, conv_algo):
     from rpst import ops
     n, cin, hs, ws, cout, k, pad, in_op, relu = case
     x = gen(10, (n, cin, hs, ws), 1.0, 0.2)
@@ -164,7 +172,7 @@ def test_conv2d_residual(cuda):
     assert rel_l2(out, ref) < 1e-5
 
 
-def test_conv2d_deterministic(cuda):
+def test_conv2d_deterministic(cuda, conv_algo):
     from rpst import ops
     x = gen(30, (2, 128, 32, 64)).to(cuda)
     w = gen(31, (256, 128, 3, 3), 0.03).to(cuda)
@@ -269,7 +277,7 @@ def test_vgg_and_decoder_golden(cuda, golden):
 # ---- fused AdaIN (statistics in the producing conv's epilogue, apply in the consumer's loader)
 @pytest.mark.parametrize("shape", [(2, 16, 64, 96, 256), (1, 8, 17, 45, 64), (3, 3, 9, 7, 32),
                                    (2, 64, 40, 40, 128)])
-def test_conv2d_stats_equal_calc_mean_std(cuda, shape):
+def test_conv2d_stats_equal_calc_mean_std(cuda, shape, conv_algo):
     from rpst import ops
     n, cin, h, w, cout = shape
     x = gen(50, (n, cin, h, w), 1.0, 0.3).to(cuda)
@@ -284,7 +292,7 @@ def test_conv2d_stats_equal_calc_mean_std(cuda, shape):
     assert rel_l2(std, s2) < 1e-6
 
 
-def test_conv2d_adain_input_op(cuda):
+def test_conv2d_adain_input_op(cuda, conv_algo):
     from rpst import ops
     c = gen(60, (2, 32, 24, 40), 2.0, 0.5).clamp_min(0)
     s = gen(61, (2, 32, 24, 40), 1.0, 1.0).clamp_min(0)

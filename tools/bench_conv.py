@@ -1,8 +1,9 @@
-"""Conv tile-variant micro-benchmark (interleaved rounds in one process).
+"""Conv tile-variant / algorithm micro-benchmark (interleaved rounds in one process).
 
-For each conv layer shape of the benchmark workloads, times every tile variant of
-rpst_conv2d (RPST_CONV_VARIANT) with HIP events on the launch stream, checks that all
-variants produce bit-identical output (same per-output K order), and prints TF/s.
+For each conv layer shape of the benchmark workloads, times every tile variant of the
+direct rpst_conv2d (RPST_CONV_VARIANT) and the Winograd path (RPST_CONV_ALGO) with HIP
+events on the launch stream, checks that all produce the same output within 1e-5 rel-L2,
+and prints effective TF/s (direct-convolution FLOPs / time).
 
     python tools/bench_conv.py [--layers adain|vgg|all] [--rounds 3]
 """
@@ -45,12 +46,19 @@ def main():
     ap.add_argument("--layers", default="all")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--only", default=None, help="substring filter on 'cin->cout'")
+    ap.add_argument("--algo", default=None, choices=["direct", "winograd"],
+                    help="time one algorithm only (profiling)")
+    ap.add_argument("--default-only", action="store_true",
+                    help="direct default variant vs Winograd only")
     args = ap.parse_args()
     layers = {"adain": ADAIN, "vgg": VGG, "fused": FUSED, "all": ADAIN + FUSED + VGG}[args.layers]
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     results = []
     for (n, cin, hs, ws, cout, k, pad, in_op) in layers:
+        if args.only and args.only != f"{cin}->{cout}":
+            continue
         x = torch.rand((n, cin, hs, ws), device=dev, generator=g)
         w = (torch.rand((cout, cin, k, k), device=dev, generator=g) - 0.5) * 0.1
         b = torch.rand((cout,), device=dev, generator=g) * 0.1
@@ -61,17 +69,27 @@ def main():
                              torch.rand(2 * n * cin, device=dev, generator=g) + 0.5])
         h, wd = ops.conv_out_hw(hs, ws, in_op)
         flops = 2.0 * n * cout * h * wd * cin * k * k
-        times = {v: [] for v in VARIANTS[bm_of(cout)]}
+        variants = [None] if args.default_only else VARIANTS[bm_of(cout)]
+        times = {("d", v): [] for v in variants}
+        if k == 3:
+            times[("w", None)] = []
+        if args.algo:
+            times = {key: [] for key in times if (key[0] == "w") == (args.algo == "winograd")}
         ref = None
         for rnd in range(args.rounds):
-            for v in times:
-                os.environ["RPST_CONV_VARIANT"] = str(v)
+            for key in times:
+                algo, v = key
+                os.environ["RPST_CONV_ALGO"] = "winograd" if algo == "w" else "direct"
+                if v is None:
+                    os.environ.pop("RPST_CONV_VARIANT", None)
+                else:
+                    os.environ["RPST_CONV_VARIANT"] = str(v)
                 out = ops.conv2d(x, p, b, cout, k, pad=pad, in_op=in_op, relu=True, aux=aux)
                 if ref is None:
                     ref = out.clone()
                 elif rnd == 0:  # chunk size changes the K summation order: tolerance
                     err = float((out - ref).norm() / ref.norm().clamp_min(1e-30))
-                    assert err < 1e-5, f"variant {v} differs: {err}"
+                    assert err < 1e-5, f"{key} differs: {err}"
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -79,13 +97,16 @@ def main():
                     ops.conv2d(x, p, b, cout, k, pad=pad, in_op=in_op, relu=True, aux=aux, out=out)
                 e1.record()
                 torch.cuda.synchronize()
-                times[v].append(e0.elapsed_time(e1) / args.reps)
+                times[key].append(e0.elapsed_time(e1) / args.reps)
         os.environ.pop("RPST_CONV_VARIANT", None)
+        os.environ.pop("RPST_CONV_ALGO", None)
         row = {"layer": f"{cin}->{cout} k{k} {h}x{wd} N{n} pad{pad} op{in_op}"}
-        for v, ts in times.items():
+        for (algo, v), ts in times.items():
             ms = min(ts)
-            row[f"v{v}_ms"] = round(ms, 3)
-            row[f"v{v}_tf"] = round(flops / ms / 1e9, 1)
+            name = "wino" if algo == "w" else ("direct" if v is None else f"v{v}")
+            row[f"{name}_ms"] = round(ms, 3)
+            # effective TF/s: direct-convolution FLOPs / time (Winograd executes 4/9 of them)
+            row[f"{name}_tf"] = round(flops / ms / 1e9, 1)
         results.append(row)
         print(json.dumps(row), flush=True)
         del x, w, p, ref
