@@ -112,8 +112,8 @@ int rpst_conv2d_stats(const float* input, const float* aux, const float* packed_
 int64_t rpst_conv2d_grid_threads(int N, int Hs, int Ws, int Cout, int ksize, int in_op);
 
 /* Algorithm rpst_conv2d uses for this layer — host-only: RPST_CONV_DIRECT (implicit GEMM,
- * all 1x1 and narrow 3x3 layers) or RPST_CONV_WINOGRAD (F(2x2,3x3) in fp32, 3x3 layers
- * with Cout >= 64). The environment variable RPST_CONV_ALGO=direct|winograd overrides. */
+ * all 1x1 and 16-wide 3x3 layers) or RPST_CONV_WINOGRAD (F(2x2,3x3) in fp32, 3x3 layers
+ * with Cout >= 32). The environment variable RPST_CONV_ALGO=direct|winograd overrides. */
 #define RPST_CONV_DIRECT 0
 #define RPST_CONV_WINOGRAD 1
 int rpst_conv2d_algorithm(int Cout, int ksize);

@@ -19,6 +19,7 @@ struct ConvArgs {
   int N, Cin, Hs, Ws, H, W, Cout, Cout_pad, nchunks;
   int tiles_x, tiles_y, co_tiles;
   int pad, relu;
+  int persist;        // Winograd: one block loops over all co tiles of its spatial tile
   float2* stat_part;  // optional: per-(n, co, wave tile) (mean, M2) of the output
   int stat_P;         // partials per (n, co) = tiles_x * tiles_y * WN
 };
@@ -129,6 +130,37 @@ __device__ __forceinline__ float halfwave_reduce_scatter16(float (&v)[16], int j
   return s + __shfl_xor(s, 1, 64);
 }
 
+// Bijective XCD-aware remap of a block index (cdna_hip_programming.md T1): blocks
+// b, b+8, b+16, ... share an XCD (and its L2) under the observed round-robin dispatch, so
+// give each such group a contiguous range of logical ids. Speed only, never correctness.
+__device__ __forceinline__ int xcd_swizzle(int b, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+// Sum each of v[0..V-1] (V a power of two <= 16) over the 32 lanes of a half-wave.
+// Returns the total of element e = (j >> (5 - log2 V)) & (V - 1) (the lanes of one group
+// of 32/V hold it).
+template <int V>
+__device__ __forceinline__ float halfwave_reduce_scatter(float (&v)[V], int j) {
+  static_assert(V >= 1 && V <= 16 && (V & (V - 1)) == 0, "power of two <= 16");
+  float w[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) w[i] = v[i];
+  int n = V, bit = 16;
+#pragma unroll
+  for (; n > 1; n >>= 1, bit >>= 1) {
+    const bool b = (j & bit) != 0;
+#pragma unroll
+    for (int i = 0; i < n / 2; ++i)
+      w[i] = (b ? w[i + n / 2] : w[i]) + __shfl_xor(b ? w[i] : w[i + n / 2], bit, 64);
+  }
+  float s = w[0];
+#pragma unroll
+  for (; bit > 0; bit >>= 1) s += __shfl_xor(s, bit, 64);
+  return s;
+}
+
 // Sum each of v[0..7] over the 32 lanes of a half-wave. Returns the total of element
 // e = (j >> 2) & 7 (lanes 4e..4e+3 of the half hold it).
 __device__ __forceinline__ float halfwave_reduce_scatter8(float (&v)[8], int j) {
@@ -146,9 +178,11 @@ __device__ __forceinline__ float halfwave_reduce_scatter8(float (&v)[8], int j) 
 }
 
 // ---- Winograd F(2x2,3x3) path (rpst_wino.hip) ----------------------------------------
-constexpr int kWinoBM = 64;    // output channels per block
-constexpr int kWinoTH = 4;     // output rows per block (x kTW columns)
 constexpr int kWinoNTH = 256;  // threads per block
+// tile shape in use: output channels (BM) x rows (TH, x kTW columns) per block
+int wino_bm();
+int wino_th();
+int wino_persist(int in_op);  // 1: grid over spatial tiles only, each block loops over co tiles
 // floats of the Winograd weight image (stored after the direct image for 3x3 convs)
 size_t wino_packed_floats(int Cout, int Cin);
 int wino_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);
