@@ -46,6 +46,13 @@ typedef void* rpst_stream_t;
 #define RPST_IN_ADD_UPSAMPLE2 3 /* x + Upsample2(y)   sanet.py:149 (Transform merge input)   */
 #define RPST_IN_ADAIN 4 /* ((x-mean_c)/std_c)*std_s+mean_s per (n,ci): AdaIN base.py:416-418 fused
                            into the consumer conv; aux = [mean_c|mean_s|std_c|std_s], N*Cin each */
+#define RPST_IN_ADD_ADAIN 5 /* x + AdaIN(c): the skip fusion of MultiScaleAdaINRPNet.decode,
+                           adain_rp.py:301 (rp_decoder[i+1](stylized + AdaIN(c_i, s_i)))  */
+
+/* conv2d epilogue activation (the `relu` argument) */
+#define RPST_ACT_NONE 0
+#define RPST_ACT_RELU 1  /* nn.ReLU                                     */
+#define RPST_ACT_LRELU 2 /* nn.LeakyReLU(0.2): Conv2dBlock base.py:147 */
 
 /* Library version (major*10000 + minor*100 + patch). */
 int rpst_version(void);
@@ -86,7 +93,8 @@ int rpst_mean_variance_norm(const float* feat, float* out, int N, int C, int64_t
  *   RPST_IN_ADAIN:        input (N,Cin,H,W) normalised on load with aux statistics
  *   RPST_IN_NONE:         input (N,Cin,H,W)
  * (Hs, Ws) are the dims of `input`. out (N,Cout,H,W):
- *   out = [relu](conv(in_op(input)) + bias) [+ residual]   (residual (N,Cout,H,W) or NULL)
+ *   out = act(conv(in_op(input)) + bias) [+ residual]   (residual (N,Cout,H,W) or NULL),
+ *   act = `relu`: RPST_ACT_NONE / RPST_ACT_RELU / RPST_ACT_LRELU
  * ksize 1 ignores pad_mode. Reflect padding needs H,W >= 2. */
 size_t rpst_conv2d_packed_size(int Cout, int Cin, int ksize);
 int rpst_conv2d_pack(const float* weight, float* packed, int Cout, int Cin, int ksize,
@@ -106,6 +114,15 @@ int rpst_conv2d_stats(const float* input, const float* aux, const float* packed_
                       int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
                       float* mean, float* std_out, float eps, void* workspace,
                       size_t workspace_bytes, rpst_stream_t stream);
+
+/* MultiScaleAdaINRPNet skip fusion (adain_rp.py:301): out = act(conv(pad(x + AdaIN(c))) +
+ * bias), x = `stylized` and c = `content` both (N,Cin,H,W), AdaIN with the calc_mean_std
+ * statistics `params` = [mean_c | mean_s | std_c | std_s] (4*N*Cin floats, as
+ * RPST_IN_ADAIN). The sum is formed while the conv stages its input tile. */
+int rpst_conv2d_skip_adain(const float* stylized, const float* content, const float* params,
+                           const float* packed_weight, const float* bias, float* out, int N,
+                           int Cin, int H, int W, int Cout, int ksize, int pad_mode, int relu,
+                           rpst_stream_t stream);
 
 /* Launch geometry (total threads) rpst_conv2d would use for this shape — host-only; lets
  * profilers match rocprofv3 per-dispatch records (Grid_Size) to a layer. */

@@ -128,6 +128,47 @@ def adain_rp_test(content: Tensor, style: Tensor, sd: SD, rp_blocks: int) -> Ten
         return rp_stack(adain(cf, sf), sd, "rp_decoder.", rp_blocks)
 
 
+# ---- §8(f) rank 3: SourceNet (classic AdaIN) -----------------------------------------
+def sourcenet_test(content: Tensor, style: Tensor, sd: SD) -> Tensor:
+    """SourceNet.test / decode (network/base.py:580-594): VGG relu4_1 of content and
+    style, AdaIN, the VGG-mirror decoder (module attribute `decoder`, keys 'decoder.*')."""
+    with torch.no_grad():
+        c4 = encode_with_intermediate(content, sd)[-1]
+        s4 = encode_with_intermediate(style, sd)[-1]
+        return decoder(adain(c4, s4), sd, "decoder.")
+
+
+# ---- §8(f) rank 1: MultiScaleAdaINRPNet, constant stack ------------------------------
+def conv2d_block(x: Tensor, sd: SD, prefix: str, inception_num: int = 0) -> Tensor:
+    """Conv2dBlock.forward (network/base.py:187-198) with pad_type 'reflect', norm 'none',
+    activation 'lrelu' (LeakyReLU(0.2)), no attention: conv(pad(x)) -> inception 1x1
+    convs -> activation."""
+    x = conv(x, sd, f"{prefix}conv", "reflect", False)
+    for k in range(inception_num):
+        x = conv(x, sd, f"{prefix}inception.{k}.0", "none", False)
+    return F.leaky_relu(x, 0.2)
+
+
+def multiscale_test(content: Tensor, style: Tensor, sd: SD, rp_blocks: int,
+                    inception_num: int = 0) -> Tensor:
+    """MultiScaleAdaINRPNet.test / decode (adain_rp.py:242-301) for enc_stack_way
+    'constant' (rp_constant_conv_blocks, base.py:260-285), shuffle/sort/use_mask off:
+    every encoder level is kept; the decoder starts from AdaIN of the last level and
+    adds AdaIN of the earlier levels, deepest first, before each next block."""
+    with torch.no_grad():
+        def enc(x):
+            feats = []
+            for i in range(rp_blocks):
+                x = conv2d_block(x, sd, f"rp_shared_encoder.{i}.", inception_num)
+                feats.append(x)
+            return feats
+        cfs, sfs = enc(content), enc(style)
+        y = conv2d_block(adain(cfs[-1], sfs[-1]), sd, "rp_decoder.0.")
+        for i, (cf, sf) in enumerate(list(zip(cfs[:-1], sfs[:-1]))[::-1]):
+            y = conv2d_block(y + adain(cf, sf), sd, f"rp_decoder.{i + 1}.")
+        return y
+
+
 def style_loss(a: Tensor, b: Tensor) -> Tensor:
     am, as_ = calc_mean_std(a)
     bm, bs = calc_mean_std(b)

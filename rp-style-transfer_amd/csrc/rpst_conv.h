@@ -12,6 +12,7 @@ constexpr int kTW = 32;  // pixels per N sub-tile = one row segment
 struct ConvArgs {
   const float* in;
   const float* aux;
+  const float* aux2;  // RPST_IN_ADD_ADAIN: the content feature c (N,Cin,H,W)
   const float* wpk;
   const float* bias;
   const float* res;
@@ -59,8 +60,38 @@ __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
 // MFMAs), so no wait for the loads sits in front of the compute phase.
 template <int INOP>
 struct RawN {
-  static constexpr int R = INOP == RPST_IN_MAXPOOL2 ? 4 : (INOP == RPST_IN_ADD_UPSAMPLE2 ? 2 : 1);
+  static constexpr int R = INOP == RPST_IN_MAXPOOL2
+                               ? 4
+                               : ((INOP == RPST_IN_ADD_UPSAMPLE2 || INOP == RPST_IN_ADD_ADAIN) ? 2 : 1);
 };
+
+// Second-operand tensor of the two-load input operators (per image), read through the
+// `raux` descriptor: ADD_UPSAMPLE2 -> aux (N,Cin,H/2,W/2); ADD_ADAIN -> aux2 (N,Cin,H,W).
+template <int INOP>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t aux_rsrc(const ConvArgs& a, int n) {
+  if constexpr (INOP == RPST_IN_ADD_ADAIN) {
+    const unsigned plane = (unsigned)(a.H * a.W);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(a.aux2 + (int64_t)n * a.Cin * plane),
+                                             (short)0, (int)(a.Cin * plane * 4u), 0x00020000);
+  } else {
+    const unsigned plane = (unsigned)((a.H >> 1) * (a.W >> 1));
+    return __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(INOP == RPST_IN_ADD_UPSAMPLE2 ? a.aux + (int64_t)n * a.Cin * plane : a.in),
+        (short)0, (int)(a.Cin * plane * 4u), 0x00020000);
+  }
+}
+
+template <int INOP>
+__device__ __forceinline__ unsigned aux_plane_of(const ConvArgs& a) {
+  return INOP == RPST_IN_ADD_ADAIN ? (unsigned)(a.H * a.W) : (unsigned)((a.H >> 1) * (a.W >> 1));
+}
+
+// epilogue activation: 0 none, 1 ReLU, 2 LeakyReLU(0.2) (torch: x > 0 ? x : x * slope)
+__device__ __forceinline__ float activate(float v, int act) {
+  if (act == RPST_ACT_RELU) return fmaxf(v, 0.f);
+  if (act == RPST_ACT_LRELU) return v > 0.f ? v : v * 0.2f;
+  return v;
+}
 
 // Issue the loads of one element: logical (post-in_op) resolved row yr / column xr of the
 // plane at byte offset `pbyte` (image-relative). ok == false -> zero (pad position /
@@ -85,6 +116,9 @@ __device__ __forceinline__ void fetch_raw(float (&r)[RawN<INOP>::R], __amdgpu_bu
   } else if constexpr (INOP == RPST_IN_ADD_UPSAMPLE2) {
     r[0] = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
     r[1] = bload(raux, ok ? abyte + (unsigned)((yr >> 1) * (a.W >> 1) + (xr >> 1)) * 4u : kOOB);
+  } else if constexpr (INOP == RPST_IN_ADD_ADAIN) {
+    r[0] = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
+    r[1] = bload(raux, ok ? abyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
   } else {  // RPST_IN_NONE and RPST_IN_ADAIN
     r[0] = bload(rin, ok ? pbyte + (unsigned)(yr * a.W + xr) * 4u : kOOB);
   }
@@ -109,6 +143,8 @@ __device__ __forceinline__ float combine(const float (&r)[RawN<INOP>::R], bool o
   if constexpr (INOP == RPST_IN_MAXPOOL2) return fmaxf(fmaxf(r[0], r[1]), fmaxf(r[2], r[3]));
   else if constexpr (INOP == RPST_IN_ADD_UPSAMPLE2) return r[0] + r[1];
   else if constexpr (INOP == RPST_IN_ADAIN) return ok ? fmaf(r[0] - p.mc, p.scale, p.ms) : 0.f;
+  else if constexpr (INOP == RPST_IN_ADD_ADAIN)
+    return ok ? r[0] + fmaf(r[1] - p.mc, p.scale, p.ms) : 0.f;
   else return r[0];
 }
 

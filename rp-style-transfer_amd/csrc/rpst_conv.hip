@@ -83,13 +83,11 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
   // ---- buffer descriptors (wave-uniform) -------------------------------------------
   const bool pooled = (INOP == RPST_IN_MAXPOOL2 || INOP == RPST_IN_UPSAMPLE2);
   const unsigned in_plane = pooled ? (unsigned)(a.Hs * a.Ws) : (unsigned)(a.H * a.W);
-  const unsigned aux_plane = (unsigned)((a.H >> 1) * (a.W >> 1));
+  const unsigned aux_plane = aux_plane_of<INOP>(a);
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.in + (int64_t)n * a.Cin * in_plane), (short)0, (int)(a.Cin * in_plane * 4u),
       0x00020000);
-  const __amdgpu_buffer_rsrc_t raux = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(INOP == RPST_IN_ADD_UPSAMPLE2 ? a.aux + (int64_t)n * a.Cin * aux_plane : a.in),
-      (short)0, (int)(a.Cin * aux_plane * 4u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t raux = aux_rsrc<INOP>(a, n);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.wpk + co0), (short)0, 0x7fffffff, 0x00020000);
 
@@ -157,7 +155,8 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
     _Pragma("unroll") for (int q = 0; q < CPT; ++q) {                                       \
       const unsigned ch = (unsigned)((c) * CK + cg + CGS * q);                              \
       const unsigned pb = ch * in_plane * 4u, ab = ch * aux_plane * 4u;                     \
-      if (INOP == RPST_IN_ADAIN) ap[q] = adain_params(a.aux, n, (int)ch, a);                \
+      if (INOP == RPST_IN_ADAIN || INOP == RPST_IN_ADD_ADAIN)                               \
+        ap[q] = adain_params(a.aux, n, (int)ch, a);                                         \
       _Pragma("unroll") for (int i = 0; i < RPT; ++i) {                                     \
         const int py = rs * RPT + i;                                                        \
         int y = y0 - OFF + py;                                                              \
@@ -189,7 +188,7 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
       for (int i = 0; i < RPT; ++i) {
         const int py = rs * RPT + i;
         bool ok = chok && bx_ok;
-        if (INOP == RPST_IN_ADAIN) {
+        if (INOP == RPST_IN_ADAIN || INOP == RPST_IN_ADD_ADAIN) {
           int y = y0 - OFF + py;
           ok = ok && resolve(y, a.H, a.pad, KS == 3);
         }
@@ -242,7 +241,7 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
       for (int nt = 0; nt < NT; ++nt) {
         const int y = y0 + wn * NT + nt;
         float v = acc[mt][nt][r] + b;
-        if (a.relu) v = fmaxf(v, 0.f);
+        v = activate(v, a.relu);
         if (y < a.H && x < a.W) {
           const int64_t o = pbase + (int64_t)y * a.W + x;
           if (a.res) v += a.res[o];
@@ -390,7 +389,7 @@ static void launch_conv(const ConvArgs& a, int BM, int variant, hipStream_t st) 
   constexpr int C8 = ConvK<KS>::CK, C4 = ConvK<KS>::CK / 2;
   // loaders with 2-4 raw loads per element only get the short-tile variants (the tall
   // ones run out of registers)
-  constexpr bool HEAVY = INOP == RPST_IN_MAXPOOL2 || INOP == RPST_IN_ADD_UPSAMPLE2;
+  constexpr bool HEAVY = RawN<INOP>::R > 1;
   if constexpr (HEAVY) {
     if (BM == 128) {
       if (variant == 4) RPST_LAUNCH(128, 4, 2, 2, 256, C4, true);
@@ -429,7 +428,8 @@ static void launch_conv(const ConvArgs& a, int BM, int variant, hipStream_t st) 
 }
 
 static bool heavy_loader(int in_op) {
-  return in_op == RPST_IN_MAXPOOL2 || in_op == RPST_IN_ADD_UPSAMPLE2;
+  return in_op == RPST_IN_MAXPOOL2 || in_op == RPST_IN_ADD_UPSAMPLE2 ||
+         in_op == RPST_IN_ADD_ADAIN;
 }
 
 static int pick_variant(int BM, int ksize, int in_op) {
@@ -572,7 +572,8 @@ extern "C" int rpst_conv2d_pack(const float* weight, float* packed, int Cout, in
   return RPST_OK;
 }
 
-static int conv_common(const float* input, const float* aux, const float* packed_weight,
+static int conv_common(const float* input, const float* aux, const float* aux2,
+                       const float* packed_weight,
                        const float* bias, const float* residual, float* out, int N, int Cin,
                        int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
                        float2* stat_part, int* stat_P, ConvArgs* args_out, hipStream_t st) {
@@ -580,10 +581,12 @@ static int conv_common(const float* input, const float* aux, const float* packed
   RPST_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && Hs > 0 && Ws > 0, "conv2d: bad shape");
   RPST_REQUIRE(ksize == 1 || ksize == 3, "conv2d: ksize must be 1 or 3, got %d", ksize);
   RPST_REQUIRE(pad_mode == RPST_PAD_ZERO || pad_mode == RPST_PAD_REFLECT, "conv2d: bad pad");
-  RPST_REQUIRE(in_op >= RPST_IN_NONE && in_op <= RPST_IN_ADAIN, "conv2d: bad in_op");
+  RPST_REQUIRE(in_op >= RPST_IN_NONE && in_op <= RPST_IN_ADD_ADAIN, "conv2d: bad in_op");
+  RPST_REQUIRE(relu >= RPST_ACT_NONE && relu <= RPST_ACT_LRELU, "conv2d: bad activation %d", relu);
   ConvArgs a{};
   a.in = input;
   a.aux = aux;
+  a.aux2 = aux2;
   a.wpk = packed_weight;
   a.bias = bias;
   a.res = residual;
@@ -594,7 +597,7 @@ static int conv_common(const float* input, const float* aux, const float* packed
   a.Ws = Ws;
   a.Cout = Cout;
   a.pad = pad_mode;
-  a.relu = relu ? 1 : 0;
+  a.relu = relu;
   switch (in_op) {
     case RPST_IN_MAXPOOL2:
       a.H = (Hs + 1) / 2;
@@ -612,6 +615,12 @@ static int conv_common(const float* input, const float* aux, const float* packed
       break;
     case RPST_IN_ADAIN:
       RPST_REQUIRE(aux != nullptr, "conv2d: ADAIN needs aux (AdaIN statistics)");
+      a.H = Hs;
+      a.W = Ws;
+      break;
+    case RPST_IN_ADD_ADAIN:
+      RPST_REQUIRE(aux != nullptr && aux2 != nullptr,
+                   "conv2d: ADD_ADAIN needs the content feature and AdaIN statistics");
       a.H = Hs;
       a.W = Ws;
       break;
@@ -662,6 +671,8 @@ static int conv_common(const float* input, const float* aux, const float* packed
     launch_conv<3, RPST_IN_ADD_UPSAMPLE2>(a, cfg.BM, variant, st);
   } else if (in_op == RPST_IN_ADAIN) {
     launch_conv<3, RPST_IN_ADAIN>(a, cfg.BM, variant, st);
+  } else if (in_op == RPST_IN_ADD_ADAIN) {
+    launch_conv<3, RPST_IN_ADD_ADAIN>(a, cfg.BM, variant, st);
   } else {
     launch_conv<3, RPST_IN_NONE>(a, cfg.BM, variant, st);
   }
@@ -672,8 +683,21 @@ extern "C" int rpst_conv2d(const float* input, const float* aux, const float* pa
                            const float* bias, const float* residual, float* out, int N,
                            int Cin, int Hs, int Ws, int Cout, int ksize, int pad_mode,
                            int in_op, int relu, rpst_stream_t stream) {
-  return conv_common(input, aux, packed_weight, bias, residual, out, N, Cin, Hs, Ws, Cout,
-                     ksize, pad_mode, in_op, relu, nullptr, nullptr, nullptr, as_stream(stream));
+  RPST_REQUIRE(in_op != RPST_IN_ADD_ADAIN, "conv2d: ADD_ADAIN goes through rpst_conv2d_skip_adain");
+  return conv_common(input, aux, nullptr, packed_weight, bias, residual, out, N, Cin, Hs, Ws,
+                     Cout, ksize, pad_mode, in_op, relu, nullptr, nullptr, nullptr,
+                     as_stream(stream));
+}
+
+extern "C" int rpst_conv2d_skip_adain(const float* stylized, const float* content,
+                                      const float* params, const float* packed_weight,
+                                      const float* bias, float* out, int N, int Cin, int H, int W,
+                                      int Cout, int ksize, int pad_mode, int relu,
+                                      rpst_stream_t stream) {
+  RPST_REQUIRE(ksize == 3, "conv2d_skip_adain: 3x3 convs only");
+  return conv_common(stylized, params, content, packed_weight, bias, nullptr, out, N, Cin, H, W,
+                     Cout, ksize, pad_mode, RPST_IN_ADD_ADAIN, relu, nullptr, nullptr, nullptr,
+                     as_stream(stream));
 }
 
 extern "C" size_t rpst_conv2d_stats_workspace_size(int N, int Hs, int Ws, int Cout, int ksize,
@@ -701,13 +725,13 @@ extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
   const ConvGeom g = conv_geom(N, Hs, Ws, Cout, ksize, in_op);
   const int planes = N * Cout;
   if (!g.wino && g.stat_nt < 4) {  // tile without the fused statistics epilogue
-    if (int e = conv_common(input, aux, packed_weight, bias, residual, out, N, Cin, Hs, Ws,
-                            Cout, ksize, pad_mode, in_op, relu, nullptr, &P, &a, st))
+    if (int e = conv_common(input, aux, nullptr, packed_weight, bias, residual, out, N, Cin, Hs,
+                            Ws, Cout, ksize, pad_mode, in_op, relu, nullptr, &P, &a, st))
       return e;
     return rpst_calc_mean_std(out, mean, std_out, N, Cout, (int64_t)a.H * a.W, eps, stream);
   }
-  if (int e = conv_common(input, aux, packed_weight, bias, residual, out, N, Cin, Hs, Ws, Cout,
-                          ksize, pad_mode, in_op, relu, static_cast<float2*>(workspace), &P,
+  if (int e = conv_common(input, aux, nullptr, packed_weight, bias, residual, out, N, Cin, Hs, Ws,
+                          Cout, ksize, pad_mode, in_op, relu, static_cast<float2*>(workspace), &P,
                           &a, st))
     return e;
   stat_merge_kernel<<<(planes + 3) / 4, 256, 0, st>>>(static_cast<const float2*>(workspace), mean,

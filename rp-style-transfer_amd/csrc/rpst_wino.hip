@@ -83,14 +83,15 @@ static size_t wino_image_floats(int MT, int Cout, int Cin) {
 // Tile shape: MT = 1 (32 co x 64 tiles per block) measured faster than MT = 2 (64 co x 32
 // tiles) on every layer of the three models (profiles/r01_bench_conv_wino.log), so only
 // its weight image is packed. Persistence over the co tiles pays for the one-load
-// loaders; the max-pool / add-upsample loaders keep one co tile per block (their extra
+// loaders; the two- and four-load loaders keep one co tile per block (their extra
 // raw registers would spill across the co-tile loop).
 constexpr int kWMT = 1;
 int wino_bm() { return 32 * kWMT; }
 int wino_th() { return 4 * (2 / kWMT); }
 int wino_persist(int in_op) {
   const char* e = getenv("RPST_WINO_PERSIST");  // A/B switch for the one-load loaders
-  if (in_op == RPST_IN_MAXPOOL2 || in_op == RPST_IN_ADD_UPSAMPLE2) return 0;
+  if (in_op == RPST_IN_MAXPOOL2 || in_op == RPST_IN_ADD_UPSAMPLE2 || in_op == RPST_IN_ADD_ADAIN)
+    return 0;
   return (e && *e) ? atoi(e) != 0 : 1;
 }
 
@@ -146,13 +147,11 @@ __global__ __launch_bounds__(kWinoNTH, 2) void wino_mfma_kernel(ConvArgs a) {
 
   const bool pooled = (INOP == RPST_IN_MAXPOOL2 || INOP == RPST_IN_UPSAMPLE2);
   const unsigned in_plane = pooled ? (unsigned)(a.Hs * a.Ws) : (unsigned)(a.H * a.W);
-  const unsigned aux_plane = (unsigned)((a.H >> 1) * (a.W >> 1));
+  const unsigned aux_plane = aux_plane_of<INOP>(a);
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.in + (int64_t)n * a.Cin * in_plane), (short)0, (int)(a.Cin * in_plane * 4u),
       0x00020000);
-  const __amdgpu_buffer_rsrc_t raux = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(INOP == RPST_IN_ADD_UPSAMPLE2 ? a.aux + (int64_t)n * a.Cin * aux_plane : a.in),
-      (short)0, (int)(a.Cin * aux_plane * 4u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t raux = aux_rsrc<INOP>(a, n);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.wpk, (short)0, 0x7fffffff, 0x00020000);
   const unsigned w_off = (unsigned)((wave * 64 + lane) * LANEW) * 4u;
@@ -204,7 +203,8 @@ __global__ __launch_bounds__(kWinoNTH, 2) void wino_mfma_kernel(ConvArgs a) {
   {                                                                                         \
     const unsigned ch = (unsigned)((c) * CK + cg);                                          \
     const unsigned pb = ch * in_plane * 4u, ab = ch * aux_plane * 4u;                       \
-    if (INOP == RPST_IN_ADAIN) AP = adain_params(a.aux, n, (int)ch, a);                     \
+    if (INOP == RPST_IN_ADAIN || INOP == RPST_IN_ADD_ADAIN)                                 \
+      AP = adain_params(a.aux, n, (int)ch, a);                                              \
     _Pragma("unroll") for (int py = 0; py < PH; ++py) {                                     \
       int y = y0 - 1 + py;                                                                  \
       const bool yok = resolve(y, a.H, a.pad, true);                                        \
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(kWinoNTH, 2) void wino_mfma_kernel(ConvArgs a) {
     const bool chok = (int)((c) * CK + cg) < a.Cin;                                         \
     _Pragma("unroll") for (int py = 0; py < PH; ++py) {                                     \
       bool ok = chok && bx_ok;                                                              \
-      if (INOP == RPST_IN_ADAIN) {                                                          \
+      if (INOP == RPST_IN_ADAIN || INOP == RPST_IN_ADD_ADAIN) {                             \
         int y = y0 - 1 + py;                                                                \
         ok = ok && resolve(y, a.H, a.pad, true);                                            \
       }                                                                                     \
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(kWinoNTH, 2) void wino_mfma_kernel(ConvArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           y[e] += b;
-          if (a.relu) y[e] = fmaxf(y[e], 0.f);
+          y[e] = activate(y[e], a.relu);
         }
         float* o = a.out + (((int64_t)n * a.Cout + co) * a.H + gy) * a.W + gx;
         if (vec) {
@@ -491,6 +491,9 @@ int wino_launch(ConvArgs& a, int in_op, hipStream_t st) {
       break;
     case RPST_IN_ADD_UPSAMPLE2:
       wino_mfma_kernel<RPST_IN_ADD_UPSAMPLE2, MT, false><<<nb, kWinoNTH, 0, st>>>(a);
+      break;
+    case RPST_IN_ADD_ADAIN:
+      wino_mfma_kernel<RPST_IN_ADD_ADAIN, MT, false><<<nb, kWinoNTH, 0, st>>>(a);
       break;
     case RPST_IN_UPSAMPLE2: RPST_WINO_GO(RPST_IN_UPSAMPLE2); break;
     case RPST_IN_ADAIN: RPST_WINO_GO(RPST_IN_ADAIN); break;

@@ -1,4 +1,5 @@
-"""Drop-in AdaINRPNet (reference network/adain_rp.py:15-138) on MI355X kernels.
+"""Drop-in AdaINRPNet (reference network/adain_rp.py:15-138) and MultiScaleAdaINRPNet
+(adain_rp.py:141-345) on MI355X kernels.
 
 Constructor, attribute names, state_dict keys and the test()/forward()/save()
 signatures follow the reference. test() runs the shared RP encoder ONCE over the
@@ -15,8 +16,10 @@ import torch.nn as nn
 from rpst import ops, plan
 from rpst.plan import KernelSequential
 
-from .base import (BaseNet, adaptive_instance_normalization, build_decrease_depth_rp_blocks,
-                   build_increase_depth_rp_blocks, calc_mean_std, mse)
+from .base import (BaseNet, Conv2dBlock, SourceNet, StackType,  # noqa: F401 (star exports)
+                   adaptive_instance_normalization, build_decrease_depth_rp_blocks,
+                   build_increase_depth_rp_blocks, calc_mean_std, mse, rp_constant_conv_blocks,
+                   rp_deeper_conv_blocks, rp_shallower_conv_blocks)
 from .base import adaptive_instance_normalization as AdaIN  # noqa: F401 (reference alias)
 
 
@@ -107,6 +110,128 @@ class AdaINRPNet(BaseNet):
         assert 0 <= alpha <= 1
         content_feat, style_feat = encode_both(self.rp_shared_encoder, content, style)
         stylized = self.rp_decoder(AdaIN(content_feat, style_feat))
+        down_stylized_feats = self.encode_with_intermediate(stylized)
+        down_style_feats = self.encode_with_intermediate(style)
+        down_content_feats = self.encode_with_intermediate(content)
+        loss_s = self.calc_style_loss(down_stylized_feats[0], down_style_feats[0])
+        for i in range(1, 4):
+            loss_s += self.calc_style_loss(down_stylized_feats[i], down_style_feats[i])
+        loss_c = self.calc_content_loss(down_stylized_feats[-1], down_content_feats[-1])
+        total_loss = self.config['content_weight'] * loss_c + self.config['style_weight'] * loss_s
+        return {'style_loss': loss_s, 'content_loss': loss_c, 'total_loss': total_loss}, total_loss
+
+
+def _block_plan(blk):
+    return plan.compile_layers(plan.block_layers(blk))
+
+
+class MultiScaleAdaINRPNet(AdaINRPNet):
+    """Multi-scale AdaIN-RP (adain_rp.py:141-345): every encoder
+    block's output is kept; decoding starts from AdaIN of the deepest level and, before
+    each next decoder block, adds AdaIN of the next shallower level (adain_rp.py:291-302).
+    Constant ('constant') and deeper/shallower ('deeper') stacks of Conv2dBlocks
+    (reflect pad, LeakyReLU 0.2). shuffle / sort / use_mask are not on the kernel path.
+
+    test() runs the shared encoder once over [content; style]; each encoder block emits
+    calc_mean_std of its output from its last conv's epilogue; the decoder's first conv
+    applies AdaIN while staging its input and every later block's first conv forms
+    stylized + AdaIN(c_i, s_i) in its loader (RPST_IN_ADD_ADAIN), so no AdaIN or sum
+    tensor is ever written."""
+
+    def __init__(self, config, vgg_encoder) -> None:
+        super().__init__(config, vgg_encoder)
+        self.config = config
+        self.rp_shared_encoder = None
+        self.rp_decoder = None
+        self._shuffle = self.config['shuffle']
+        self._shuffle_layers = self.config['shuffle_layers']
+        self._sort = self.config['sort']
+        self.layer_num = self.config['rp_blocks']
+        self._stylized_layers = self.config['stylized_layers']
+        if self.config['enc_stack_way'] == StackType.Deeper:
+            self.rp_shared_encoder = rp_deeper_conv_blocks(
+                self.config['rp_blocks'], 3, self.config['hidden_dim'], self.encoder_out_dim,
+                inception_num=self.config['inception_num'])
+            self.rp_decoder = rp_shallower_conv_blocks(
+                self.config['rp_blocks'], self.decoder_in_dim, self.decoder_hidden_dim, 3)
+        elif self.config['enc_stack_way'] == StackType.Constant:
+            self.encoder_out_dim = self.config['hidden_dim']
+            self.rp_shared_encoder = rp_constant_conv_blocks(
+                self.config['rp_blocks'], 3, self.config['hidden_dim'], self.encoder_out_dim,
+                inception_num=self.config['inception_num'], attention=self.config['attention'])
+            self.decoder_in_dim = self.encoder_out_dim
+            self.rp_decoder = rp_constant_conv_blocks(
+                self.config['rp_blocks'], self.decoder_in_dim, self.config['hidden_dim'], 3)
+        if self.config['resume']:
+            checkpoint_path = self.config['checkpoint_path']
+            self.begin = int(os.path.splitext(os.path.basename(checkpoint_path))[0])
+            state_dict = torch.load(checkpoint_path, weights_only=True)
+            self.rp_shared_encoder.load_state_dict(state_dict['encoder'])
+            self.rp_decoder.load_state_dict(state_dict['decoder'])
+
+    def _kernel_path_check(self, use_mask):
+        if use_mask or self._sort or self._shuffle:
+            raise NotImplementedError(
+                "MultiScaleAdaINRPNet: shuffle / sort / use_mask have no rpst kernel path")
+
+    def encode_rp_intermediate(self, input):
+        results = [input]
+        for i in range(len(self.rp_shared_encoder)):
+            results.append(self.rp_shared_encoder[i](results[-1]))
+        return results[1:]
+
+    def test(self, content, style, iterations=0, bid=0, c_mask_path=None, s_mask_path=None):
+        self.eval()
+        with torch.no_grad():
+            self._kernel_path_check(self.config['use_mask'])
+            if not FUSED_ADAIN:
+                content_feats = self.encode_rp_intermediate(content)
+                style_feats = self.encode_rp_intermediate(style)
+                stylized = self.decode(content_feats, style_feats,
+                                       use_mask=self.config['use_mask'])
+                self.train()
+                return stylized
+            n = content.shape[0]
+            x = torch.cat([content, style], dim=0)
+            levels = []  # (feature over 2n, mean, std) per encoder block
+            for blk in self.rp_shared_encoder:
+                x, mean, std = plan.run(_block_plan(blk), x, stats_last=True)
+                levels.append((x, mean, std))
+
+            def params(lv):
+                _, m, s = lv
+                return ops.adain_params(m[:n], s[:n], m[n:], s[n:])
+
+            feats = levels[-1][0]
+            y = plan.run(_block_plan(self.rp_decoder[0]), feats[:n],
+                         first_aux=params(levels[-1]), first_in_op=ops.IN_ADAIN)
+            for i, lv in enumerate(levels[:-1][::-1]):
+                y = plan.run(_block_plan(self.rp_decoder[i + 1]), y, first_aux=params(lv),
+                             first_in_op=ops.IN_ADD_ADAIN, first_content=lv[0][:n])
+            self.train()
+            return y
+
+    def decode(self, content_feats, style_feats, use_mask=False, c_mask_path=None, s_mask_path=None):
+        """adain_rp.py:291-302, op by op: AdaIN kernels, then each block with the skip
+        sum formed in its first conv's loader."""
+        self._kernel_path_check(use_mask)
+        stylized = AdaIN(content_feats[-1], style_feats[-1])
+        stylized = self.rp_decoder[0](stylized)
+        for i, (content_feat, style_feat) in enumerate(
+                list(zip(content_feats[:-1], style_feats[:-1]))[::-1]):
+            cm, cs = calc_mean_std(content_feat)
+            sm, ss = calc_mean_std(style_feat)
+            stylized = plan.run(_block_plan(self.rp_decoder[i + 1]), stylized,
+                                first_aux=ops.adain_params(cm, cs, sm, ss),
+                                first_in_op=ops.IN_ADD_ADAIN, first_content=content_feat)
+        return stylized
+
+    def forward(self, content, style, alpha=1.0):
+        """Loss dict of adain_rp.py:322-345 (inference kernels: call under torch.no_grad())."""
+        assert 0 <= alpha <= 1
+        content_feats = self.encode_rp_intermediate(content)
+        style_feats = self.encode_rp_intermediate(style)
+        stylized = self.decode(content_feats, style_feats)
         down_stylized_feats = self.encode_with_intermediate(stylized)
         down_style_feats = self.encode_with_intermediate(style)
         down_content_feats = self.encode_with_intermediate(content)

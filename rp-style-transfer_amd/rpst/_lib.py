@@ -38,6 +38,7 @@ SIGNATURES = {
     "rpst_conv2d_stats": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I,
                                _P, _P, _F, _P, _SZ, _P]),
     "rpst_conv2d": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "rpst_conv2d_skip_adain": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_maxpool2x2_ceil": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "rpst_upsample_nearest2x": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "rpst_sanet_attention_workspace_size": (_SZ, [_I, _I]),

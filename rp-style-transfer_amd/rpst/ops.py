@@ -14,7 +14,18 @@ import torch
 from . import _lib
 
 PAD_ZERO, PAD_REFLECT = 0, 1
-IN_NONE, IN_MAXPOOL2, IN_UPSAMPLE2, IN_ADD_UPSAMPLE2, IN_ADAIN = 0, 1, 2, 3, 4
+IN_NONE, IN_MAXPOOL2, IN_UPSAMPLE2, IN_ADD_UPSAMPLE2, IN_ADAIN, IN_ADD_ADAIN = 0, 1, 2, 3, 4, 5
+ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2  # conv epilogue: none / ReLU / LeakyReLU(0.2)
+
+
+def _act(relu) -> int:
+    """The conv `relu` argument: a bool (ReLU or not) or an ACT_* code."""
+    if isinstance(relu, bool):
+        return ACT_RELU if relu else ACT_NONE
+    a = int(relu)
+    if a not in (ACT_NONE, ACT_RELU, ACT_LRELU):
+        raise ValueError(f"rpst: unknown activation code {relu}")
+    return a
 
 
 class Trace:
@@ -171,8 +182,10 @@ def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], 
            ksize: int, pad: int = PAD_ZERO, in_op: int = IN_NONE, relu: bool = False,
            aux: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out = [relu](conv_k(in_op(x)) + bias) [+ residual]; see include/rpst.h."""
+    """out = act(conv_k(in_op(x)) + bias) [+ residual]; see include/rpst.h."""
     assert x.dim() == 4
+    if in_op == IN_ADD_ADAIN:
+        raise ValueError("rpst: the skip-AdaIN operator takes two inputs: use conv2d_skip_adain")
     _check(x, packed, bias, aux, residual)
     x = _c(x)
     n, cin, hs, ws = x.shape
@@ -193,8 +206,31 @@ def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], 
                  4.0 * (x.numel() + n * cout * h * w)):
         _lib.call("rpst_conv2d", x.data_ptr(), _ptr(aux), packed.data_ptr(),
                   _ptr(None if bias is None else _c(bias.detach())), _ptr(residual),
-                  out.data_ptr(), n, cin, hs, ws, cout, ksize, pad, in_op, int(bool(relu)),
+                  out.data_ptr(), n, cin, hs, ws, cout, ksize, pad, in_op, _act(relu),
                   _stream(x))
+    return out
+
+
+def conv2d_skip_adain(x: torch.Tensor, content: torch.Tensor, params: torch.Tensor,
+                      packed: torch.Tensor, bias: Optional[torch.Tensor], cout: int,
+                      ksize: int = 3, pad: int = PAD_REFLECT, relu=ACT_LRELU,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = act(conv(pad(x + AdaIN(content))) + bias): the skip fusion of
+    MultiScaleAdaINRPNet.decode (adain_rp.py:301); params = adain_params(...) of
+    (content, style) — the sum is formed in the conv's tile loader."""
+    assert x.dim() == 4 and x.shape == content.shape
+    _check(x, content, params, packed, bias)
+    x, content, params = _c(x), _c(content), _c(params)
+    n, cin, h, w = x.shape
+    assert params.numel() == 4 * n * cin, "params = [mean_c|mean_s|std_c|std_s]"
+    if out is None:
+        out = torch.empty((n, cout, h, w), device=x.device, dtype=torch.float32)
+    with _traced(_conv_name(ksize, cin, cout, h, w, n, IN_ADD_ADAIN),
+                 2.0 * n * cout * h * w * cin * ksize * ksize,
+                 4.0 * (2 * x.numel() + n * cout * h * w)):
+        _lib.call("rpst_conv2d_skip_adain", x.data_ptr(), content.data_ptr(), params.data_ptr(),
+                  packed.data_ptr(), _ptr(None if bias is None else _c(bias.detach())),
+                  out.data_ptr(), n, cin, h, w, cout, ksize, pad, _act(relu), _stream(x))
     return out
 
 
@@ -218,7 +254,7 @@ def conv2d_stats(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Ten
                  4.0 * (x.numel() + n * cout * h * w)):
         _lib.call("rpst_conv2d_stats", x.data_ptr(), _ptr(aux), packed.data_ptr(),
                   _ptr(None if bias is None else _c(bias.detach())), None, out.data_ptr(), n,
-                  cin, hs, ws, cout, ksize, pad, in_op, int(bool(relu)), mean.data_ptr(),
+                  cin, hs, ws, cout, ksize, pad, in_op, _act(relu), mean.data_ptr(),
                   std.data_ptr(), eps, ws_t.data_ptr(), nbytes, _stream(x))
     return out, mean, std
 

@@ -1,7 +1,8 @@
 """Compile an nn.Sequential conv stack into fused rpst conv launches and run it.
 
 The reference builds its stacks from plain layers (network/base.py:25-111,363-396,
-sanet.py:162-192): [MaxPool2d | Upsample] -> [ReflectionPad2d] -> Conv2d -> [ReLU].
+sanet.py:162-192) and Conv2dBlocks (base.py:114-198): [MaxPool2d | Upsample] ->
+[ReflectionPad2d | ZeroPad2d] -> Conv2d -> [ReLU | LeakyReLU(0.2)].
 Each such group becomes ONE rpst_conv2d launch: the pool/upsample and the padding are
 applied by the conv kernel's tile loader and ReLU by its epilogue, so no intermediate
 (padded, pooled or upsampled) tensor is ever written to HBM.
@@ -22,7 +23,7 @@ class ConvStep:
     conv: nn.Conv2d
     pad: int
     in_op: int
-    relu: bool
+    relu: int  # ops.ACT_* epilogue activation
 
 
 @dataclass
@@ -31,19 +32,34 @@ class OpStep:
 
 
 def _is_pad1(m: nn.Module) -> bool:
-    return isinstance(m, nn.ReflectionPad2d) and tuple(m.padding) == (1, 1, 1, 1)
+    return isinstance(m, (nn.ReflectionPad2d, nn.ZeroPad2d)) and tuple(m.padding) == (1, 1, 1, 1)
+
+
+def block_layers(blk: nn.Module) -> List[nn.Module]:
+    """The layer sequence of a Conv2dBlock (network/base.py:187-198): pad, conv, the 1x1
+    inception convs, activation. Norm / attention variants are rejected at construction
+    by network.base.Conv2dBlock."""
+    layers = [blk.pad, blk.conv]
+    if blk.inception is not None:
+        layers += [seq[0] for seq in blk.inception]
+    if blk.activation is not None:
+        layers.append(blk.activation)
+    return layers
 
 
 def compile_layers(layers: Iterable[nn.Module]) -> List[object]:
     steps: List[object] = []
     in_op = ops.IN_NONE
     reflect = False
+    zero_pad = False
     last_conv: Optional[ConvStep] = None
     for m in layers:
-        if isinstance(m, nn.ReLU):
+        if isinstance(m, (nn.ReLU, nn.LeakyReLU)):
             if last_conv is None or last_conv.relu:
-                raise NotImplementedError("rpst plan: ReLU must directly follow a Conv2d")
-            last_conv.relu = True
+                raise NotImplementedError("rpst plan: an activation must directly follow a Conv2d")
+            if isinstance(m, nn.LeakyReLU) and m.negative_slope != 0.2:
+                raise NotImplementedError(f"rpst plan: unsupported {m} (slope 0.2 only)")
+            last_conv.relu = ops.ACT_RELU if isinstance(m, nn.ReLU) else ops.ACT_LRELU
             continue
         last_conv = None
         if isinstance(m, nn.MaxPool2d):
@@ -61,10 +77,13 @@ def compile_layers(layers: Iterable[nn.Module]) -> List[object]:
             if in_op != ops.IN_NONE or reflect:
                 raise NotImplementedError("rpst plan: upsample after pad/op")
             in_op = ops.IN_UPSAMPLE2
-        elif isinstance(m, nn.ReflectionPad2d):
-            if not _is_pad1(m) or reflect:
+        elif isinstance(m, (nn.ReflectionPad2d, nn.ZeroPad2d)):
+            if not _is_pad1(m) or reflect or zero_pad:
                 raise NotImplementedError(f"rpst plan: unsupported {m}")
-            reflect = True
+            if isinstance(m, nn.ReflectionPad2d):
+                reflect = True
+            else:
+                zero_pad = True
         elif isinstance(m, nn.Conv2d):
             k = tuple(m.kernel_size)
             if (tuple(m.stride) != (1, 1) or tuple(m.dilation) != (1, 1) or m.groups != 1
@@ -74,22 +93,24 @@ def compile_layers(layers: Iterable[nn.Module]) -> List[object]:
             if k == (3, 3):
                 if reflect and pad_t == (0, 0):
                     pad = ops.PAD_REFLECT
-                elif not reflect and pad_t == (1, 1) and m.padding_mode == "zeros":
+                elif zero_pad and pad_t == (0, 0):
+                    pad = ops.PAD_ZERO
+                elif not reflect and not zero_pad and pad_t == (1, 1) and m.padding_mode == "zeros":
                     pad = ops.PAD_ZERO
                 else:
                     raise NotImplementedError(f"rpst plan: unsupported padding for {m}")
             else:
-                if reflect or pad_t != (0, 0) or in_op != ops.IN_NONE:
+                if reflect or zero_pad or pad_t != (0, 0) or in_op != ops.IN_NONE:
                     raise NotImplementedError(f"rpst plan: unsupported 1x1 conv {m}")
                 pad = ops.PAD_ZERO
-            step = ConvStep(m, pad, in_op, False)
+            step = ConvStep(m, pad, in_op, ops.ACT_NONE)
             steps.append(step)
             last_conv = step
-            in_op, reflect = ops.IN_NONE, False
+            in_op, reflect, zero_pad = ops.IN_NONE, False, False
         else:
             raise NotImplementedError(f"rpst plan: unsupported layer {type(m).__name__}")
-    if reflect:
-        raise NotImplementedError("rpst plan: trailing ReflectionPad2d")
+    if reflect or zero_pad:
+        raise NotImplementedError("rpst plan: trailing padding layer")
     if in_op != ops.IN_NONE:
         steps.append(OpStep(in_op))
     return steps
@@ -117,9 +138,10 @@ def run_conv_step(step: ConvStep, x: torch.Tensor, aux=None, residual=None) -> t
 
 
 def run(steps: List[object], x: torch.Tensor, first_aux=None, first_in_op=None,
-        stats_last: bool = False):
+        stats_last: bool = False, first_content=None):
     """Run a compiled plan. first_in_op/first_aux override the first conv's input operator
-    (e.g. RPST_IN_ADAIN to fuse AdaIN into the decoder's first conv); stats_last makes the
+    (e.g. RPST_IN_ADAIN to fuse AdaIN into the decoder's first conv; RPST_IN_ADD_ADAIN
+    with first_content = the skip feature, for x + AdaIN(content)); stats_last makes the
     last conv also return calc_mean_std of its output -> (x, mean, std)."""
     mean = std = None
     for i, s in enumerate(steps):
@@ -130,7 +152,13 @@ def run(steps: List[object], x: torch.Tensor, first_aux=None, first_in_op=None,
                     raise NotImplementedError("rpst plan: first conv already has an input op")
                 in_op, aux = first_in_op, first_aux
             c = s.conv
-            if stats_last and i == len(steps) - 1:
+            if in_op == ops.IN_ADD_ADAIN:
+                if stats_last and i == len(steps) - 1:
+                    raise NotImplementedError("rpst plan: skip-AdaIN conv with statistics")
+                x = ops.conv2d_skip_adain(x, first_content, aux, packed_weight(c), c.bias,
+                                          c.out_channels, c.kernel_size[0], pad=s.pad,
+                                          relu=s.relu)
+            elif stats_last and i == len(steps) - 1:
                 x, mean, std = ops.conv2d_stats(x, packed_weight(c), c.bias, c.out_channels,
                                                 c.kernel_size[0], pad=s.pad, in_op=in_op,
                                                 relu=s.relu, aux=aux)

@@ -247,6 +247,47 @@ def gen_vgg(net):
     np.savez_compressed(os.path.join(HERE, "vgg.npz"), **out)
 
 
+def multiscale_config(hidden, blocks=5, inception=0):
+    cfg = rp_config(hidden, blocks)
+    cfg.update({"shuffle": False, "shuffle_layers": 1, "sort": False,
+                "stylized_layers": blocks, "enc_stack_way": "constant",
+                "inception_num": inception, "attention": "none"})
+    return cfg
+
+
+def gen_multiscale(net):
+    """MultiScaleAdaINRPNet.test, constant stack."""
+    out = {}
+    cases = [(8, 5, 0, (2, 3, 24, 32), 41), (32, 5, 0, (1, 3, 16, 16), 42),
+             (8, 3, 1, (1, 3, 9, 13), 43)]
+    for i, (hid, blocks, inc, shp, seed) in enumerate(cases):
+        m = net.MultiScaleAdaINRPNet(multiscale_config(hid, blocks, inc), copy.deepcopy(net.vgg))
+        ck = synth_model_(m, seed)
+        c = synth.image(4100 + i, shp)
+        s = synth.image(4200 + i, shp)
+        y = m.test(t(c), t(s))
+        out.update({f"hidden{i}": hid, f"blocks{i}": blocks, f"inception{i}": inc,
+                    f"seed{i}": seed, f"checksum{i}": ck, f"content{i}": c, f"style{i}": s,
+                    f"out{i}": y.numpy()})
+    np.savez_compressed(os.path.join(HERE, "multiscale.npz"), n=len(cases), **out)
+
+
+def gen_sourcenet(net):
+    """SourceNet.test, classic AdaIN on VGG relu4_1."""
+    out = {}
+    cases = [((1, 3, 32, 32), 51), ((2, 3, 24, 40), 52)]
+    for i, (shp, seed) in enumerate(cases):
+        m = net.SourceNet({"use_mask": False, "content_weight": 1.0, "style_weight": 10.0},
+                          copy.deepcopy(net.vgg))
+        ck = synth_model_(m, seed)
+        c = synth.image(5100 + i, shp)
+        s = synth.image(5200 + i, shp)
+        y = m.test(t(c), t(s))
+        out.update({f"seed{i}": seed, f"checksum{i}": ck, f"content{i}": c, f"style{i}": s,
+                    f"out{i}": y.numpy()})
+    np.savez_compressed(os.path.join(HERE, "sourcenet.npz"), n=len(cases), **out)
+
+
 def gen_keys(net):
     """state_dict key/shape lists of the reference models (checkpoint compatibility)."""
     import json
@@ -255,6 +296,10 @@ def gen_keys(net):
         "AdaINRPNet": net.AdaINRPNet(rp_config(16), vgg),
         "WCTRPNet": net.WCTRPNet(rp_config(16), vgg),
         "SAModel": net.SAModel({}, vgg, 0, 512),
+        "MultiScaleAdaINRPNet": net.MultiScaleAdaINRPNet(multiscale_config(32, 5, 0), vgg),
+        "MultiScaleAdaINRPNet_inception1": net.MultiScaleAdaINRPNet(
+            multiscale_config(16, 4, 1), vgg),
+        "SourceNet": net.SourceNet({"use_mask": False}, vgg),
         "vgg": net.vgg,
         "decoder": net.decoder,
     }
@@ -263,17 +308,18 @@ def gen_keys(net):
         json.dump(out, f, indent=0)
 
 
+GENERATORS = {"keys": gen_keys, "stats": gen_stats, "adain_rp": gen_adain_rp,
+              "forward": gen_forward, "wct": gen_wct, "sanet": gen_sanet, "vgg": gen_vgg,
+              "multiscale": gen_multiscale, "sourcenet": gen_sourcenet}
+
+
 def main():
+    """python gen_golden.py [name ...]  (default: all)"""
     torch.set_num_threads(8)
     torch.manual_seed(0)
     net = _import_reference()
-    gen_keys(net)
-    gen_stats(net)
-    gen_adain_rp(net)
-    gen_forward(net)
-    gen_wct(net)
-    gen_sanet(net)
-    gen_vgg(net)
+    for name in (sys.argv[1:] or list(GENERATORS)):
+        GENERATORS[name](net)
     print("goldens written to", HERE)
 
 

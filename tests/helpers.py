@@ -36,3 +36,16 @@ def state_dict_of(model):
 def rp_config(hidden, blocks=5):
     return {"rp_blocks": blocks, "hidden_dim": hidden, "content_weight": 1.0,
             "style_weight": 10.0, "resume": False, "use_mask": False}
+
+
+def multiscale_config(hidden, blocks=5, inception=0):
+    """MultiScaleAdaINRPNet config (config/rl/train_constant_multiscale_rp_adain_recon.yaml
+    with hidden/blocks/inception varied)."""
+    cfg = rp_config(hidden, blocks)
+    cfg.update({"shuffle": False, "shuffle_layers": 1, "sort": False,
+                "stylized_layers": blocks, "enc_stack_way": "constant",
+                "inception_num": inception, "attention": "none"})
+    return cfg
+
+
+SOURCE_CONFIG = {"use_mask": False, "content_weight": 1.0, "style_weight": 10.0}

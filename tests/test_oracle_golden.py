@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import rel_l2, rp_config, state_dict_of, synth_
+from helpers import SOURCE_CONFIG, multiscale_config, rel_l2, rp_config, state_dict_of, synth_
 from oracle import restate as R
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -133,7 +133,33 @@ def test_samodel_test(golden):
         assert rel_l2(out, g[f"model_out{i}"]) < 1e-6
 
 
-@pytest.mark.parametrize("name", ["AdaINRPNet", "WCTRPNet", "SAModel", "vgg", "decoder"])
+def test_multiscale_test(golden):
+    """MultiScaleAdaINRPNet.test against the reference's outputs."""
+    import network as net
+    g = golden("multiscale")
+    for i in range(int(g["n"])):
+        hid, blocks, inc = int(g[f"hidden{i}"]), int(g[f"blocks{i}"]), int(g[f"inception{i}"])
+        m = net.MultiScaleAdaINRPNet(multiscale_config(hid, blocks, inc), copy.deepcopy(net.vgg))
+        np.testing.assert_allclose(synth_(m, int(g[f"seed{i}"])), g[f"checksum{i}"], rtol=1e-12)
+        out = R.multiscale_test(t(g[f"content{i}"]), t(g[f"style{i}"]), state_dict_of(m),
+                                blocks, inc)
+        assert rel_l2(out, g[f"out{i}"]) < 1e-6, (i, rel_l2(out, g[f"out{i}"]))
+
+
+def test_sourcenet_test(golden):
+    """SourceNet.test (classic AdaIN) against the reference."""
+    import network as net
+    g = golden("sourcenet")
+    for i in range(int(g["n"])):
+        m = net.SourceNet(SOURCE_CONFIG, copy.deepcopy(net.vgg))
+        np.testing.assert_allclose(synth_(m, int(g[f"seed{i}"])), g[f"checksum{i}"], rtol=1e-12)
+        out = R.sourcenet_test(t(g[f"content{i}"]), t(g[f"style{i}"]), state_dict_of(m))
+        assert rel_l2(out, g[f"out{i}"]) < 1e-6, (i, rel_l2(out, g[f"out{i}"]))
+
+
+@pytest.mark.parametrize("name", ["AdaINRPNet", "WCTRPNet", "SAModel", "vgg", "decoder",
+                                  "MultiScaleAdaINRPNet", "MultiScaleAdaINRPNet_inception1",
+                                  "SourceNet"])
 def test_state_dict_keys_match_reference(name):
     """Checkpoint compatibility: same keys and shapes as the reference modules."""
     import network as net
@@ -142,6 +168,11 @@ def test_state_dict_keys_match_reference(name):
     mine = {"AdaINRPNet": lambda: net.AdaINRPNet(rp_config(16), vgg),
             "WCTRPNet": lambda: net.WCTRPNet(rp_config(16), vgg),
             "SAModel": lambda: net.SAModel({}, vgg, 0, 512),
+            "MultiScaleAdaINRPNet": lambda: net.MultiScaleAdaINRPNet(
+                multiscale_config(32, 5, 0), vgg),
+            "MultiScaleAdaINRPNet_inception1": lambda: net.MultiScaleAdaINRPNet(
+                multiscale_config(16, 4, 1), vgg),
+            "SourceNet": lambda: net.SourceNet({"use_mask": False}, vgg),
             "vgg": lambda: net.vgg, "decoder": lambda: net.decoder}[name]()
     got = [[k, list(v.shape)] for k, v in mine.state_dict().items()]
     assert got == ref
