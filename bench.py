@@ -5,7 +5,7 @@ hidden_dim=16), batch 32 per GPU, 512x512 fp32, synthetic U[0,1) images and
 He-uniform synthetic weights (no checkpoints exist offline). One "step" = one test()
 call over the whole per-GPU batch, inputs already resident in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--model adain|wct|sanet]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model adain|wct|sanet|multiscale|source]
 
 N>1 runs one process per GPU under torch.distributed.run; each rank stylises its own
 batch (weak scaling: the batch is split per image, no collective touches the data; a
@@ -49,18 +49,33 @@ def build_model(kind, dev):
         m = net.AdaINRPNet(cfg, copy.deepcopy(net.vgg))
     elif kind == "wct":
         m = net.WCTRPNet(cfg, copy.deepcopy(net.vgg))
+    elif kind == "multiscale":
+        m = net.MultiScaleAdaINRPNet(MULTISCALE_CONFIG, copy.deepcopy(net.vgg))
+    elif kind == "source":
+        m = net.SourceNet(SOURCE_CONFIG, copy.deepcopy(net.vgg))
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, 512)
     synth.synth_module_(m, 0)
     return m.to(dev)
 
 
+# MultiScaleAdaINRPNet as config/rl/train_constant_multiscale_rp_adain_recon.yaml
+# (hidden 32, 5 constant blocks, no shuffle/sort/mask/attention); SourceNet (classic AdaIN)
+MULTISCALE_CONFIG = {"rp_blocks": 5, "hidden_dim": 32, "content_weight": 1.0,
+                     "style_weight": 10.0, "resume": False, "use_mask": False, "shuffle": False,
+                     "shuffle_layers": 1, "sort": False, "stylized_layers": 5,
+                     "enc_stack_way": "constant", "inception_num": 0, "attention": "none"}
+SOURCE_CONFIG = {"use_mask": False, "content_weight": 1.0, "style_weight": 10.0}
+
+
 WORKLOADS = {
     "adain": "AdaINRPNet.test() rp_blocks=5 hidden_dim=16, 512x512 (BASELINE configs[1])",
     "wct": "WCTRPNet.test() rp_blocks=5 hidden_dim=16, 512x512, fp64 WCT (BASELINE configs[2])",
     "sanet": "SAModel.test() VGG relu1_1-5_1 + SANet 4_1/5_1 + decoder, 512x512 (BASELINE configs[3])",
+    "multiscale": "MultiScaleAdaINRPNet.test() constant stack hidden 32 x 5, 512x512 (SURVEY 8(f) rank 1)",
+    "source": "SourceNet.test() VGG relu4_1 AdaIN + decoder, 512x512 (SURVEY 8(f) rank 3)",
 }
-DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32}
+DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32, "multiscale": 32, "source": 32}
 
 
 def cpu_baseline(kind, size, budget_s=12.0):
@@ -75,11 +90,18 @@ def cpu_baseline(kind, size, budget_s=12.0):
     elif kind == "wct":
         m = net.WCTRPNet(cfg, copy.deepcopy(net.vgg))
         fn = lambda c, s, sd: R.wct_rp_test(c, s, sd, 5)  # noqa: E731
+    elif kind == "multiscale":
+        m = net.MultiScaleAdaINRPNet(MULTISCALE_CONFIG, copy.deepcopy(net.vgg))
+        fn = lambda c, s, sd: R.multiscale_test(c, s, sd, 5)  # noqa: E731
+    elif kind == "source":
+        m = net.SourceNet(SOURCE_CONFIG, copy.deepcopy(net.vgg))
+        fn = R.sourcenet_test
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, size)
         fn = R.samodel_test
     synth.synth_module_(m, 0)
-    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    # (.cpu(): SourceNet shares the module-level decoder, which build_model moved to the GPU)
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     c = torch.from_numpy(synth.image(11, (1, 3, size, size)))
     s = torch.from_numpy(synth.image(12, (1, 3, size, size)))
     threads = torch.get_num_threads()
@@ -193,7 +215,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", choices=["adain", "wct", "sanet"], default="adain")
+    ap.add_argument("--model", choices=list(WORKLOADS), default="adain")
     ap.add_argument("--batch", type=int, default=None, help="images per GPU")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
