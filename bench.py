@@ -53,6 +53,8 @@ def build_model(kind, dev):
         m = net.MultiScaleAdaINRPNet(MULTISCALE_CONFIG, copy.deepcopy(net.vgg))
     elif kind == "source":
         m = net.SourceNet(SOURCE_CONFIG, copy.deepcopy(net.vgg))
+    elif kind == "adaptive":
+        m = net.AdaptiveSAModel(ADAPTIVE_CONFIG, copy.deepcopy(net.vgg), 0, 512)
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, 512)
     synth.synth_module_(m, 0)
@@ -66,6 +68,9 @@ MULTISCALE_CONFIG = {"rp_blocks": 5, "hidden_dim": 32, "content_weight": 1.0,
                      "shuffle_layers": 1, "sort": False, "stylized_layers": 5,
                      "enc_stack_way": "constant", "inception_num": 0, "attention": "none"}
 SOURCE_CONFIG = {"use_mask": False, "content_weight": 1.0, "style_weight": 10.0}
+# config/rl/train_dynamic_sanet.yaml: ada_module 'relu' (AEALReluModule)
+ADAPTIVE_CONFIG = {"ada_module": "relu", "content_weight": 1.0, "style_weight": 3.0,
+                   "l_identity1_weight": 50.0, "l_identity2_weight": 1.0}
 
 
 WORKLOADS = {
@@ -74,8 +79,11 @@ WORKLOADS = {
     "sanet": "SAModel.test() VGG relu1_1-5_1 + SANet 4_1/5_1 + decoder, 512x512 (BASELINE configs[3])",
     "multiscale": "MultiScaleAdaINRPNet.test() constant stack hidden 32 x 5, 512x512 (SURVEY 8(f) rank 1)",
     "source": "SourceNet.test() VGG relu4_1 AdaIN + decoder, 512x512 (SURVEY 8(f) rank 3)",
+    "adaptive": "AdaptiveSAModel.test() ada_module=relu (AEA clamp) VGG relu1_1-5_1 + decoder, "
+                "512x512 (SURVEY 8(f) rank 3)",
 }
-DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32, "multiscale": 32, "source": 32}
+DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32, "multiscale": 32, "source": 32,
+                 "adaptive": 32}
 
 
 def cpu_baseline(kind, size, budget_s=12.0):
@@ -96,6 +104,9 @@ def cpu_baseline(kind, size, budget_s=12.0):
     elif kind == "source":
         m = net.SourceNet(SOURCE_CONFIG, copy.deepcopy(net.vgg))
         fn = R.sourcenet_test
+    elif kind == "adaptive":
+        m = net.AdaptiveSAModel(ADAPTIVE_CONFIG, copy.deepcopy(net.vgg), 0, size)
+        fn = lambda c, s, sd: R.adaptive_samodel_test(c, s, sd, "relu")  # noqa: E731
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, size)
         fn = R.samodel_test

@@ -152,6 +152,41 @@ int rpst_sanet_attention(const float* F, const float* G, const float* H, float* 
                          int C, int HW, void* workspace, size_t workspace_bytes,
                          rpst_stream_t stream);
 
+/* ---- f3: AdaptiveSANet  network/sanet.py:12-18, 26-71, 100-138 ----
+ * cal_affinity_matrix(c, s) (sanet.py:12-18): out[b] = normalize(c[b])^T normalize(s[b]),
+ * normalize = x / max(||x||_2 over channels, 1e-12). c, s (B, C, HW) -> out (B, HW, HW).
+ * Workspace: rpst_cosine_affinity_workspace_size(B, C, HW). */
+size_t rpst_cosine_affinity_workspace_size(int B, int C, int HW);
+int rpst_cosine_affinity(const float* content, const float* style, float* out, int B, int C,
+                         int HW, void* workspace, size_t workspace_bytes, rpst_stream_t stream);
+
+/* AEAModule.forward (mode 0, sanet.py:42-47) / AEALReluModule.forward (mode 1, :63-69):
+ * clamp[b,i] = head(w2 . LeakyReLU_0.2(W1 x[b,i,:] + b1) + b2), head = sigmoid(t)*interval
+ * + from (mode 0) or (tanh(t)+1)/2 (mode 1); out_fx = sigmoid(scale (fx - clamp)) (mode 0)
+ * or softmax_rows(relu(fx - clamp)) (mode 1). x, fx, out_fx (B, HW, HW); W1 (hidden, HW),
+ * b1 (hidden), w2 (hidden), b2 (1) device pointers; out_clamp (B, HW).
+ * Workspace: rpst_aea_clamp_workspace_size(B, HW, hidden). */
+size_t rpst_aea_clamp_workspace_size(int B, int HW, int hidden);
+int rpst_aea_clamp(const float* x, const float* fx, const float* w1, const float* b1,
+                   const float* w2, const float* b2, int hidden, int mode, float scale,
+                   float from, float interval, float* out_fx, float* out_clamp, int B, int HW,
+                   void* workspace, size_t workspace_bytes, rpst_stream_t stream);
+
+/* AdaptiveSANet attention core (sanet.py:106-124): with S = F^T G and P = softmax_rows(S),
+ * O[b] = H[b] Q^T with Q = AEA(cal_affinity_matrix(content, style), P) as rpst_aea_clamp
+ * (mode/scale/from/interval). P and Q are formed while S is staged into the second GEMM and
+ * are never stored unless claim_before / claim_after (B, HW, HW) are non-null;
+ * claim_value (B, HW) receives the clamp values when non-null.
+ * Workspace: rpst_adaptive_attention_workspace_size(B, C, HW, hidden). */
+size_t rpst_adaptive_attention_workspace_size(int B, int C, int HW, int hidden);
+int rpst_adaptive_attention(const float* F, const float* G, const float* H,
+                            const float* content, const float* style, const float* w1,
+                            const float* b1, const float* w2, const float* b2, int hidden,
+                            int mode, float scale, float from, float interval, float* O,
+                            float* claim_value, float* claim_before, float* claim_after, int B,
+                            int C, int HW, void* workspace, size_t workspace_bytes,
+                            rpst_stream_t stream);
+
 /* ---- a7: matrix_sqrt / matrix_inv_sqrt  network/wct_rp.py:7-40 ----------------------
  * out[b] = (A[b] + 1e-4 I)^(+1/2) (inverse = 0) or ^(-1/2) (inverse = 1) for symmetric PSD
  * fp64 n x n matrices, batch of `batch`. Coupled Newton-Schulz (fixed 40 steps); equal to

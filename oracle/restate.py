@@ -279,6 +279,62 @@ def samodel_test(content: Tensor, style: Tensor, sd: SD) -> Tensor:
         return decoder(fusion, sd, "decoder.")
 
 
+# ---- f3: AdaptiveSANet (sanet.py:12-18, 26-71, 100-160, 278-345) -----------------
+def cal_affinity_matrix(content: Tensor, style: Tensor) -> Tensor:
+    """sanet.py:12-18: cosine similarity of positions over channels, (B, HW, HW)."""
+    b, c, h, w = content.shape
+    nc = F.normalize(content.reshape(b, c, h * w), dim=1)
+    ns = F.normalize(style.reshape(b, c, h * w), dim=1)
+    return torch.bmm(nc.permute(0, 2, 1), ns)
+
+
+def aea(x: Tensor, f_x: Tensor, sd: SD, prefix: str, mode: str, scale_value: float = 50.0,
+        from_value: float = 0.4, value_interval: float = 0.5) -> Tuple[Tensor, Tensor]:
+    """AEAModule.forward (mode 'aea', sanet.py:42-47) / AEALReluModule.forward (else,
+    sanet.py:63-69) with f_psi = Linear, LeakyReLU(0.2), Linear, Sigmoid|Tanh."""
+    b, hw, c = x.shape
+    z = F.leaky_relu(F.linear(x.reshape(b * hw, c), sd[prefix + "f_psi.0.weight"],
+                              sd[prefix + "f_psi.0.bias"]), 0.2)
+    t = F.linear(z, sd[prefix + "f_psi.2.weight"], sd[prefix + "f_psi.2.bias"])
+    if mode == "aea":
+        clamp = (torch.sigmoid(t) * value_interval + from_value).view(b, hw, 1)
+        return torch.sigmoid(scale_value * (f_x - clamp)), clamp
+    clamp = ((torch.tanh(t) + 1) / 2).view(b, hw, 1)
+    return torch.softmax(F.relu(f_x - clamp), dim=-1), clamp
+
+
+def adaptive_sanet(content: Tensor, style: Tensor, sd: SD, prefix: str, mode: str):
+    """AdaptiveSANet.forward (sanet.py:106-131) -> (out, claim_value)."""
+    Fm = conv(mean_variance_norm(content), sd, prefix + "f", "none", False)
+    G = conv(mean_variance_norm(style), sd, prefix + "g", "none", False)
+    H = conv(style, sd, prefix + "h", "none", False)
+    b, c, h, w = Fm.shape
+    A = cal_affinity_matrix(content, style)
+    S = torch.softmax(torch.bmm(Fm.view(b, -1, w * h).permute(0, 2, 1),
+                                G.view(b, -1, w * h)), dim=-1)
+    Q, clamp = aea(A, S, sd, prefix + "attention_layer.", mode)
+    O = torch.bmm(H.view(b, -1, w * h), Q.permute(0, 2, 1)).view(content.shape)
+    return conv(O, sd, prefix + "out_conv", "none", False) + content, clamp
+
+
+def adaptive_transform(c4, s4, c5, s5, sd: SD, prefix: str, mode: str) -> Tensor:
+    """AdaptiveTransform.forward (sanet.py:159-160)."""
+    a = adaptive_sanet(c4, s4, sd, prefix + "sanet4_1.", mode)[0]
+    b = F.interpolate(adaptive_sanet(c5, s5, sd, prefix + "sanet5_1.", mode)[0],
+                      scale_factor=2, mode="nearest")
+    return conv(a + b, sd, prefix + "merge_conv", "reflect", False)
+
+
+def adaptive_samodel_test(content: Tensor, style: Tensor, sd: SD, mode: str) -> Tensor:
+    """AdaptiveSAModel.test (sanet.py:334-341) without the claim-map plots."""
+    with torch.no_grad():
+        sfeat = encode_with_intermediate(style, sd, 5)
+        cfeat = encode_with_intermediate(content, sd, 5)
+        fusion = adaptive_transform(cfeat[3], sfeat[3], cfeat[4], sfeat[4], sd, "transform.",
+                                    mode)
+        return decoder(fusion, sd, "decoder.")
+
+
 def rel_l2(a: Tensor, b: Tensor) -> float:
     a = a.double()
     b = b.double()

@@ -24,21 +24,55 @@ enum { LAY_RK = 0, LAY_KR = 1 };
 
 constexpr int kGBM = 128, kGBN = 128, kGBK = 32, kGPad = 4;
 
+// B-operand staging transforms (applied to S while it is staged; row r = query index):
+//   BX_NONE   v
+//   BX_EXP    exp(v - m_r)                                  softmax numerator (SANet)
+//   BX_AEA    sigmoid(scale (exp(v - m_r) inv_r - c_r))     AEAModule clamp (sanet.py:45-47)
+//   BX_AEAR   exp(relu(exp(v - m_r) inv_r - c_r) - m2_r)    AEALReluModule (sanet.py:66-69),
+//             numerator of softmax(relu(P - c)); 1/l2_r is the epilogue column scale
+enum { BX_NONE = 0, BX_EXP = 1, BX_AEA = 2, BX_AEAR = 3 };
+
+// Per-row vectors of the B operand's transform (each indexed batch * sV + r).
+struct RowVec {
+  const float* m;      // row max of S
+  const float* inv;    // 1 / sum exp(S - m)
+  const float* clamp;  // AEA threshold per query row
+  const float* m2;     // BX_AEAR: row max of relu(P - c)
+  float scale;         // BX_AEA: sigmoid slope (scale_value)
+};
+
 struct GemmArgs {
   const float* A;
   const float* B;
   float* C;
-  const float* rowmax;    // EXPB: per-n max (B operand row index n)
+  RowVec rv;              // B-operand transform vectors (BX_* != BX_NONE)
   const float* colscale;  // optional per-n multiplier in the epilogue
+  const float* colbias;   // optional per-n bias added after the scale (nn.Linear bias)
+  int act;                // epilogue activation: 0 none, 1 LeakyReLU(0.2)
   int M, N, K, lda, ldb, ldc;
-  int64_t sA, sB, sC, sV;  // batch strides (elements); sV for rowmax / colscale
+  int64_t sA, sB, sC, sV;  // batch strides (elements); sV for the row / column vectors
 };
 
+template <int BX>
+__device__ __forceinline__ float bx_apply(float v, float m, float inv, float c, float m2,
+                                          float scale) {
+  if (BX == BX_EXP) return expf(v - m);
+  if (BX == BX_AEA) {
+    const float p = expf(v - m) * inv;
+    return 1.f / (1.f + expf(-(scale * (p - c))));
+  }
+  if (BX == BX_AEAR) {
+    const float p = expf(v - m) * inv;
+    return expf(fmaxf(p - c, 0.f) - m2);
+  }
+  return v;
+}
+
 // Stage a kGBK x 128 tile of operand X (rows r0.., k0..) into registers.
-template <int LAY, bool EXP, bool VEC>
+template <int LAY, int BX, bool VEC>
 __device__ __forceinline__ void g_load(float (&reg)[16], const float* __restrict__ X, int ld,
-                                       int r0, int k0, int R, int K,
-                                       const float* __restrict__ rmax, int tid) {
+                                       int r0, int k0, int R, int K, const RowVec& rv,
+                                       int64_t voff, int tid) {
   if (LAY == LAY_KR) {
     // thread -> (k = tid>>5 + 8p, r4 = (tid&31)*4), 4 passes of 8 k-rows
     const int kk = tid >> 5, r = r0 + (tid & 31) * 4;
@@ -77,10 +111,15 @@ __device__ __forceinline__ void g_load(float (&reg)[16], const float* __restrict
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = (r < R && k + e < K) ? X[(int64_t)r * ld + k + e] : 0.f;
       }
-      if (EXP) {
-        const float mx = r < R ? rmax[r] : 0.f;
+      if (BX != BX_NONE) {
+        const int64_t q = voff + (r < R ? r : 0);
+        const float mx = rv.m[q];
+        const float inv = BX >= BX_AEA ? rv.inv[q] : 0.f;
+        const float cl = BX >= BX_AEA ? rv.clamp[q] : 0.f;
+        const float m2 = BX == BX_AEAR ? rv.m2[q] : 0.f;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (r < R && k + e < K) ? expf(v[e] - mx) : 0.f;
+        for (int e = 0; e < 4; ++e)
+          v[e] = (r < R && k + e < K) ? bx_apply<BX>(v[e], mx, inv, cl, m2, rv.scale) : 0.f;
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) reg[4 * p + e] = v[e];
@@ -106,7 +145,7 @@ __device__ __forceinline__ void g_store(float* __restrict__ Xs, const float (&re
   }
 }
 
-template <int ALAY, int BLAY, bool EXPB, bool VECA, bool VECB>
+template <int ALAY, int BLAY, int BX, bool VECA, bool VECB>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   constexpr int LD = 128 + kGPad;
   __shared__ float As[kGBK * LD];
@@ -116,8 +155,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   const float* A = g.A + b * g.sA;
   const float* B = g.B + b * g.sB;
   float* C = g.C + b * g.sC;
-  const float* rmax = EXPB ? g.rowmax + b * g.sV : nullptr;
-  const float* cscale = g.colscale ? g.colscale + b * g.sV : nullptr;
+  const int64_t voff = (int64_t)b * g.sV;
+  const float* cscale = g.colscale ? g.colscale + voff : nullptr;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -133,15 +172,15 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
 
   float ra[16], rb[16];
   const int ktiles = (g.K + kGBK - 1) / kGBK;
-  g_load<ALAY, false, VECA>(ra, A, g.lda, m0, 0, g.M, g.K, nullptr, tid);
-  g_load<BLAY, EXPB, VECB>(rb, B, g.ldb, n0, 0, g.N, g.K, rmax, tid);
+  g_load<ALAY, BX_NONE, VECA>(ra, A, g.lda, m0, 0, g.M, g.K, g.rv, 0, tid);
+  g_load<BLAY, BX, VECB>(rb, B, g.ldb, n0, 0, g.N, g.K, g.rv, voff, tid);
   for (int kt = 0; kt < ktiles; ++kt) {
     g_store<ALAY>(As, ra, tid);
     g_store<BLAY>(Bs, rb, tid);
     __syncthreads();
     if (kt + 1 < ktiles) {
-      g_load<ALAY, false, VECA>(ra, A, g.lda, m0, (kt + 1) * kGBK, g.M, g.K, nullptr, tid);
-      g_load<BLAY, EXPB, VECB>(rb, B, g.ldb, n0, (kt + 1) * kGBK, g.N, g.K, rmax, tid);
+      g_load<ALAY, BX_NONE, VECA>(ra, A, g.lda, m0, (kt + 1) * kGBK, g.M, g.K, g.rv, 0, tid);
+      g_load<BLAY, BX, VECB>(rb, B, g.ldb, n0, (kt + 1) * kGBK, g.N, g.K, g.rv, voff, tid);
     }
 #pragma unroll
     for (int kk = 0; kk < kGBK / 2; ++kk) {
@@ -164,12 +203,16 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     const int n = n0 + wn * 64 + nt * 32 + j;
     if (n >= g.N) continue;
     const float cs = cscale ? cscale[n] : 1.f;
+    const float cb = g.colbias ? g.colbias[n] : 0.f;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < g.M) C[(int64_t)m * g.ldc + n] = acc[mt][nt][r] * cs;
+        float v = acc[mt][nt][r] * cs;
+        if (g.colbias) v += cb;
+        if (g.act == 1) v = v > 0.f ? v : 0.2f * v;
+        if (m < g.M) C[(int64_t)m * g.ldc + n] = v;
       }
   }
 }
@@ -209,7 +252,7 @@ __global__ __launch_bounds__(256) void rowstats_kernel(const float* __restrict__
   }
 }
 
-template <int ALAY, int BLAY, bool EXPB>
+template <int ALAY, int BLAY, int BX>
 static void launch_gemm(const GemmArgs& g, int batch, hipStream_t st) {
   dim3 grid((g.N + kGBN - 1) / kGBN, (g.M + kGBM - 1) / kGBM, batch);
   auto aligned = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
@@ -219,9 +262,160 @@ static void launch_gemm(const GemmArgs& g, int batch, hipStream_t st) {
   const bool vb = aligned(g.B) && (g.ldb % 4 == 0) && (g.sB % 4 == 0) &&
                   ((BLAY == LAY_KR) ? (g.N % 4 == 0) : (g.K % 4 == 0));
   if (va && vb)
-    gemm_f32_kernel<ALAY, BLAY, EXPB, true, true><<<grid, 256, 0, st>>>(g);
+    gemm_f32_kernel<ALAY, BLAY, BX, true, true><<<grid, 256, 0, st>>>(g);
   else
-    gemm_f32_kernel<ALAY, BLAY, EXPB, false, false><<<grid, 256, 0, st>>>(g);
+    gemm_f32_kernel<ALAY, BLAY, BX, false, false><<<grid, 256, 0, st>>>(g);
+}
+
+
+// ---- AdaptiveSANet (sanet.py:12-18, 26-71, 100-138) -----------------------------------
+// functional.normalize(x, dim=1): x / max(||x||_2 over channels, 1e-12), per position.
+// One thread per (b, position): the channel loop strides by HW, so a wave reads 64
+// consecutive positions of one channel row per step (coalesced).
+__global__ __launch_bounds__(256) void colnorm_kernel(const float* __restrict__ x,
+                                                      float* __restrict__ out, int B, int C,
+                                                      int HW) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)B * HW) return;
+  const int64_t b = idx / HW, i = idx - b * HW;
+  const float* xp = x + b * C * (int64_t)HW + i;
+  double ss = 0.0;
+  for (int c = 0; c < C; ++c) {
+    const double v = xp[(int64_t)c * HW];
+    ss += v * v;
+  }
+  const float nrm = fmaxf((float)sqrt(ss), 1e-12f);
+  float* op = out + b * C * (int64_t)HW + i;
+  for (int c = 0; c < C; ++c) op[(int64_t)c * HW] = xp[(int64_t)c * HW] / nrm;
+}
+
+// f_psi's last Linear(hid -> 1) + head: AEA  clamp = sigmoid(t) * interval + from
+// (sanet.py:45); AEALRelu  clamp = (tanh(t) + 1) / 2 (sanet.py:66). One wave per row.
+__global__ __launch_bounds__(256) void clamp_head_kernel(const float* __restrict__ Z,
+                                                         const float* __restrict__ w2,
+                                                         const float* __restrict__ b2,
+                                                         float* __restrict__ clamp,
+                                                         int64_t rows, int hid, int mode,
+                                                         float from, float interval) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* z = Z + row * hid;
+  float acc = 0.f;
+  for (int n = lane; n < hid; n += 64) acc = fmaf(z[n], w2[n], acc);
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    const float t = acc + b2[0];
+    clamp[row] = mode == 0 ? (1.f / (1.f + expf(-t))) * interval + from : (tanhf(t) + 1.f) / 2.f;
+  }
+}
+
+// AEALRelu second softmax: per row, m2 = max_j relu(P_ij - c_i), inv2 = 1 / sum_j
+// exp(relu(P_ij - c_i) - m2), with P_ij = exp(S_ij - m_i) inv_i formed exactly as the
+// GEMM staging forms it. One wave per row.
+__global__ __launch_bounds__(256) void rowstats_relu_kernel(
+    const float* __restrict__ S, const float* __restrict__ rmax, const float* __restrict__ rinv,
+    const float* __restrict__ clamp, float* __restrict__ m2, float* __restrict__ inv2,
+    int64_t rows, int L) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* s = S + row * L;
+  const float m = rmax[row], inv = rinv[row], c = clamp[row];
+  float mx = -INFINITY;
+  for (int i = lane; i < L; i += 64) mx = fmaxf(mx, fmaxf(expf(s[i] - m) * inv - c, 0.f));
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int i = lane; i < L; i += 64) sum += expf(fmaxf(expf(s[i] - m) * inv - c, 0.f) - mx);
+  sum = wave_sum(sum);
+  if (lane == 0) {
+    m2[row] = mx;
+    inv2[row] = 1.f / sum;
+  }
+}
+
+// Materialise P = softmax(S) (claim_before) and/or the clamped attention (claim_after)
+// for callers that keep them (AdaptiveSANet.claim_before / claim_after).
+__global__ __launch_bounds__(256) void claim_maps_kernel(
+    const float* __restrict__ S, RowVec rv, const float* __restrict__ inv2, int mode,
+    float* __restrict__ before, float* __restrict__ after, int64_t rows, int L) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows * L) return;
+  const int64_t r = idx / L;
+  const float v = S[idx];
+  const float p = expf(v - rv.m[r]) * rv.inv[r];
+  if (before) before[idx] = p;
+  if (after) {
+    after[idx] = mode == 0
+                     ? bx_apply<BX_AEA>(v, rv.m[r], rv.inv[r], rv.clamp[r], 0.f, rv.scale)
+                     : bx_apply<BX_AEAR>(v, rv.m[r], rv.inv[r], rv.clamp[r], rv.m2[r], 0.f) *
+                           inv2[r];
+  }
+}
+
+// Elementwise AEA transform of a given attention matrix fx (AEAModule.forward's second
+// half, for the function-level module API): out = f(fx, clamp_row).
+__global__ __launch_bounds__(256) void aea_apply_kernel(const float* __restrict__ fx,
+                                                        const float* __restrict__ clamp,
+                                                        const float* __restrict__ m2,
+                                                        const float* __restrict__ inv2,
+                                                        float* __restrict__ out, int64_t rows,
+                                                        int L, int mode, float scale) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows * L) return;
+  const int64_t r = idx / L;
+  const float d = fx[idx] - clamp[r];
+  out[idx] = mode == 0 ? 1.f / (1.f + expf(-(scale * d))) : expf(fmaxf(d, 0.f) - m2[r]) * inv2[r];
+}
+
+// Row max / inverse sum of exp(relu(fx - c) - max) for aea_apply_kernel's mode 1.
+__global__ __launch_bounds__(256) void rowstats_relu_plain_kernel(
+    const float* __restrict__ fx, const float* __restrict__ clamp, float* __restrict__ m2,
+    float* __restrict__ inv2, int64_t rows, int L) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* s = fx + row * L;
+  const float c = clamp[row];
+  float mx = -INFINITY;
+  for (int i = lane; i < L; i += 64) mx = fmaxf(mx, fmaxf(s[i] - c, 0.f));
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int i = lane; i < L; i += 64) sum += expf(fmaxf(s[i] - c, 0.f) - mx);
+  sum = wave_sum(sum);
+  if (lane == 0) {
+    m2[row] = mx;
+    inv2[row] = 1.f / sum;
+  }
+}
+
+// clamp[b, i] = head(LeakyReLU(A[b, i, :] W1^T + b1)) (AEAModule.f_psi over affinity rows)
+static int clamp_values(const float* A, const float* w1, const float* b1, const float* w2,
+                        const float* b2, int hid, int mode, float from, float interval,
+                        float* Z, float* clamp, int B, int HW, hipStream_t st) {
+  // Z[b][i][n] = sum_j A[b][i][j] W1[n][j] + b1[n]: M = HW (i), N = hid (n), K = HW (j)
+  GemmArgs gz{A, w1, Z, {}, nullptr, b1, 1, HW, hid, HW, HW, HW, hid,
+              (int64_t)HW * HW, 0, (int64_t)HW * hid, 0};
+  launch_gemm<LAY_RK, LAY_RK, BX_NONE>(gz, B, st);
+  if (int e = launch_status("gemm_f32_kernel(Z=A W1^T)")) return e;
+  const int64_t rows = (int64_t)B * HW;
+  clamp_head_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Z, w2, b2, clamp, rows, hid,
+                                                               mode, from, interval);
+  return launch_status("clamp_head_kernel");
+}
+
+static int affinity(const float* c, const float* s, float* out, float* cn, float* sn, int B,
+                    int C, int HW, hipStream_t st) {
+  const int64_t pos = (int64_t)B * HW;
+  colnorm_kernel<<<(unsigned)((pos + 255) / 256), 256, 0, st>>>(c, cn, B, C, HW);
+  colnorm_kernel<<<(unsigned)((pos + 255) / 256), 256, 0, st>>>(s, sn, B, C, HW);
+  if (int e = launch_status("colnorm_kernel")) return e;
+  const int64_t fhw = (int64_t)C * HW;
+  // A[b][i][j] = sum_c cn[b][c][i] sn[b][c][j]
+  GemmArgs ga{cn, sn, out, {}, nullptr, nullptr, 0, HW, HW, C, HW, HW, HW,
+              fhw, fhw, (int64_t)HW * HW, 0};
+  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(ga, B, st);
+  return launch_status("gemm_f32_kernel(A=cn^T sn)");
 }
 
 }  // namespace rpst
@@ -250,14 +444,153 @@ extern "C" int rpst_sanet_attention(const float* F, const float* G, const float*
   float* rinv = rmax + (size_t)B * HW;
   const int64_t fhw = (int64_t)C * HW;
   // S[b][i][j] = sum_c F[b][c][i] G[b][c][j]
-  GemmArgs g1{F, G, S, nullptr, nullptr, HW, HW, C, HW, HW, HW, fhw, fhw, (int64_t)HW * HW, 0};
-  launch_gemm<LAY_KR, LAY_KR, false>(g1, B, st);
+  GemmArgs g1{F, G, S, {}, nullptr, nullptr, 0, HW, HW, C, HW, HW, HW,
+               fhw, fhw, (int64_t)HW * HW, 0};
+  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(g1, B, st);
   if (int e = launch_status("gemm_f32_kernel(S=F^T G)")) return e;
   const int64_t rows = (int64_t)B * HW;
   rowstats_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rmax, rinv, rows, HW);
   if (int e = launch_status("rowstats_kernel")) return e;
   // O[b][c][i] = (1/l_i) sum_j H[b][c][j] exp(S[b][i][j] - m_i)
-  GemmArgs g2{H, S, O, rmax, rinv, C, HW, HW, HW, HW, HW, fhw, (int64_t)HW * HW, fhw, HW};
-  launch_gemm<LAY_RK, LAY_RK, true>(g2, B, st);
+  GemmArgs g2{H, S, O, {rmax, nullptr, nullptr, nullptr, 0.f}, rinv, nullptr, 0,
+               C, HW, HW, HW, HW, HW, fhw, (int64_t)HW * HW, fhw, HW};
+  launch_gemm<LAY_RK, LAY_RK, BX_EXP>(g2, B, st);
   return launch_status("gemm_f32_kernel(O=H P^T)");
+}
+
+extern "C" size_t rpst_cosine_affinity_workspace_size(int B, int C, int HW) {
+  if (B <= 0 || C <= 0 || HW <= 0) return 0;
+  return sizeof(float) * 2 * (size_t)B * C * HW;
+}
+
+extern "C" int rpst_cosine_affinity(const float* content, const float* style, float* out,
+                                    int B, int C, int HW, void* workspace,
+                                    size_t workspace_bytes, rpst_stream_t stream) {
+  RPST_REQUIRE(content && style && out, "cosine_affinity: null pointer");
+  RPST_REQUIRE(B > 0 && C > 0 && HW > 0 && B <= 65535, "cosine_affinity: bad shape");
+  if (!workspace || workspace_bytes < rpst_cosine_affinity_workspace_size(B, C, HW)) {
+    set_error("cosine_affinity: workspace too small");
+    return RPST_EWORKSPACE;
+  }
+  float* cn = static_cast<float*>(workspace);
+  return affinity(content, style, out, cn, cn + (size_t)B * C * HW, B, C, HW,
+                  as_stream(stream));
+}
+
+extern "C" size_t rpst_aea_clamp_workspace_size(int B, int HW, int hidden) {
+  if (B <= 0 || HW <= 0 || hidden <= 0) return 0;
+  return sizeof(float) * ((size_t)B * HW * hidden + 2 * (size_t)B * HW);
+}
+
+extern "C" int rpst_aea_clamp(const float* x, const float* fx, const float* w1,
+                              const float* b1, const float* w2, const float* b2, int hidden,
+                              int mode, float scale, float from, float interval, float* out_fx,
+                              float* out_clamp, int B, int HW, void* workspace,
+                              size_t workspace_bytes, rpst_stream_t stream) {
+  RPST_REQUIRE(x && fx && w1 && b1 && w2 && b2 && out_fx && out_clamp, "aea_clamp: null pointer");
+  RPST_REQUIRE(B > 0 && HW > 0 && hidden > 0 && B <= 65535, "aea_clamp: bad shape");
+  RPST_REQUIRE(mode == 0 || mode == 1, "aea_clamp: mode must be 0 (aea) or 1 (relu)");
+  if (!workspace || workspace_bytes < rpst_aea_clamp_workspace_size(B, HW, hidden)) {
+    set_error("aea_clamp: workspace too small");
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  float* Z = static_cast<float*>(workspace);
+  float* m2 = Z + (size_t)B * HW * hidden;
+  float* inv2 = m2 + (size_t)B * HW;
+  if (int e = clamp_values(x, w1, b1, w2, b2, hidden, mode, from, interval, Z, out_clamp, B,
+                           HW, st))
+    return e;
+  const int64_t rows = (int64_t)B * HW;
+  if (mode == 1) {
+    rowstats_relu_plain_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(fx, out_clamp, m2,
+                                                                           inv2, rows, HW);
+    if (int e = launch_status("rowstats_relu_plain_kernel")) return e;
+  }
+  const int64_t n = rows * HW;
+  aea_apply_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(fx, out_clamp, m2, inv2, out_fx,
+                                                                rows, HW, mode, scale);
+  return launch_status("aea_apply_kernel");
+}
+
+extern "C" size_t rpst_adaptive_attention_workspace_size(int B, int C, int HW, int hidden) {
+  if (B <= 0 || C <= 0 || HW <= 0 || hidden <= 0) return 0;
+  return sizeof(float) * ((size_t)B * HW * HW + (size_t)B * HW * hidden +
+                          2 * (size_t)B * C * HW + 5 * (size_t)B * HW);
+}
+
+extern "C" int rpst_adaptive_attention(const float* F, const float* G, const float* H,
+                                       const float* content, const float* style,
+                                       const float* w1, const float* b1, const float* w2,
+                                       const float* b2, int hidden, int mode, float scale,
+                                       float from, float interval, float* O, float* claim_value,
+                                       float* claim_before, float* claim_after, int B, int C,
+                                       int HW, void* workspace, size_t workspace_bytes,
+                                       rpst_stream_t stream) {
+  RPST_REQUIRE(F && G && H && content && style && w1 && b1 && w2 && b2 && O,
+               "adaptive_attention: null pointer");
+  RPST_REQUIRE(B > 0 && C > 0 && HW > 0 && hidden > 0 && B <= 65535,
+               "adaptive_attention: bad shape B=%d C=%d HW=%d hidden=%d", B, C, HW, hidden);
+  RPST_REQUIRE(mode == 0 || mode == 1, "adaptive_attention: mode must be 0 (aea) or 1 (relu)");
+  if (!workspace ||
+      workspace_bytes < rpst_adaptive_attention_workspace_size(B, C, HW, hidden)) {
+    set_error("adaptive_attention: workspace %zu < %zu bytes", workspace_bytes,
+              rpst_adaptive_attention_workspace_size(B, C, HW, hidden));
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  float* S = static_cast<float*>(workspace);  // affinity first, then the logits
+  float* Z = S + (size_t)B * HW * HW;
+  float* cn = Z + (size_t)B * HW * hidden;
+  float* sn = cn + (size_t)B * C * HW;
+  float* rmax = sn + (size_t)B * C * HW;
+  float* rinv = rmax + (size_t)B * HW;
+  float* clamp = rinv + (size_t)B * HW;
+  float* m2 = clamp + (size_t)B * HW;
+  float* inv2 = m2 + (size_t)B * HW;
+  // 1. clamp values from the cosine affinity of the raw features (sanet.py:110, 45 / 66)
+  if (int e = affinity(content, style, S, cn, sn, B, C, HW, st)) return e;
+  if (int e = clamp_values(S, w1, b1, w2, b2, hidden, mode, from, interval, Z, clamp, B, HW,
+                           st))
+    return e;
+  // 2. logits S = F^T G and softmax row statistics (sanet.py:114-117)
+  const int64_t fhw = (int64_t)C * HW;
+  GemmArgs g1{F, G, S, {}, nullptr, nullptr, 0, HW, HW, C, HW, HW, HW,
+              fhw, fhw, (int64_t)HW * HW, 0};
+  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(g1, B, st);
+  if (int e = launch_status("gemm_f32_kernel(S=F^T G)")) return e;
+  const int64_t rows = (int64_t)B * HW;
+  rowstats_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rmax, rinv, rows, HW);
+  if (int e = launch_status("rowstats_kernel")) return e;
+  RowVec rv{rmax, rinv, clamp, m2, scale};
+  if (mode == 1) {
+    rowstats_relu_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rmax, rinv, clamp, m2,
+                                                                     inv2, rows, HW);
+    if (int e = launch_status("rowstats_relu_kernel")) return e;
+  }
+  if (claim_before || claim_after) {
+    const int64_t n = rows * HW;
+    claim_maps_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(S, rv, inv2, mode,
+                                                                   claim_before, claim_after,
+                                                                   rows, HW);
+    if (int e = launch_status("claim_maps_kernel")) return e;
+  }
+  if (claim_value) {
+    if (hipMemcpyAsync(claim_value, clamp, sizeof(float) * rows, hipMemcpyDeviceToDevice, st) !=
+        hipSuccess) {
+      set_error("adaptive_attention: claim_value copy failed");
+      return RPST_EHIP;
+    }
+  }
+  // 3. O[b][c][i] = sum_j H[b][c][j] Q[b][i][j], Q formed while S is staged (sanet.py:122-124)
+  if (mode == 0) {
+    GemmArgs g2{H, S, O, rv, nullptr, nullptr, 0, C, HW, HW, HW, HW, HW,
+                fhw, (int64_t)HW * HW, fhw, HW};
+    launch_gemm<LAY_RK, LAY_RK, BX_AEA>(g2, B, st);
+  } else {
+    GemmArgs g2{H, S, O, rv, inv2, nullptr, 0, C, HW, HW, HW, HW, HW,
+                fhw, (int64_t)HW * HW, fhw, HW};
+    launch_gemm<LAY_RK, LAY_RK, BX_AEAR>(g2, B, st);
+  }
+  return launch_status("gemm_f32_kernel(O=H Q^T)");
 }

@@ -1,6 +1,7 @@
 """Drop-in replacement for the reference `network` package (network/__init__.py:1-6),
 restricted to the hot path: AdaIN-RP, WCT-RP and SANet inference on MI355X kernels, plus
-SURVEY §8(f)'s MultiScaleAdaINRPNet (constant / deeper stacks) and SourceNet.
+SURVEY §8(f)'s MultiScaleAdaINRPNet (constant / deeper stacks), SourceNet and the
+AdaptiveSANet / AdaptiveSAModel (AEA clamp) family.
 
     sys.path.insert(0, "<repo>/rp-style-transfer_amd")
     import network as net          # instead of the reference's network/
@@ -14,7 +15,9 @@ from .base import (BaseNet, Conv2dBlock, SourceNet, StackType, adaptive_instance
                    decoder, rp_constant_conv_blocks, rp_deeper_conv_blocks,
                    rp_shallower_conv_blocks, vgg)
 from .adain_rp import AdaIN, AdaINRPNet, MultiScaleAdaINRPNet
-from .sanet import SAModel, SANet, Transform, mean_variance_norm
+from .sanet import (AdaptiveSAModel, AdaptiveSANet, AdaptiveTransform, AEALReluModule,
+                    AEAModule, SAModel, SANet, Transform, cal_affinity_matrix,
+                    mean_variance_norm)
 from .wct_rp import WCTRPNet, matrix_inv_sqrt, matrix_sqrt
 
 __all__ = ["BaseNet", "Conv2dBlock", "SourceNet", "StackType", "rp_constant_conv_blocks",
@@ -22,4 +25,6 @@ __all__ = ["BaseNet", "Conv2dBlock", "SourceNet", "StackType", "rp_constant_conv
            "adaptive_instance_normalization", "build_decrease_depth_rp_blocks",
            "build_increase_depth_rp_blocks", "calc_mean_std", "decoder", "vgg", "AdaIN",
            "AdaINRPNet", "SAModel", "SANet", "Transform", "mean_variance_norm", "WCTRPNet",
+           "AdaptiveSAModel", "AdaptiveSANet", "AdaptiveTransform", "AEAModule",
+           "AEALReluModule", "cal_affinity_matrix",
            "matrix_inv_sqrt", "matrix_sqrt"]

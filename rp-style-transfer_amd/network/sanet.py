@@ -7,6 +7,10 @@
                          B operand is staged, then out_conv with the residual fused
   Transform.forward   sanet.py:148-149 -> merge_conv reads a + up2(b) in its loader
   SAModel.test        sanet.py:238-246 -> VGG relu1_1..5_1 over [style; content] once
+  AdaptiveSANet       sanet.py:100-138: cosine affinity GEMM, the
+                      AEA clamp MLP as a GEMM with a LeakyReLU epilogue + head kernel, and
+                      the clamped attention formed while S is staged into the last GEMM
+  AdaptiveSAModel     sanet.py:278-345 (test() without the matplotlib/seaborn claim plots)
 No 1/sqrt(d) scaling, exactly as the reference (sanet.py:90-91).
 """
 from __future__ import annotations
@@ -17,12 +21,58 @@ import torch.nn as nn
 from rpst import ops
 from rpst.plan import KernelSequential, packed_weight
 
-from .base import _make_decoder, calc_mean_std, mse
+from .base import BaseNet, _make_decoder, calc_mean_std, mse
 
 
 def mean_variance_norm(feat):
     """(x - mean) / std with calc_mean_std statistics (sanet.py:20-24)."""
     return ops.mean_variance_norm(feat)
+
+
+def cal_affinity_matrix(content_feat, style_feat):
+    """normalize(c)^T normalize(s) over channels, (B, HW, HW) (sanet.py:12-18)."""
+    assert content_feat.size() == style_feat.size()
+    return ops.cosine_affinity(content_feat, style_feat)
+
+
+class AEAModule(nn.Module):
+    """Adaptive clamp (sanet.py:26-47): clamp = sigmoid(f_psi(x_i)) * interval + from per
+    query row, clamp_fx = sigmoid(scale * (f_x - clamp))."""
+    mode = ops.AEA_MODES["aea"]
+
+    def __init__(self, inplanes, scale_value=50, from_value=0.4, value_interval=0.5):
+        super().__init__()
+        self.inplanes = inplanes
+        self.scale_value = scale_value
+        self.from_value = from_value
+        self.value_interval = value_interval
+        self.f_psi = nn.Sequential(
+            nn.Linear(self.inplanes, self.inplanes // 16),
+            nn.LeakyReLU(0.2, inplace=True),
+            nn.Linear(self.inplanes // 16, 1),
+            self._head())
+
+    @staticmethod
+    def _head():
+        return nn.Sigmoid()
+
+    def forward(self, x, f_x):
+        return ops.aea_clamp(x, f_x, self.f_psi, self.mode, float(self.scale_value),
+                             float(self.from_value), float(self.value_interval))
+
+
+class AEALReluModule(AEAModule):
+    """sanet.py:50-69: clamp = (tanh(f_psi(x_i)) + 1) / 2, clamp_fx =
+    softmax(relu(f_x - clamp), dim=-1)."""
+    mode = ops.AEA_MODES["relu"]
+
+    def __init__(self, inplanes, scale_value=50, from_value=0.4, value_interval=0.5):
+        super().__init__(inplanes, scale_value, from_value, value_interval)
+        self.clamp_sig = nn.Sequential(nn.ReLU(inplace=True), nn.Softmax(dim=-1))
+
+    @staticmethod
+    def _head():
+        return nn.Tanh()
 
 
 def _conv1x1(conv: nn.Conv2d, x, residual=None):
@@ -63,6 +113,56 @@ class Transform(nn.Module):
         # merge_conv(reflect_pad(a + upsample2(b))) as ONE conv launch
         return ops.conv2d(a, packed_weight(c), c.bias, c.out_channels, 3, pad=ops.PAD_REFLECT,
                           in_op=ops.IN_ADD_UPSAMPLE2, aux=b)
+
+
+class AdaptiveSANet(nn.Module):
+    """SANet with the AEA clamp on its attention (sanet.py:100-138). The attention maps are
+    not materialised; claim_value (B, HW, 1) is always kept, claim_before / claim_after
+    (B, HW, HW) only when keep_claims is set (the reference keeps them for its plots)."""
+
+    def __init__(self, in_planes, spatial_dims, ada_module='aea'):
+        super().__init__()
+        self.f = nn.Conv2d(in_planes, in_planes, (1, 1))
+        self.g = nn.Conv2d(in_planes, in_planes, (1, 1))
+        self.h = nn.Conv2d(in_planes, in_planes, (1, 1))
+        self.sm = nn.Softmax(dim=-1)
+        self.out_conv = nn.Conv2d(in_planes, in_planes, (1, 1))
+        self.attention_layer = (AEAModule(spatial_dims) if ada_module == 'aea'
+                                else AEALReluModule(spatial_dims))
+        self.claim_value = 0
+        self.claim_before = 0
+        self.claim_after = 0
+        self.claim_after_sm = 0
+        self.keep_claims = False
+
+    def forward(self, content, style):
+        F = _conv1x1(self.f, mean_variance_norm(content))
+        G = _conv1x1(self.g, mean_variance_norm(style))
+        H = _conv1x1(self.h, style)
+        al = self.attention_layer
+        O, claim, before, after = ops.adaptive_attention(
+            F, G, H, content, style, al.f_psi, al.mode, float(al.scale_value),
+            float(al.from_value), float(al.value_interval), keep_claims=self.keep_claims)
+        if self.keep_claims:
+            self.claim_before, self.claim_after = before, after
+        self.claim_value = claim
+        return _conv1x1(self.out_conv, O, residual=content)
+
+
+class AdaptiveTransform(nn.Module):
+    """sanet.py:151-160: AdaptiveSANet at relu4_1 and relu5_1, merged by one conv launch."""
+
+    def __init__(self, in_planes, relu4_1_dims, relu5_1_dims, ada_module='aea'):
+        super().__init__()
+        self.sanet4_1 = AdaptiveSANet(in_planes=in_planes, spatial_dims=relu4_1_dims,
+                                      ada_module=ada_module)
+        self.sanet5_1 = AdaptiveSANet(in_planes=in_planes, spatial_dims=relu5_1_dims,
+                                      ada_module=ada_module)
+        self.upsample5_1 = nn.Upsample(scale_factor=2, mode='nearest')
+        self.merge_conv_pad = nn.ReflectionPad2d((1, 1, 1, 1))
+        self.merge_conv = nn.Conv2d(in_planes, in_planes, (3, 3))
+
+    forward = Transform.forward
 
 
 decoder = _make_decoder()
@@ -147,3 +247,60 @@ class SAModel(nn.Module):
                       + self.config['l_identity2_weight'] * l_identity2)
         return {'style_loss': loss_s, 'content_loss': loss_c, 'l_identity1_loss': l_identity1,
                 'l_identity2_loss': l_identity2, 'total_loss': total_loss}, total_loss
+
+
+class AdaptiveSAModel(BaseNet):
+    """sanet.py:278-345. test() returns the stylised batch; the reference's claim-map
+    heatmaps (matplotlib/seaborn files under config['output']) are visualisation and are
+    not drawn (set transform.sanet*_1.keep_claims to keep the maps for plotting)."""
+
+    def __init__(self, config, encoder, start_iter, img_size):
+        super().__init__()
+        self.config = config
+        enc_layers = list(encoder.children())[:44]
+        self.enc_1 = KernelSequential(*enc_layers[:4])
+        self.enc_2 = KernelSequential(*enc_layers[4:11])
+        self.enc_3 = KernelSequential(*enc_layers[11:18])
+        self.enc_4 = KernelSequential(*enc_layers[18:31])
+        self.enc_5 = KernelSequential(*enc_layers[31:44])
+        self.relu4_1_dims = (img_size // 2 ** 3) ** 2
+        self.relu5_1_dims = (img_size // 2 ** 4) ** 2
+        self.transform = AdaptiveTransform(in_planes=512, relu4_1_dims=self.relu4_1_dims,
+                                           relu5_1_dims=self.relu5_1_dims,
+                                           ada_module=self.config['ada_module'])
+        self.decoder = decoder
+        if start_iter > 0:
+            self.transform.load_state_dict(torch.load(
+                'transformer_iter_' + str(start_iter) + '.pth', weights_only=True))
+            self.decoder.load_state_dict(torch.load(
+                'decoder_iter_' + str(start_iter) + '.pth', weights_only=True))
+        self.mse_loss = nn.MSELoss()
+        for name in ['enc_1', 'enc_2', 'enc_3', 'enc_4', 'enc_5']:
+            for param in getattr(self, name).parameters():
+                param.requires_grad = False
+
+    encode_with_intermediate = SAModel.encode_with_intermediate
+    calc_content_loss = SAModel.calc_content_loss
+    calc_style_loss = SAModel.calc_style_loss
+
+    def save(self, save_path, iterations=0):
+        torch.save({'decoder': self.decoder.state_dict(),
+                    'transform': self.transform.state_dict()}, save_path)
+
+    def fuse(self, content_feats, style_feats):
+        return self.transform(content_feats[3], style_feats[3], content_feats[4], style_feats[4])
+
+    def test(self, content, style, iterations=0, bid=0, c_mask_path=None, s_mask_path=None):
+        self.eval()
+        with torch.no_grad():
+            n = content.shape[0]
+            feats = self.encode_with_intermediate(torch.cat([style, content], dim=0))
+            style_feats = [f[:n] for f in feats]
+            content_feats = [f[n:] for f in feats]
+            stylized = self.decoder(self.fuse(content_feats, style_feats))
+            self.train()
+            return stylized
+
+    def forward(self, content, style):
+        """Loss dict of sanet.py:347-382 (inference kernels: call under no_grad)."""
+        return SAModel.forward(self, content, style)

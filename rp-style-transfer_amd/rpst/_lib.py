@@ -43,6 +43,14 @@ SIGNATURES = {
     "rpst_upsample_nearest2x": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "rpst_sanet_attention_workspace_size": (_SZ, [_I, _I]),
     "rpst_sanet_attention": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
+    "rpst_cosine_affinity_workspace_size": (_SZ, [_I, _I, _I]),
+    "rpst_cosine_affinity": (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
+    "rpst_aea_clamp_workspace_size": (_SZ, [_I, _I, _I]),
+    "rpst_aea_clamp": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _P, _P, _I, _I, _P, _SZ,
+                            _P]),
+    "rpst_adaptive_attention_workspace_size": (_SZ, [_I, _I, _I, _I]),
+    "rpst_adaptive_attention": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _P,
+                                     _P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
     "rpst_matrix_power_workspace_size": (_SZ, [_I, _I]),
     "rpst_matrix_power_psd_f64": (_I, [_P, _P, _I, _I, _I, _P, _SZ, _P]),
     "rpst_wct_workspace_size": (_SZ, [_I, _I, _I64]),

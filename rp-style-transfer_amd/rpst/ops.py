@@ -309,6 +309,91 @@ def sanet_attention(F: torch.Tensor, G: torch.Tensor, H: torch.Tensor) -> torch.
     return out
 
 
+def cosine_affinity(content: torch.Tensor, style: torch.Tensor) -> torch.Tensor:
+    """cal_affinity_matrix (sanet.py:12-18): normalize(c)^T normalize(s), (B, HW, HW)."""
+    assert content.size() == style.size() and content.dim() == 4
+    _check(content, style)
+    content, style = _c(content), _c(style)
+    B, C, h, w = content.shape
+    hw = h * w
+    out = torch.empty((B, hw, hw), device=content.device, dtype=torch.float32)
+    nbytes = _lib.load().rpst_cosine_affinity_workspace_size(B, C, hw)
+    ws = torch.empty(nbytes, device=content.device, dtype=torch.uint8)
+    _lib.call("rpst_cosine_affinity", content.data_ptr(), style.data_ptr(), out.data_ptr(), B, C,
+              hw, ws.data_ptr(), nbytes, _stream(content))
+    return out
+
+
+AEA_MODES = {"aea": 0, "relu": 1}
+
+
+def _mlp_params(f_psi):
+    """(W1, b1, w2, b2, hidden) of f_psi = Sequential(Linear, LeakyReLU, Linear, head)."""
+    l1, l2 = f_psi[0], f_psi[2]
+    ps = [l1.weight, l1.bias, l2.weight, l2.bias]
+    _check(*ps)
+    return [_c(p.detach()) for p in ps] + [l1.out_features]
+
+
+def aea_clamp(x: torch.Tensor, f_x: torch.Tensor, f_psi, mode: int, scale: float,
+              from_value: float, interval: float):
+    """AEAModule / AEALReluModule.forward (sanet.py:42-47 / 63-69):
+    returns (clamp_fx (B, HW, HW), clamp_value (B, HW, 1))."""
+    assert x.dim() == 3 and x.shape == f_x.shape and x.shape[1] == x.shape[2]
+    _check(x, f_x)
+    x, f_x = _c(x), _c(f_x)
+    B, hw = x.shape[0], x.shape[1]
+    w1, b1, w2, b2, hid = _mlp_params(f_psi)
+    assert w1.shape[1] == hw, "f_psi input width must equal HW (spatial_dims)"
+    out = torch.empty_like(f_x)
+    clamp = torch.empty((B, hw, 1), device=x.device, dtype=torch.float32)
+    nbytes = _lib.load().rpst_aea_clamp_workspace_size(B, hw, hid)
+    ws = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
+    _lib.call("rpst_aea_clamp", x.data_ptr(), f_x.data_ptr(), w1.data_ptr(), b1.data_ptr(),
+              w2.data_ptr(), b2.data_ptr(), hid, mode, scale, from_value, interval,
+              out.data_ptr(), clamp.data_ptr(), B, hw, ws.data_ptr(), nbytes, _stream(x))
+    return out, clamp
+
+
+def adaptive_attention(F: torch.Tensor, G: torch.Tensor, H: torch.Tensor,
+                       content: torch.Tensor, style: torch.Tensor, f_psi, mode: int,
+                       scale: float, from_value: float, interval: float,
+                       keep_claims: bool = False):
+    """AdaptiveSANet core (sanet.py:106-124): O = H AEA(affinity(c, s), softmax(F^T G))^T.
+    Returns (O, claim_value (B, HW, 1), claim_before, claim_after); the (B, HW, HW) claim
+    maps are materialised only when keep_claims (else None)."""
+    assert F.dim() == 4 and F.shape == G.shape == H.shape == content.shape == style.shape
+    _check(F, G, H, content, style)
+    F, G, H, content, style = _c(F), _c(G), _c(H), _c(content), _c(style)
+    B, C, h, w = F.shape
+    hw = h * w
+    w1, b1, w2, b2, hid = _mlp_params(f_psi)
+    assert w1.shape[1] == hw, "f_psi input width must equal HW (spatial_dims)"
+    out = torch.empty_like(F)
+    claim = torch.empty((B, hw, 1), device=F.device, dtype=torch.float32)
+    before = after = None
+    if keep_claims:
+        before = torch.empty((B, hw, hw), device=F.device, dtype=torch.float32)
+        after = torch.empty_like(before)
+    lib = _lib.load()
+    per_img = lib.rpst_adaptive_attention_workspace_size(1, C, hw, hid)
+    chunk = max(1, min(B, SANET_WS_CAP // max(per_img, 1)))
+    ws_bytes = lib.rpst_adaptive_attention_workspace_size(chunk, C, hw, hid)
+    ws = torch.empty(ws_bytes, device=F.device, dtype=torch.uint8)
+    for b0 in range(0, B, chunk):
+        nb = min(chunk, B - b0)
+        flops = nb * (6.0 * hw * hw * C + 2.0 * hw * hw * hid)
+        with _traced(f"adaptive_attention C{C} HW{hw} N{nb}", flops, 0.0):
+            _lib.call("rpst_adaptive_attention", F[b0].data_ptr(), G[b0].data_ptr(),
+                      H[b0].data_ptr(), content[b0].data_ptr(), style[b0].data_ptr(),
+                      w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(), hid, mode,
+                      scale, from_value, interval, out[b0].data_ptr(), claim[b0].data_ptr(),
+                      before[b0].data_ptr() if keep_claims else None,
+                      after[b0].data_ptr() if keep_claims else None, nb, C, hw,
+                      ws.data_ptr(), ws_bytes, _stream(F))
+    return out, claim, before, after
+
+
 def matrix_power_psd(A: torch.Tensor, p: float) -> torch.Tensor:
     """(A + 1e-4 I)^p, p = +-1/2, for symmetric PSD fp64 (n,n) or (b,n,n) matrices
     (wct_rp.py:7-40)."""

@@ -225,6 +225,68 @@ def gen_sanet(net):
     np.savez_compressed(os.path.join(HERE, "sanet.npz"), **out)
 
 
+def gen_adaptive(net):
+    """AdaptiveSANet / AdaptiveTransform / AdaptiveSAModel, both AEA
+    modules. AdaptiveSAModel.test() draws seaborn heatmaps after the forward pass, so its
+    output is produced by the same calls test() makes (encode style, encode content,
+    fuse, decoder; sanet.py:336-341) without the plotting."""
+    from network.sanet import (AdaptiveSANet, AdaptiveTransform, AEALReluModule, AEAModule,
+                               cal_affinity_matrix)
+    out = {}
+    # affinity and the AEA modules at the function level
+    c = rand_feat(800, (2, 16, 6, 8), scale=2.0, offset=0.3, relu=True)
+    s = rand_feat(801, (2, 16, 6, 8), scale=2.0, offset=0.3, relu=True)
+    c[0, :, 0, 0] = 0.0  # an all-zero position: normalize's 1e-12 floor
+    aff = cal_affinity_matrix(t(c), t(s))
+    out.update(aff_c=c, aff_s=s, aff_out=aff.numpy())
+    for mode, cls in (("aea", AEAModule), ("relu", AEALReluModule)):
+        mod = cls(48)
+        ck = synth_model_(mod, 90 if mode == "aea" else 91)
+        fx = torch.softmax(t(rand_feat(802, (2, 48, 48), scale=4.0)), dim=-1)
+        with torch.no_grad():
+            y, cl = mod(aff, fx)
+        out.update({f"aea_{mode}_fx": fx.numpy(), f"aea_{mode}_out": y.numpy(),
+                    f"aea_{mode}_clamp": cl.numpy(), f"aea_{mode}_ck": ck})
+    for mode in ("aea", "relu"):
+        for i, (b, cdim, h, w) in enumerate([(2, 32, 8, 8), (1, 64, 5, 7)]):
+            mod = AdaptiveSANet(cdim, h * w, mode)
+            seed = 92 + 2 * i + (mode == "relu")
+            ck = synth_model_(mod, seed)
+            c = rand_feat(810 + i, (b, cdim, h, w), scale=2.0, offset=0.5, relu=True)
+            s = rand_feat(820 + i, (b, cdim, h, w), scale=2.0, offset=0.5, relu=True)
+            with torch.no_grad():
+                y = mod(t(c), t(s))
+            out.update({f"asa_{mode}_c{i}": c, f"asa_{mode}_s{i}": s,
+                        f"asa_{mode}_out{i}": y.numpy(), f"asa_{mode}_ck{i}": ck,
+                        f"asa_{mode}_claim{i}": mod.claim_value.numpy(),
+                        f"asa_{mode}_seed{i}": seed})
+        tr = AdaptiveTransform(32, 64, 16, mode)
+        ck = synth_model_(tr, 98 + (mode == "relu"))
+        c4 = rand_feat(830, (2, 32, 8, 8), relu=True)
+        s4 = rand_feat(831, (2, 32, 8, 8), relu=True)
+        c5 = rand_feat(832, (2, 32, 4, 4), relu=True)
+        s5 = rand_feat(833, (2, 32, 4, 4), relu=True)
+        with torch.no_grad():
+            y = tr(t(c4), t(s4), t(c5), t(s5))
+        out.update({f"atr_{mode}_c4": c4, f"atr_{mode}_s4": s4, f"atr_{mode}_c5": c5,
+                    f"atr_{mode}_s5": s5, f"atr_{mode}_out": y.numpy(), f"atr_{mode}_ck": ck})
+        cfg = {"content_weight": 1.0, "style_weight": 3.0, "l_identity1_weight": 50.0,
+               "l_identity2_weight": 1.0, "ada_module": mode, "output": "/nonexistent"}
+        m = net.AdaptiveSAModel(cfg, copy.deepcopy(net.vgg), 0, 64)
+        ck = synth_model_(m, 100 + (mode == "relu"))
+        cimg = synth.image(9100, (1, 3, 64, 64))
+        simg = synth.image(9200, (1, 3, 64, 64))
+        m.eval()
+        with torch.no_grad():
+            sf = m.encode_with_intermediate(t(simg))
+            cf = m.encode_with_intermediate(t(cimg))
+            y = m.decoder(m.fuse(cf, sf))
+        out.update({f"model_{mode}_content": cimg, f"model_{mode}_style": simg,
+                    f"model_{mode}_out": y.numpy(), f"model_{mode}_ck": ck,
+                    f"model_{mode}_seed": 100 + (mode == "relu")})
+    np.savez_compressed(os.path.join(HERE, "adaptive.npz"), **out)
+
+
 def gen_vgg(net):
     out = {}
     vgg = copy.deepcopy(net.vgg)
@@ -300,6 +362,8 @@ def gen_keys(net):
         "MultiScaleAdaINRPNet_inception1": net.MultiScaleAdaINRPNet(
             multiscale_config(16, 4, 1), vgg),
         "SourceNet": net.SourceNet({"use_mask": False}, vgg),
+        "AdaptiveSAModel_aea": net.AdaptiveSAModel({"ada_module": "aea"}, vgg, 0, 512),
+        "AdaptiveSAModel_relu": net.AdaptiveSAModel({"ada_module": "relu"}, vgg, 0, 512),
         "vgg": net.vgg,
         "decoder": net.decoder,
     }
@@ -310,7 +374,8 @@ def gen_keys(net):
 
 GENERATORS = {"keys": gen_keys, "stats": gen_stats, "adain_rp": gen_adain_rp,
               "forward": gen_forward, "wct": gen_wct, "sanet": gen_sanet, "vgg": gen_vgg,
-              "multiscale": gen_multiscale, "sourcenet": gen_sourcenet}
+              "multiscale": gen_multiscale, "sourcenet": gen_sourcenet,
+              "adaptive": gen_adaptive}
 
 
 def main():

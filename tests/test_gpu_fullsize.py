@@ -20,7 +20,7 @@ def test_adain_rp_512(cuda):
     from rpst import synth
     m = net.AdaINRPNet(rp_config(16), copy.deepcopy(net.vgg))
     synth_(m, 0)
-    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     c = torch.from_numpy(synth.image(1000, (1, 3, 512, 512)))
     s = torch.from_numpy(synth.image(2000, (1, 3, 512, 512)))
     out = m.to(cuda).test(c.to(cuda), s.to(cuda))
@@ -35,7 +35,7 @@ def test_adain_rp_1024_one_image(cuda):
     from rpst import synth
     m = net.AdaINRPNet(rp_config(16), copy.deepcopy(net.vgg))
     synth_(m, 0)
-    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     c = torch.from_numpy(synth.image(3, (1, 3, 1024, 1024)))
     s = torch.from_numpy(synth.image(4, (1, 3, 1024, 1024)))
     out = m.to(cuda).test(c.to(cuda), s.to(cuda))
@@ -87,7 +87,7 @@ def test_samodel_512(cuda):
     from rpst import synth
     m = net.SAModel({}, copy.deepcopy(net.vgg), 0, 512)
     synth_(m, 0)
-    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     c = torch.from_numpy(synth.image(5, (1, 3, 512, 512)))
     s = torch.from_numpy(synth.image(6, (1, 3, 512, 512)))
     out = m.to(cuda).test(c.to(cuda), s.to(cuda))

@@ -238,7 +238,7 @@ def test_adain_rp_vs_oracle_hidden16(cuda):
     import network as net
     m = net.AdaINRPNet(rp_config(16), copy.deepcopy(net.vgg))
     synth_(m, 5)
-    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     from rpst import synth
     c = torch.from_numpy(synth.image(1, (2, 3, 64, 96)))
     s = torch.from_numpy(synth.image(2, (2, 3, 64, 96)))

@@ -157,9 +157,44 @@ def test_sourcenet_test(golden):
         assert rel_l2(out, g[f"out{i}"]) < 1e-6, (i, rel_l2(out, g[f"out{i}"]))
 
 
+def test_adaptive_sanet_family(golden):
+    """cal_affinity_matrix, AEAModule / AEALReluModule, AdaptiveSANet, AdaptiveTransform and
+    AdaptiveSAModel against the reference."""
+    import network as net
+    g = golden("adaptive")
+    aff = R.cal_affinity_matrix(t(g["aff_c"]), t(g["aff_s"]))
+    assert rel_l2(aff, g["aff_out"]) < 1e-6
+    for mode, cls in (("aea", net.AEAModule), ("relu", net.AEALReluModule)):
+        mod = cls(48)
+        np.testing.assert_allclose(synth_(mod, 90 if mode == "aea" else 91),
+                                   g[f"aea_{mode}_ck"], rtol=1e-12)
+        y, cl = R.aea(t(g["aff_out"]), t(g[f"aea_{mode}_fx"]), state_dict_of(mod), "", mode)
+        assert rel_l2(y, g[f"aea_{mode}_out"]) < 1e-6 and rel_l2(cl, g[f"aea_{mode}_clamp"]) < 1e-6
+        for i in range(2):
+            c = t(g[f"asa_{mode}_c{i}"])
+            mod = net.AdaptiveSANet(c.shape[1], c.shape[2] * c.shape[3], mode)
+            np.testing.assert_allclose(synth_(mod, int(g[f"asa_{mode}_seed{i}"])),
+                                       g[f"asa_{mode}_ck{i}"], rtol=1e-12)
+            y, cl = R.adaptive_sanet(c, t(g[f"asa_{mode}_s{i}"]), state_dict_of(mod), "", mode)
+            assert rel_l2(y, g[f"asa_{mode}_out{i}"]) < 1e-6, (mode, i)
+            assert rel_l2(cl, g[f"asa_{mode}_claim{i}"]) < 1e-6
+        tr = net.AdaptiveTransform(32, 64, 16, mode)
+        np.testing.assert_allclose(synth_(tr, 98 + (mode == "relu")), g[f"atr_{mode}_ck"],
+                                   rtol=1e-12)
+        y = R.adaptive_transform(*(t(g[f"atr_{mode}_{k}"]) for k in ("c4", "s4", "c5", "s5")),
+                                 state_dict_of(tr), "", mode)
+        assert rel_l2(y, g[f"atr_{mode}_out"]) < 1e-6
+        m = net.AdaptiveSAModel({"ada_module": mode}, copy.deepcopy(net.vgg), 0, 64)
+        np.testing.assert_allclose(synth_(m, int(g[f"model_{mode}_seed"])), g[f"model_{mode}_ck"],
+                                   rtol=1e-12)
+        y = R.adaptive_samodel_test(t(g[f"model_{mode}_content"]), t(g[f"model_{mode}_style"]),
+                                    state_dict_of(m), mode)
+        assert rel_l2(y, g[f"model_{mode}_out"]) < 1e-6, mode
+
+
 @pytest.mark.parametrize("name", ["AdaINRPNet", "WCTRPNet", "SAModel", "vgg", "decoder",
                                   "MultiScaleAdaINRPNet", "MultiScaleAdaINRPNet_inception1",
-                                  "SourceNet"])
+                                  "SourceNet", "AdaptiveSAModel_aea", "AdaptiveSAModel_relu"])
 def test_state_dict_keys_match_reference(name):
     """Checkpoint compatibility: same keys and shapes as the reference modules."""
     import network as net
@@ -173,6 +208,10 @@ def test_state_dict_keys_match_reference(name):
             "MultiScaleAdaINRPNet_inception1": lambda: net.MultiScaleAdaINRPNet(
                 multiscale_config(16, 4, 1), vgg),
             "SourceNet": lambda: net.SourceNet({"use_mask": False}, vgg),
+            "AdaptiveSAModel_aea": lambda: net.AdaptiveSAModel({"ada_module": "aea"}, vgg, 0,
+                                                               512),
+            "AdaptiveSAModel_relu": lambda: net.AdaptiveSAModel({"ada_module": "relu"}, vgg, 0,
+                                                                512),
             "vgg": lambda: net.vgg, "decoder": lambda: net.decoder}[name]()
     got = [[k, list(v.shape)] for k, v in mine.state_dict().items()]
     assert got == ref
