@@ -187,6 +187,16 @@ int rpst_adaptive_attention(const float* F, const float* G, const float* H,
                             int C, int HW, void* workspace, size_t workspace_bytes,
                             rpst_stream_t stream);
 
+/* ---- f4: host I/O pixel conversions  test.py:49-54, 139-149 ------
+ * transforms.ToTensor: in (N, H, W, 3) uint8 -> out (N, 3, H, W) fp32 = u8 / 255. */
+int rpst_u8hwc_to_f32nchw(const uint8_t* in, float* out, int N, int H, int W,
+                          rpst_stream_t stream);
+/* torchvision.utils.save_image's pixel path: in (N, 3, H, W) fp32 -> uint8 of
+ * clamp(x * 255 + 0.5, 0, 255) written as the tile at (y0, x0) of each of N canvases
+ * (canvas_h, canvas_w, 3) HWC. make_grid's padding is the caller's memset of the canvas. */
+int rpst_f32nchw_to_u8_tile(const float* in, uint8_t* canvas, int N, int H, int W,
+                            int canvas_h, int canvas_w, int y0, int x0, rpst_stream_t stream);
+
 /* ---- a7: matrix_sqrt / matrix_inv_sqrt  network/wct_rp.py:7-40 ----------------------
  * out[b] = (A[b] + 1e-4 I)^(+1/2) (inverse = 0) or ^(-1/2) (inverse = 1) for symmetric PSD
  * fp64 n x n matrices, batch of `batch`. Coupled Newton-Schulz (fixed 40 steps); equal to

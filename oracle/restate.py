@@ -335,6 +335,47 @@ def adaptive_samodel_test(content: Tensor, style: Tensor, sd: SD, mode: str) -> 
         return decoder(fusion, sd, "decoder.")
 
 
+# ---- f4: host I/O pixel paths (test.py:49-54, 139-149) ---------------------------------
+# torchvision (ToTensor, utils.make_grid / save_image) is a third-party dependency of the
+# reference that is absent from this image; these restate its published algorithm
+# (torchvision >= 0.8: ToTensor = u8.float().div(255); save_image = make_grid(padding=2,
+# pad_value=0) then mul(255).add_(0.5).clamp_(0, 255).permute(1, 2, 0).to(uint8)).
+# Parity against torchvision itself is unpinned; the PNG bytes come from PIL in both.
+def to_tensor_u8(hwc) -> Tensor:
+    """transforms.ToTensor of a uint8 (H, W, 3) array -> (3, H, W) fp32."""
+    t = torch.from_numpy(hwc).permute(2, 0, 1).contiguous()
+    return t.to(torch.float32).div(255)
+
+
+def make_grid(images: Tensor, nrow: int = 8, padding: int = 2, pad_value: float = 0.0) -> Tensor:
+    """torchvision.utils.make_grid for a (B, 3, H, W) batch (no normalisation)."""
+    if images.dim() == 3:
+        images = images.unsqueeze(0)
+    if images.shape[0] == 1:
+        return images.squeeze(0)
+    nmaps = images.shape[0]
+    xmaps = min(nrow, nmaps)
+    ymaps = (nmaps + xmaps - 1) // xmaps
+    height, width = images.shape[2] + padding, images.shape[3] + padding
+    grid = images.new_full((images.shape[1], height * ymaps + padding, width * xmaps + padding),
+                           pad_value)
+    k = 0
+    for y in range(ymaps):
+        for x in range(xmaps):
+            if k >= nmaps:
+                break
+            grid.narrow(1, y * height + padding, height - padding).narrow(
+                2, x * width + padding, width - padding).copy_(images[k])
+            k += 1
+    return grid
+
+
+def save_image_u8(images: Tensor, nrow: int = 8):
+    """The uint8 (H, W, 3) array torchvision.utils.save_image hands to PIL."""
+    grid = make_grid(images, nrow=nrow)
+    return grid.mul(255).add_(0.5).clamp_(0, 255).permute(1, 2, 0).to("cpu", torch.uint8).numpy()
+
+
 def rel_l2(a: Tensor, b: Tensor) -> float:
     a = a.double()
     b = b.double()

@@ -1,0 +1,212 @@
+"""Host I/O around the stylisation path: what the reference's
+test driver does around `network.test()` (test.py:117-150, datasets/base.py:51-165).
+
+  datasets   PairedDataset (datasets/base.py:51-86: content/<name> paired with
+             style/<name>) and PhotorealisticPairedDataset (:89-131: style/tar<name
+             without 'in'>, plus labelme_segmentation mask paths)
+  decode     PIL open -> convert('RGB') -> resize((size, size), BILINEAR): exactly what
+             transforms.Resize((s, s)) does to a PIL image (test.py:49-54), on a host
+             thread pool
+  ToTensor   on the GPU (`rpst_u8hwc_to_f32nchw`): uint8 pixels cross PCIe, 3 B/pixel
+  save_image on the GPU (`rpst_f32nchw_to_u8_tile`): make_grid(nrow=3, padding=2,
+             pad_value=0) of [content, style, stylized] and the single stylised image,
+             x*255+0.5 clamped to uint8 (test.py:139-149); PNG encoding by PIL on host
+             threads.
+
+`Pipeline` overlaps the three: batch k+1 decodes on the thread pool while batch k runs
+on the GPU; pinned host buffers and a copy stream carry the pixels; PNG encoding of
+batch k runs on the writer threads behind a HIP event.
+"""
+from __future__ import annotations
+
+import os
+from concurrent.futures import ThreadPoolExecutor
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .ops import _check, _stream
+
+PAD = 2  # torchvision.utils.make_grid default padding (test.py:145 uses the default)
+
+
+# ---- datasets (paths and names only; decoding is the pipeline's) ----------------------
+class PairedDataset:
+    """datasets/base.py:51-86: content/<f> is paired with style/<f> (same file name)."""
+
+    def __init__(self, root: str):
+        self.root = root
+        self.content_dir = os.path.join(root, "content")
+        self.style_dir = os.path.join(root, "style")
+        self.content_names = os.listdir(self.content_dir)
+        self.style_names = os.listdir(self.style_dir)
+
+    def style_name_of(self, content_name: str) -> str:
+        return content_name
+
+    def item(self, index: int):
+        """(content_path, style_path, content_stem, style_stem, c_mask, s_mask)."""
+        cp = os.path.join(self.content_dir, self.content_names[index])
+        sp = os.path.join(self.style_dir, self.style_name_of(self.content_names[index]))
+        cn = os.path.splitext(os.path.basename(cp))[0]
+        sn = os.path.splitext(os.path.basename(sp))[0]
+        return cp, sp, cn, sn, [], []
+
+    def __len__(self):
+        return len(self.content_names)
+
+
+class PhotorealisticPairedDataset(PairedDataset):
+    """datasets/base.py:89-131: style/tar<content name without 'in'>, masks under
+    labelme_segmentation/<stem>.png (paths only; the masked networks are out of scope)."""
+
+    def __init__(self, root: str):
+        super().__init__(root)
+        self.seg_dir = os.path.join(root, "labelme_segmentation")
+
+    def style_name_of(self, content_name: str) -> str:
+        return "tar{}".format(content_name.replace("in", ""))
+
+    def item(self, index: int):
+        cp, sp, cn, sn, _, _ = super().item(index)
+        return (cp, sp, cn, sn, os.path.join(self.seg_dir, f"{cn}.png"),
+                os.path.join(self.seg_dir, f"{sn}.png"))
+
+
+DATASETS = {"paired": PairedDataset, "photoreal": PhotorealisticPairedDataset}
+
+
+def load_image(path: str, size: int) -> np.ndarray:
+    """Image.open().convert('RGB') + transforms.Resize((size, size)) -> uint8 (size, size, 3).
+    torchvision's Resize on a PIL image is PIL's resize with BILINEAR (antialiased)."""
+    from PIL import Image
+    with Image.open(path) as im:
+        im = im.convert("RGB")
+        if im.size != (size, size):
+            im = im.resize((size, size), Image.BILINEAR)
+        return np.asarray(im, dtype=np.uint8).copy()
+
+
+def save_png(arr: np.ndarray, path: str) -> None:
+    from PIL import Image
+    Image.fromarray(arr).save(path)
+
+
+# ---- GPU pixel conversions -------------------------------------------------------------
+def to_tensor(u8: torch.Tensor) -> torch.Tensor:
+    """(N, H, W, 3) uint8 on the GPU -> (N, 3, H, W) fp32 in [0, 1] (transforms.ToTensor)."""
+    assert u8.dim() == 4 and u8.shape[-1] == 3 and u8.dtype == torch.uint8 and u8.is_cuda
+    u8 = u8.contiguous()
+    n, h, w, _ = u8.shape
+    out = torch.empty((n, 3, h, w), device=u8.device, dtype=torch.float32)
+    _lib.call("rpst_u8hwc_to_f32nchw", u8.data_ptr(), out.data_ptr(), n, h, w, _stream(u8))
+    return out
+
+
+def _tile(x: torch.Tensor, canvas: torch.Tensor, y0: int, x0: int) -> None:
+    n, c, h, w = x.shape
+    assert c == 3, "save_image path expects RGB tensors"
+    _lib.call("rpst_f32nchw_to_u8_tile", x.data_ptr(), canvas.data_ptr(), n, h, w,
+              canvas.shape[1], canvas.shape[2], y0, x0, _stream(x))
+
+
+def to_uint8(x: torch.Tensor) -> torch.Tensor:
+    """save_image of one image per batch entry: (N, 3, H, W) fp32 -> (N, H, W, 3) uint8."""
+    _check(x)
+    x = x.contiguous()
+    n, _, h, w = x.shape
+    out = torch.empty((n, h, w, 3), device=x.device, dtype=torch.uint8)
+    _tile(x, out, 0, 0)
+    return out
+
+
+def grid_uint8(images: Sequence[torch.Tensor]) -> torch.Tensor:
+    """save_image(stack([a, b, c]), nrow=len(images)) per batch entry: one row of tiles
+    with make_grid's padding of 2 and pad value 0 -> (N, H+4, k(W+2)+2, 3) uint8."""
+    _check(*images)
+    n, _, h, w = images[0].shape
+    k = len(images)
+    canvas = torch.zeros((n, h + 2 * PAD, k * (w + PAD) + PAD, 3), device=images[0].device,
+                         dtype=torch.uint8)
+    for j, im in enumerate(images):
+        assert im.shape == images[0].shape
+        _tile(im.contiguous(), canvas, PAD, PAD + j * (w + PAD))
+    return canvas
+
+
+# ---- pipeline ----------------------------------------------------------------------------
+class Pipeline:
+    """Stylise a paired dataset batch by batch and write `{cn}-{sn}.png` and
+    `{cn}-{sn}-cat.png` (test.py:128-150) into out_dir.
+
+    stylize(content, style) -> stylized runs on `device` (e.g. a model's `test`)."""
+
+    def __init__(self, stylize: Callable[[torch.Tensor, torch.Tensor], torch.Tensor],
+                 device, img_size: int, batch_size: int = 1, num_workers: int = 4,
+                 cat: bool = True):
+        self.stylize = stylize
+        self.device = torch.device(device)
+        self.img_size = img_size
+        self.batch_size = max(1, batch_size)
+        self.workers = max(1, num_workers)
+        self.cat = cat
+
+    def _decode(self, dataset, idx: List[int]):
+        items = [dataset.item(i) for i in idx]
+        pix = np.empty((2, len(idx), self.img_size, self.img_size, 3), dtype=np.uint8)
+        for j, it in enumerate(items):
+            pix[0, j] = load_image(it[0], self.img_size)
+            pix[1, j] = load_image(it[1], self.img_size)
+        return items, torch.from_numpy(pix).pin_memory()
+
+    def run(self, dataset, out_dir: str, log: Optional[Callable[[str], None]] = None) -> int:
+        os.makedirs(out_dir, exist_ok=True)
+        batches = [list(range(s, min(s + self.batch_size, len(dataset))))
+                   for s in range(0, len(dataset), self.batch_size)]
+        if not batches:
+            return 0
+        copy_stream = torch.cuda.Stream(self.device)
+        written = 0
+        with ThreadPoolExecutor(self.workers) as readers, \
+                ThreadPoolExecutor(self.workers) as writers, torch.no_grad():
+            pending = [readers.submit(self._decode, dataset, batches[0])]
+            saves = []
+            for k in range(len(batches)):
+                if k + 1 < len(batches):  # decode the next batch while this one runs
+                    pending.append(readers.submit(self._decode, dataset, batches[k + 1]))
+                items, pinned = pending.pop(0).result()
+                with torch.cuda.stream(copy_stream):
+                    dev_u8 = pinned.to(self.device, non_blocking=True)
+                compute = torch.cuda.current_stream(self.device)
+                compute.wait_stream(copy_stream)
+                dev_u8.record_stream(compute)
+                content, style = to_tensor(dev_u8[0]), to_tensor(dev_u8[1])
+                stylized = self.stylize(content, style)
+                outs = [to_uint8(stylized)]
+                if self.cat:
+                    outs.append(grid_uint8([content, style, stylized]))
+                host = [torch.empty(o.shape, dtype=torch.uint8, pin_memory=True) for o in outs]
+                copy_stream.wait_stream(compute)
+                with torch.cuda.stream(copy_stream):
+                    for o, h in zip(outs, host):
+                        o.record_stream(copy_stream)
+                        h.copy_(o, non_blocking=True)
+                    done = torch.cuda.Event()
+                    done.record(copy_stream)
+                saves.append(writers.submit(self._write, done, items, host, out_dir, log))
+            for f in saves:
+                written += f.result()
+        return written
+
+    @staticmethod
+    def _write(done, items, host, out_dir, log) -> int:
+        done.synchronize()
+        for j, (_, _, cn, sn, _, _) in enumerate(items):
+            save_png(host[0][j].numpy(), os.path.join(out_dir, f"{cn}-{sn}.png"))
+            if len(host) > 1:
+                save_png(host[1][j].numpy(), os.path.join(out_dir, f"{cn}-{sn}-cat.png"))
+            if log:
+                log(f"Proceed {cn}-{sn}.")
+        return len(items)
