@@ -55,6 +55,8 @@ def build_model(kind, dev):
         m = net.SourceNet(SOURCE_CONFIG, copy.deepcopy(net.vgg))
     elif kind == "adaptive":
         m = net.AdaptiveSAModel(ADAPTIVE_CONFIG, copy.deepcopy(net.vgg), 0, 512)
+    elif kind == "train":
+        m = net.AdaINRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, 512)
     synth.synth_module_(m, 0)
@@ -81,9 +83,12 @@ WORKLOADS = {
     "source": "SourceNet.test() VGG relu4_1 AdaIN + decoder, 512x512 (SURVEY 8(f) rank 3)",
     "adaptive": "AdaptiveSAModel.test() ada_module=relu (AEA clamp) VGG relu1_1-5_1 + decoder, "
                 "512x512 (SURVEY 8(f) rank 3)",
+    "train": "AdaINRPNet training iteration: forward() losses + total_loss.backward() + Adam "
+             "step, rp_blocks=5 hidden_dim=16, 512x512 (SURVEY 8(f) rank 2; gradients "
+             "all-reduced over ranks)",
 }
 DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32, "multiscale": 32, "source": 32,
-                 "adaptive": 32}
+                 "adaptive": 32, "train": 8}
 
 
 def cpu_baseline(kind, size, budget_s=12.0):
@@ -91,7 +96,7 @@ def cpu_baseline(kind, size, budget_s=12.0):
     from oracle import restate as R
     from rpst import synth
     import network as net
-    cfg = {"rp_blocks": 5, "hidden_dim": 16}
+    cfg = {"rp_blocks": 5, "hidden_dim": 16, "content_weight": 1.0, "style_weight": 10.0}
     if kind == "adain":
         m = net.AdaINRPNet(cfg, copy.deepcopy(net.vgg))
         fn = lambda c, s, sd: R.adain_rp_test(c, s, sd, 5)  # noqa: E731
@@ -107,6 +112,9 @@ def cpu_baseline(kind, size, budget_s=12.0):
     elif kind == "adaptive":
         m = net.AdaptiveSAModel(ADAPTIVE_CONFIG, copy.deepcopy(net.vgg), 0, size)
         fn = lambda c, s, sd: R.adaptive_samodel_test(c, s, sd, "relu")  # noqa: E731
+    elif kind == "train":
+        m = net.AdaINRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
+        fn = lambda c, s, sd: R.adain_rp_grads(c, s, sd, 5, 1.0, 1.0)  # noqa: E731
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, size)
         fn = R.samodel_test
@@ -152,7 +160,7 @@ def roofline_from_trace(summary):
     from rpst import _lib
     best = None
     for name, a in summary.items():
-        if not name.startswith(("conv", "wino")):
+        if not name.startswith(("conv", "wino", "wgrad")):
             continue
         if best is None or a["ms"] > best[1]["ms"]:
             best = (name, a)
@@ -171,15 +179,20 @@ def roofline_from_trace(summary):
     k, chans, hw, nn, op = name.split()
     cin, cout = (int(v) for v in chans.split("->"))
     h, w = (int(v) for v in hw.split("x"))
-    n, in_op, ks = int(nn[1:]), int(op[2:]), int(k[4])
+    n, in_op, ks = int(nn[1:]), int(op[2:]), int(k[-1])
     hs, ws = ((h * 2, w * 2) if in_op == 1 else ((h // 2, w // 2) if in_op == 2 else (h, w)))
-    grid = _lib.load().rpst_conv2d_grid_threads(n, hs, ws, cout, ks, in_op)
-    kname = "wino_mfma_kernel" if wino else "conv_mfma_kernel"
-    traffic = pmc_lookup(kname, grid)
+    if name.startswith("wgrad"):  # weight gradient (training): not in the PMC table
+        kname, traffic = "conv_wgrad_kernel", None
+    else:
+        grid = _lib.load().rpst_conv2d_grid_threads(n, hs, ws, cout, ks, in_op)
+        kname = "wino_mfma_kernel" if wino else "conv_mfma_kernel"
+        traffic = pmc_lookup(kname, grid)
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
             "traffic": traffic, "kernel": f"{kname} [{name}]",
-            "algorithm": "winograd F(2x2,3x3) fp32" if wino else "direct implicit GEMM fp32",
+            "algorithm": "winograd F(2x2,3x3) fp32" if wino else (
+                "weight-gradient implicit GEMM fp32" if name.startswith("wgrad")
+                else "direct implicit GEMM fp32"),
             "effective_tflops": round(effective, 2),
             "launch_ms": round(avg_ms, 4), "flop_per_launch": flop,
             "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None}
@@ -247,8 +260,26 @@ def main():
     content = torch.from_numpy(synth.image(1000 + rank, shape)).to(dev)
     style = torch.from_numpy(synth.image(2000 + rank, shape)).to(dev)
 
+    if args.model == "train":
+        from rpst.shard import GradientAllReduce
+        params = [p for p in model.parameters() if p.requires_grad]
+        optimizer = torch.optim.Adam(params, lr=1e-4)
+        reduce_grads = GradientAllReduce(params) if world > 1 else None
+
+        def step():
+            optimizer.zero_grad()
+            _, total = model(content, style)
+            total.backward()
+            if reduce_grads is not None:
+                reduce_grads()
+            optimizer.step()
+            return total
+    else:
+        def step():
+            return model.test(content, style)
+
     for _ in range(args.warmup):
-        model.test(content, style)
+        step()
     torch.cuda.synchronize()
 
     ops.TRACE = ops.Trace()
@@ -257,14 +288,14 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = model.test(content, style)
+        out = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     summary = ops.TRACE.summary()
     ops.TRACE = None
-    assert out.shape == shape and torch.isfinite(out).all()
+    assert torch.isfinite(out).all() and (args.model == "train" or out.shape == shape)
 
     if world > 1:
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -281,7 +312,9 @@ def main():
             else "fp32 conv / f64 WCT", "data": "synthetic U[0,1) images, synthetic He-uniform weights",
             "config": {"workload": WORKLOADS[args.model], "per_gpu_batch": B,
                        "global_batch": B * world, "image": f"{args.size}x{args.size}",
-                       "parallelism": f"per-image batch split over {world} GPU(s), no collectives"},
+                       "parallelism": (f"data parallel over {world} GPU(s), one gradient "
+                                       "all-reduce per step") if args.model == "train" else
+                       f"per-image batch split over {world} GPU(s), no collectives"},
             "roofline": roofline_from_trace(summary),
             "roofline_adain": adain_roofline(
                 summary if any(k.startswith("adain") for k in summary)

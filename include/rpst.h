@@ -197,6 +197,52 @@ int rpst_u8hwc_to_f32nchw(const uint8_t* in, float* out, int N, int H, int W,
 int rpst_f32nchw_to_u8_tile(const float* in, uint8_t* canvas, int N, int H, int W,
                             int canvas_h, int canvas_w, int y0, int x0, rpst_stream_t stream);
 
+/* ---- f2: training backward  AdaINRPNet.forward adain_rp.py:110-138 +
+ * total_loss.backward() train.py:186-189. Conv dgrad runs on rpst_conv2d with weights from
+ * rpst_conv_weight_flip (packed by rpst_conv2d_pack); reflect-padded convs then add
+ * rpst_reflect_pad_border_grad.
+ * w (Cout, Cin, k, k) -> wt (Cin, Cout, k, k), wt[ci][co][a][b] = w[co][ci][k-1-a][k-1-b]. */
+int rpst_conv_weight_flip(const float* w, float* wt, int Cout, int Cin, int ksize,
+                          rpst_stream_t stream);
+/* ReLU backward: out = y > 0 ? g : 0 (y = the ReLU output), n elements. */
+int rpst_relu_backward(const float* g, const float* y, float* out, int64_t n,
+                       rpst_stream_t stream);
+/* MaxPool2d(2, 2, ceil_mode=True) backward: x (N,C,H,W) the pool input, g the gradient at
+ * its output -> dx (N,C,H,W) (argmax as ATen: first max in window order, NaN wins);
+ * relu_mask = 1 also applies ReLU backward with y = x (x is a ReLU output). */
+int rpst_maxpool2x2_ceil_backward(const float* x, const float* g, float* dx, int N, int C,
+                                  int H, int W, int relu_mask, rpst_stream_t stream);
+/* ReflectionPad2d(1) + conv3x3 backward, border part: dy (N,Cout,H,W), w (Cout,Cin,3,3);
+ * dx (N,Cin,H,W) holds the zero-padded dgrad and receives the padded border's gradient
+ * folded onto the rows / columns it reflects. H, W >= 2. */
+int rpst_reflect_pad_border_grad(const float* dy, const float* w, float* dx, int N, int Cin,
+                                 int Cout, int H, int W, rpst_stream_t stream);
+/* conv3x3 (stride 1, zero pad 1) weight / bias gradient: x (N,Cin,H,W) the conv input, dy
+ * (N,Cout,H,W) the gradient at its output -> dw (Cout,Cin,3,3), db (Cout) (db may be NULL).
+ * Workspace: rpst_conv_wgrad_workspace_size(N, Cin, H, W, Cout). */
+size_t rpst_conv_wgrad_workspace_size(int N, int Cin, int H, int W, int Cout);
+int rpst_conv_wgrad(const float* x, const float* dy, float* dw, float* db, int N, int Cin,
+                    int H, int W, int Cout, void* workspace, size_t workspace_bytes,
+                    rpst_stream_t stream);
+/* adaptive_instance_normalization backward (base.py:410-418): g the gradient at the AdaIN
+ * output, c / s the content / style features (planes x HW), stats = [mean_c | std_c |
+ * mean_s | std_s] (planes each) -> dc, ds. Workspace: 2*planes floats. */
+int rpst_adain_backward(const float* g, const float* c, const float* s, const float* stats,
+                        float* dc, float* ds, int planes, int64_t HW, void* workspace,
+                        size_t workspace_bytes, rpst_stream_t stream);
+/* Gradient of weights[0] * calc_style_loss(F, target) (+ weights[1] * mse(F, Fc) when Fc is
+ * non-NULL) w.r.t. F (planes x HW), adain_rp.py:84-88 / 131-136 with MSELoss (mean);
+ * stats = [mean | std | mean_t | std_t] (planes each); weights is a DEVICE pointer;
+ * accumulate = 1 adds into out. */
+int rpst_style_content_loss_grad(const float* F, const float* Fc, const float* stats,
+                                 const float* weights, float* out, int planes, int64_t HW,
+                                 int accumulate, rpst_stream_t stream);
+/* *out = scale * sum (a - b)^2 over n elements (fp64 accumulation, fixed order).
+ * Workspace: rpst_sq_diff_workspace_size(). */
+size_t rpst_sq_diff_workspace_size(void);
+int rpst_sq_diff_sum(const float* a, const float* b, int64_t n, double scale, float* out,
+                     void* workspace, size_t workspace_bytes, rpst_stream_t stream);
+
 /* ---- a7: matrix_sqrt / matrix_inv_sqrt  network/wct_rp.py:7-40 ----------------------
  * out[b] = (A[b] + 1e-4 I)^(+1/2) (inverse = 0) or ^(-1/2) (inverse = 1) for symmetric PSD
  * fp64 n x n matrices, batch of `batch`. Coupled Newton-Schulz (fixed 40 steps); equal to

@@ -175,21 +175,39 @@ def style_loss(a: Tensor, b: Tensor) -> Tensor:
     return F.mse_loss(am, bm) + F.mse_loss(as_, bs)
 
 
+def adain_rp_losses(content, style, sd, rp_blocks, content_weight, style_weight):
+    """AdaINRPNet.forward loss dict (adain_rp.py:110-138), differentiable w.r.t. the
+    entries of sd (autograd on CPU: the gradient oracle of the training path)."""
+    cf = rp_stack(content, sd, "rp_shared_encoder.", rp_blocks)
+    sf = rp_stack(style, sd, "rp_shared_encoder.", rp_blocks)
+    stylized = rp_stack(adain(cf, sf), sd, "rp_decoder.", rp_blocks)
+    ds = encode_with_intermediate(stylized, sd)
+    dt = encode_with_intermediate(style, sd)
+    dc = encode_with_intermediate(content, sd)
+    ls = style_loss(ds[0], dt[0])
+    for i in range(1, 4):
+        ls = ls + style_loss(ds[i], dt[i])
+    lc = F.mse_loss(ds[-1], dc[-1])
+    tot = content_weight * lc + style_weight * ls
+    return {"style_loss": ls, "content_loss": lc, "total_loss": tot}
+
+
 def adain_rp_forward(content, style, sd, rp_blocks, content_weight, style_weight):
-    """AdaINRPNet.forward loss dict (adain_rp.py:110-138)."""
+    """AdaINRPNet.forward loss dict (adain_rp.py:110-138), values only."""
     with torch.no_grad():
-        cf = rp_stack(content, sd, "rp_shared_encoder.", rp_blocks)
-        sf = rp_stack(style, sd, "rp_shared_encoder.", rp_blocks)
-        stylized = rp_stack(adain(cf, sf), sd, "rp_decoder.", rp_blocks)
-        ds = encode_with_intermediate(stylized, sd)
-        dt = encode_with_intermediate(style, sd)
-        dc = encode_with_intermediate(content, sd)
-        ls = style_loss(ds[0], dt[0])
-        for i in range(1, 4):
-            ls = ls + style_loss(ds[i], dt[i])
-        lc = F.mse_loss(ds[-1], dc[-1])
-        tot = content_weight * lc + style_weight * ls
-        return {"style_loss": ls, "content_loss": lc, "total_loss": tot}
+        return adain_rp_losses(content, style, sd, rp_blocks, content_weight, style_weight)
+
+
+def adain_rp_grads(content, style, sd, rp_blocks, content_weight, style_weight):
+    """(loss dict, {name: d total_loss / d param}) for the RP encoder / decoder parameters
+    (the trainable ones; the VGG is frozen, adain_rp.py:27-29)."""
+    sd = {k: (v.detach().clone().requires_grad_(k.startswith(("rp_shared_encoder.", "rp_decoder.")))
+              if v.is_floating_point() else v) for k, v in sd.items()}
+    with torch.enable_grad():
+        losses = adain_rp_losses(content, style, sd, rp_blocks, content_weight, style_weight)
+        names = [k for k, v in sd.items() if v.requires_grad]
+        grads = torch.autograd.grad(losses["total_loss"], [sd[k] for k in names])
+    return ({k: v.detach() for k, v in losses.items()}, dict(zip(names, grads)))
 
 
 # ---- a7/a8/a9: WCT ----------------------------------------------------------------

@@ -1,0 +1,525 @@
+// Backward kernels of the AdaIN-RP training step:
+// AdaINRPNet.forward (network/adain_rp.py:110-138) + total_loss.backward() (train.py:186-189).
+//
+//   conv dgrad        = the forward conv kernel on flip-transposed weights (conv_flip_kernel
+//                       here, packing by rpst_conv2d_pack); reflect-padded convs (the frozen
+//                       VGG) add the padded border's gradient folded back onto the rows /
+//                       columns it reflects (reflect_border_grad_kernel)
+//   conv wgrad        conv_wgrad_kernel: implicit GEMM dW[co][ci][tap] = sum over (n,y,x) of
+//                       dY[n][co][y][x] X[n][ci][y+dy][x+dx] on fp32 MFMA, split over K
+//                       (pixels) with a fixed-order reduction (wgrad_reduce_kernel)
+//   bias grad         channel_sum_kernel
+//   ReLU / max-pool   relu_backward_kernel, maxpool2_backward_kernel (argmax = first max in
+//                       window order, NaN wins, as ATen's max_pool2d)
+//   AdaIN             adain_backward_reduce_kernel + adain_backward_apply_kernel
+//   losses            loss_seed_kernel (d/dF of calc_style_loss + calc_content_loss) and
+//                       sq_diff_sum_kernel (the loss values)
+// All reductions are fixed-order (no float atomics): results are deterministic.
+#include "rpst_common.h"
+
+namespace rpst {
+
+// ---- weights for dgrad: wt[ci][co][kh][kw] = w[co][ci][k-1-kh][k-1-kw] ------------------
+__global__ __launch_bounds__(256) void conv_flip_kernel(const float* __restrict__ w,
+                                                        float* __restrict__ wt, int Cout,
+                                                        int Cin, int K) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t kk = (int64_t)K * K;
+  if (i >= (int64_t)Cout * Cin * kk) return;
+  const int t = (int)(i % kk);
+  const int64_t r = i / kk;
+  const int ci = (int)(r % Cin), co = (int)(r / Cin);
+  wt[((int64_t)ci * Cout + co) * kk + (kk - 1 - t)] = w[i];
+}
+
+// ---- ReLU backward: threshold_backward(grad, output, 0) -----------------------------------
+__global__ __launch_bounds__(256) void relu_backward_kernel(const float* __restrict__ g,
+                                                            const float* __restrict__ y,
+                                                            float* __restrict__ out, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    const float4 gv = *reinterpret_cast<const float4*>(g + i);
+    const float4 yv = *reinterpret_cast<const float4*>(y + i);
+    float4 o;
+    o.x = yv.x > 0.f ? gv.x : 0.f;
+    o.y = yv.y > 0.f ? gv.y : 0.f;
+    o.z = yv.z > 0.f ? gv.z : 0.f;
+    o.w = yv.w > 0.f ? gv.w : 0.f;
+    *reinterpret_cast<float4*>(out + i) = o;
+  } else {
+    for (int64_t j = i; j < n; ++j) out[j] = y[j] > 0.f ? g[j] : 0.f;
+  }
+}
+
+// ---- MaxPool2d(2, 2, ceil_mode=True) backward, optionally masked by ReLU(x) > 0 ----------
+__global__ __launch_bounds__(256) void maxpool2_backward_kernel(
+    const float* __restrict__ x, const float* __restrict__ g, float* __restrict__ dx,
+    int64_t planes, int H, int W, int relu_mask) {
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= planes * Ho * Wo) return;
+  const int ox = (int)(i % Wo);
+  const int64_t r = i / Wo;
+  const int oy = (int)(r % Ho);
+  const int64_t p = r / Ho;
+  const float* s = x + p * H * W;
+  float* d = dx + p * H * W;
+  // ATen's CPU max_pool2d: window in row-major order, `val > max || isnan(val)` updates,
+  // the index starts at the window's first element
+  int best = 0;
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int yy = 2 * oy + (k >> 1), xx = 2 * ox + (k & 1);
+    if (yy < H && xx < W) {
+      const float v = s[(int64_t)yy * W + xx];
+      if (v > m || v != v) {
+        m = v;
+        best = k;
+      }
+    }
+  }
+  const float gv = g[i];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int yy = 2 * oy + (k >> 1), xx = 2 * ox + (k & 1);
+    if (yy < H && xx < W) {
+      float v = (k == best) ? gv : 0.f;
+      if (relu_mask && !(s[(int64_t)yy * W + xx] > 0.f)) v = 0.f;
+      d[(int64_t)yy * W + xx] = v;
+    }
+  }
+}
+
+// ---- reflect-pad border gradient ---------------------------------------------------------
+// Forward: Y = conv3x3_valid(ReflectionPad2d(1)(X)). The zero-padded dgrad conv gives the
+// gradient of the padded input's interior, dXp[1..H][1..W]; this adds the border entries
+// dXp[p][q] (p in {0, H+1} or q in {0, W+1}) to the X element they reflect: row 0 -> 1,
+// row H+1 -> H-2, column 0 -> 1, column W+1 -> W-2 (corners both ways). One thread per
+// target element (rows {1, H-2} fully, columns {1, W-2} on the other rows): every element
+// is updated by exactly one thread, in a fixed order.
+__device__ __forceinline__ int refl(int t, int n) { return t < 0 ? -t : (t >= n ? 2 * n - 2 - t : t); }
+
+__device__ float border_dxp(const float* __restrict__ dy, const float* __restrict__ w,
+                           int Cout, int Cin, int ci, int H, int W, int p, int q) {
+  // dXp[p][q] = sum_co sum_{kh,kw} dY[co][p-kh][q-kw] W[co][ci][kh][kw]
+  float acc = 0.f;
+  const int64_t HW = (int64_t)H * W;
+  for (int co = 0; co < Cout; ++co) {
+    const float* dyc = dy + co * HW;
+    const float* wc = w + ((int64_t)co * Cin + ci) * 9;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int y = p - kh;
+      if (y < 0 || y >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int x = q - kw;
+        if (x < 0 || x >= W) continue;
+        acc = fmaf(dyc[(int64_t)y * W + x], wc[kh * 3 + kw], acc);
+      }
+    }
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(64) void reflect_border_grad_kernel(
+    const float* __restrict__ dy, const float* __restrict__ w, float* __restrict__ dx, int N,
+    int Cin, int Cout, int H, int W, int nrows, int r0, int r1, int ncols, int c0, int c1) {
+  // targets per plane: nrows full rows (r0, r1) + ncols columns (c0, c1) minus those rows
+  const int64_t per = (int64_t)nrows * W + (int64_t)ncols * (H - nrows);
+  const int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (t >= (int64_t)N * Cin * per) return;
+  const int64_t plane = t / per;
+  int64_t k = t - plane * per;
+  const int n = (int)(plane / Cin), ci = (int)(plane - (int64_t)n * Cin);
+  int i, j;
+  if (k < (int64_t)nrows * W) {
+    i = (k < W) ? r0 : r1;
+    j = (int)(k % W);
+  } else {
+    k -= (int64_t)nrows * W;
+    const int cidx = (int)(k / (H - nrows));
+    // the rr-th row that is not one of the full rows
+    const int lo = r0 < r1 ? r0 : r1, hi = r0 < r1 ? r1 : r0;
+    int rr = (int)(k % (H - nrows));
+    if (rr >= lo) ++rr;
+    if (nrows == 2 && rr >= hi) ++rr;
+    i = rr;
+    j = cidx == 0 ? c0 : c1;
+  }
+  const float* dyn = dy + (int64_t)n * Cout * H * W;
+  float add = 0.f;
+  // border rows p in {0, H+1} (every column q of the padded row, corners included)
+  for (int pi = 0; pi < 2; ++pi) {
+    const int p = pi ? H + 1 : 0;
+    if (refl(p - 1, H) != i) continue;
+    for (int qi = 0; qi < 3; ++qi) {
+      const int q = qi == 0 ? 0 : (qi == 1 ? j + 1 : W + 1);
+      if (qi != 1 && refl(q - 1, W) != j) continue;
+      add += border_dxp(dyn, w, Cout, Cin, ci, H, W, p, q);
+    }
+  }
+  // border columns q in {0, W+1} on interior padded rows p = i + 1
+  for (int qi = 0; qi < 2; ++qi) {
+    const int q = qi ? W + 1 : 0;
+    if (refl(q - 1, W) != j) continue;
+    add += border_dxp(dyn, w, Cout, Cin, ci, H, W, i + 1, q);
+  }
+  float* d = dx + ((int64_t)n * Cin + ci) * H * W + (int64_t)i * W + j;
+  *d = *d + add;
+}
+
+// ---- conv weight gradient (3x3, stride 1, zero pad 1) ---------------------------------------
+// Block: 256 threads (2 x 2 waves), tile 64 co x 64 ci, all 9 taps (9 accumulators per wave).
+// K = pixels, walked in row segments of 64 columns: LDS holds dY[px][co] (64 x 65) and
+// X[row][col][ci] (3 x 66 x 65, rows y-1..y+1, columns x0-1..x0+64, zero outside the image);
+// v_mfma_f32_32x32x2_f32 with A = dY (co x px) and B = X shifted by the tap (px x ci).
+constexpr int kWgTile = 64, kWgPx = 64, kWgLd = 65, kWgCols = kWgPx + 2;
+
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(
+    const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part, int N,
+    int Cin, int H, int W, int Cout, int splits, int64_t segs_per_split) {
+  __shared__ float Ys[kWgPx * kWgLd];
+  __shared__ float Xs[3 * kWgCols * kWgLd];
+  const int tilesCi = (Cin + kWgTile - 1) / kWgTile;
+  const int tile = blockIdx.x, split = blockIdx.y;
+  const int co0 = (tile / tilesCi) * kWgTile, ci0 = (tile % tilesCi) * kWgTile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int segW = (W + kWgPx - 1) / kWgPx;
+  const int64_t segs = (int64_t)N * H * segW;
+  const int64_t s0 = (int64_t)split * segs_per_split;
+  const int64_t s1 = s0 + segs_per_split < segs ? s0 + segs_per_split : segs;
+  const int64_t HW = (int64_t)H * W;
+
+  floatx16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  for (int64_t sg = s0; sg < s1; ++sg) {
+    const int xs = (int)(sg % segW);
+    const int64_t ry = sg / segW;
+    const int y = (int)(ry % H), n = (int)(ry / H);
+    const int x0 = xs * kWgPx;
+    // stage dY[n][co0..+63][y][x0..+63] -> Ys[px][co]
+    for (int e = tid; e < kWgTile * kWgPx; e += 256) {
+      const int c = e / kWgPx, px = e % kWgPx;
+      const int co = co0 + c, xx = x0 + px;
+      float v = 0.f;
+      if (co < Cout && xx < W) v = dy[((int64_t)n * Cout + co) * HW + (int64_t)y * W + xx];
+      Ys[px * kWgLd + c] = v;
+    }
+    // stage X[n][ci0..+63][y-1..y+1][x0-1..x0+64] -> Xs[row][col][ci]
+    for (int e = tid; e < kWgTile * 3 * kWgCols; e += 256) {
+      const int c = e / (3 * kWgCols), rc = e % (3 * kWgCols);
+      const int row = rc / kWgCols, col = rc % kWgCols;
+      const int ci = ci0 + c, yy = y - 1 + row, xx = x0 - 1 + col;
+      float v = 0.f;
+      if (ci < Cin && yy >= 0 && yy < H && xx >= 0 && xx < W)
+        v = x[((int64_t)n * Cin + ci) * HW + (int64_t)yy * W + xx];
+      Xs[(row * kWgCols + col) * kWgLd + c] = v;
+    }
+    __syncthreads();
+    const int h = lane >> 5, j = lane & 31;
+#pragma unroll 4
+    for (int kk = 0; kk < kWgPx / 2; ++kk) {
+      const int px = 2 * kk + h;
+      const float a = Ys[px * kWgLd + wm * 32 + j];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int dyy = t / 3, dxx = t % 3;
+        const float b = Xs[(dyy * kWgCols + px + dxx) * kWgLd + wn * 32 + j];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // partial[split][co][ci][9]; accumulator element r of lane: row (co) = (r&3) + 8(r>>2) +
+  // 4h, column (ci) = j
+  const int h = lane >> 5, j = lane & 31;
+  const int ci = ci0 + wn * 32 + j;
+  if (ci >= Cin) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (co >= Cout) continue;
+    float* o = part + (((int64_t)split * Cout + co) * Cin + ci) * 9;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) o[t] = acc[t][r];
+  }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
+                                                           float* __restrict__ dw, int64_t n,
+                                                           int splits) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[(int64_t)k * n + i];
+  dw[i] = s;
+}
+
+// ---- per-channel sums (bias gradient): out[c] = sum_n sum_hw g[n][c][hw] -----------------
+__global__ __launch_bounds__(256) void channel_sum_kernel(const float* __restrict__ g,
+                                                          float* __restrict__ out, int N, int C,
+                                                          int64_t HW) {
+  const int c = blockIdx.x;
+  double s = 0.0;
+  for (int n = 0; n < N; ++n) {
+    const float* p = g + ((int64_t)n * C + c) * HW;
+    for (int64_t i = threadIdx.x; i < HW; i += 256) s += p[i];
+  }
+  s = wave_sum(s);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[c] = (float)(red[0] + red[1] + red[2] + red[3]);
+}
+
+// ---- AdaIN backward ----------------------------------------------------------------------
+// out = nc * sigma_s + mu_s, nc = (c - mu_c) / sigma_c, sigma = sqrt(var_unbiased + eps):
+//   S1 = sum g, S2 = sum g nc (per plane)
+//   dc = (sigma_s / sigma_c) (g - S1 / HW - nc S2 / (HW - 1))
+//   ds = S1 / HW + S2 (s - mu_s) / ((HW - 1) sigma_s)
+// stats = [mean_c | std_c | mean_s | std_s] (planes each).
+__global__ __launch_bounds__(256) void adain_backward_reduce_kernel(
+    const float* __restrict__ g, const float* __restrict__ c, const float* __restrict__ stats,
+    float* __restrict__ sums, int planes, int64_t HW) {
+  const int p = blockIdx.x;
+  const float mc = stats[p], sc = stats[planes + p];
+  const float* gp = g + (int64_t)p * HW;
+  const float* cp = c + (int64_t)p * HW;
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t i = threadIdx.x; i < HW; i += 256) {
+    const float gv = gp[i];
+    const float nc = (cp[i] - mc) / sc;
+    s1 += gv;
+    s2 += (double)gv * nc;
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  __shared__ double red[2][4];
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s1;
+    red[1][threadIdx.x >> 6] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sums[p] = (float)(red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    sums[planes + p] = (float)(red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+__global__ __launch_bounds__(256) void adain_backward_apply_kernel(
+    const float* __restrict__ g, const float* __restrict__ c, const float* __restrict__ s,
+    const float* __restrict__ stats, const float* __restrict__ sums, float* __restrict__ dc,
+    float* __restrict__ ds, int planes, int64_t HW) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)planes * HW) return;
+  const int p = (int)(i / HW);
+  const float mc = stats[p], sc = stats[planes + p];
+  const float ms = stats[2 * planes + p], ss = stats[3 * planes + p];
+  const float S1 = sums[p], S2 = sums[planes + p];
+  const float n = (float)HW, n1 = (float)(HW - 1);
+  const float nc = (c[i] - mc) / sc;
+  dc[i] = (ss / sc) * (g[i] - S1 / n - nc * S2 / n1);
+  ds[i] = S1 / n + S2 * (s[i] - ms) / (n1 * ss);
+}
+
+// ---- losses ------------------------------------------------------------------------------
+// d/dF of w_s * [mse(mu(F), mu_t) + mse(sigma(F), sigma_t)] (+ w_c * mse(F, Fc)) with
+// mse over the (N, C) statistics (mean reduction): per plane
+//   a = w_s 2 (mu - mu_t) / (N C HW),  b = w_s 2 (sigma - sigma_t) / (N C (HW - 1) sigma)
+//   dF = a + b (F - mu) [+ w_c 2 (F - Fc) / (N C HW)]
+// Weights are read from the device (wts[0] = w_s, wts[1] = w_c) so autograd's incoming
+// gradient scales them without a host round trip. acc = 1 adds into out.
+__global__ __launch_bounds__(256) void loss_seed_kernel(
+    const float* __restrict__ F, const float* __restrict__ Fc, const float* __restrict__ st,
+    const float* __restrict__ wts, float* __restrict__ out, int planes, int64_t HW, int acc) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)planes * HW) return;
+  const int p = (int)(i / HW);
+  // st = [mean | std | mean_t | std_t]
+  const float mu = st[p], sd = st[planes + p], mut = st[2 * planes + p], sdt = st[3 * planes + p];
+  const float ws = wts[0];
+  const double nc = (double)planes;
+  const float a = (float)(ws * 2.0 * ((double)mu - mut) / (nc * (double)HW));
+  const float b = (float)(ws * 2.0 * ((double)sd - sdt) / (nc * (double)(HW - 1) * sd));
+  float v = a + b * (F[i] - mu);
+  if (Fc) v += (float)(wts[1] * 2.0 / (nc * (double)HW)) * (F[i] - Fc[i]);
+  out[i] = acc ? out[i] + v : v;
+}
+
+// Deterministic sum of (a - b)^2 over n elements: per-block partials, then one block.
+__global__ __launch_bounds__(256) void sq_diff_partial_kernel(const float* __restrict__ a,
+                                                              const float* __restrict__ b,
+                                                              double* __restrict__ part,
+                                                              int64_t n) {
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double d = (double)a[i] - (double)b[i];
+    s += d * d;
+  }
+  s = wave_sum(s);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void sq_diff_final_kernel(const double* __restrict__ part,
+                                                            int nparts, double scale,
+                                                            float* __restrict__ out) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
+  s = wave_sum(s);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (float)((red[0] + red[1] + red[2] + red[3]) * scale);
+}
+
+}  // namespace rpst
+
+using namespace rpst;
+
+static inline unsigned blocks_for(int64_t n, int per = 256) { return (unsigned)((n + per - 1) / per); }
+
+extern "C" int rpst_conv_weight_flip(const float* w, float* wt, int Cout, int Cin, int ksize,
+                                     rpst_stream_t stream) {
+  RPST_REQUIRE(w && wt && Cout > 0 && Cin > 0 && (ksize == 1 || ksize == 3),
+               "conv_weight_flip: bad args");
+  const int64_t n = (int64_t)Cout * Cin * ksize * ksize;
+  conv_flip_kernel<<<blocks_for(n), 256, 0, as_stream(stream)>>>(w, wt, Cout, Cin, ksize);
+  return launch_status("conv_flip_kernel");
+}
+
+extern "C" int rpst_relu_backward(const float* g, const float* y, float* out, int64_t n,
+                                  rpst_stream_t stream) {
+  RPST_REQUIRE(g && y && out && n > 0, "relu_backward: bad args");
+  relu_backward_kernel<<<blocks_for((n + 3) / 4), 256, 0, as_stream(stream)>>>(g, y, out, n);
+  return launch_status("relu_backward_kernel");
+}
+
+extern "C" int rpst_maxpool2x2_ceil_backward(const float* x, const float* g, float* dx, int N,
+                                             int C, int H, int W, int relu_mask,
+                                             rpst_stream_t stream) {
+  RPST_REQUIRE(x && g && dx && N > 0 && C > 0 && H > 0 && W > 0, "maxpool_backward: bad args");
+  const int64_t n = (int64_t)N * C * ((H + 1) / 2) * ((W + 1) / 2);
+  maxpool2_backward_kernel<<<blocks_for(n), 256, 0, as_stream(stream)>>>(
+      x, g, dx, (int64_t)N * C, H, W, relu_mask);
+  return launch_status("maxpool2_backward_kernel");
+}
+
+extern "C" int rpst_reflect_pad_border_grad(const float* dy, const float* w, float* dx, int N,
+                                            int Cin, int Cout, int H, int W,
+                                            rpst_stream_t stream) {
+  RPST_REQUIRE(dy && w && dx && N > 0 && Cin > 0 && Cout > 0, "reflect_border_grad: bad args");
+  RPST_REQUIRE(H >= 2 && W >= 2, "reflect_border_grad: ReflectionPad2d(1) needs H, W >= 2");
+  const int r0 = 1, r1 = H - 2, c0 = 1, c1 = W - 2;
+  const int nrows = (r0 == r1) ? 1 : 2, ncols = (c0 == c1) ? 1 : 2;
+  const int64_t per = (int64_t)nrows * W + (int64_t)ncols * (H - nrows);
+  const int64_t n = (int64_t)N * Cin * per;
+  reflect_border_grad_kernel<<<blocks_for(n, 64), 64, 0, as_stream(stream)>>>(
+      dy, w, dx, N, Cin, Cout, H, W, nrows, r0, r1, ncols, c0, c1);
+  return launch_status("reflect_border_grad_kernel");
+}
+
+static void wgrad_geometry(int N, int Cin, int H, int W, int Cout, int* splits,
+                           int64_t* segs_per_split) {
+  const int tiles = ((Cout + kWgTile - 1) / kWgTile) * ((Cin + kWgTile - 1) / kWgTile);
+  const int64_t segs = (int64_t)N * H * ((W + kWgPx - 1) / kWgPx);
+  // ~1024 workgroups in all, at least 4 segments each
+  int64_t s = (1024 + tiles - 1) / tiles;
+  if (s > segs / 4) s = segs / 4;
+  if (s < 1) s = 1;
+  *segs_per_split = (segs + s - 1) / s;
+  *splits = (int)((segs + *segs_per_split - 1) / *segs_per_split);
+}
+
+extern "C" size_t rpst_conv_wgrad_workspace_size(int N, int Cin, int H, int W, int Cout) {
+  if (N <= 0 || Cin <= 0 || H <= 0 || W <= 0 || Cout <= 0) return 0;
+  int splits;
+  int64_t sps;
+  wgrad_geometry(N, Cin, H, W, Cout, &splits, &sps);
+  return sizeof(float) * (size_t)splits * Cout * Cin * 9;
+}
+
+extern "C" int rpst_conv_wgrad(const float* x, const float* dy, float* dw, float* db, int N,
+                               int Cin, int H, int W, int Cout, void* workspace,
+                               size_t workspace_bytes, rpst_stream_t stream) {
+  RPST_REQUIRE(x && dy && dw && N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0,
+               "conv_wgrad: bad args");
+  if (!workspace || workspace_bytes < rpst_conv_wgrad_workspace_size(N, Cin, H, W, Cout)) {
+    set_error("conv_wgrad: workspace too small");
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  int splits;
+  int64_t sps;
+  wgrad_geometry(N, Cin, H, W, Cout, &splits, &sps);
+  const int tiles = ((Cout + kWgTile - 1) / kWgTile) * ((Cin + kWgTile - 1) / kWgTile);
+  float* part = static_cast<float*>(workspace);
+  conv_wgrad_kernel<<<dim3(tiles, splits), 256, 0, st>>>(x, dy, part, N, Cin, H, W, Cout,
+                                                         splits, sps);
+  if (int e = launch_status("conv_wgrad_kernel")) return e;
+  const int64_t n = (int64_t)Cout * Cin * 9;
+  wgrad_reduce_kernel<<<blocks_for(n), 256, 0, st>>>(part, dw, n, splits);
+  if (int e = launch_status("wgrad_reduce_kernel")) return e;
+  if (db) {
+    channel_sum_kernel<<<Cout, 256, 0, st>>>(dy, db, N, Cout, (int64_t)H * W);
+    return launch_status("channel_sum_kernel");
+  }
+  return RPST_OK;
+}
+
+extern "C" int rpst_adain_backward(const float* g, const float* c, const float* s,
+                                   const float* stats, float* dc, float* ds, int planes,
+                                   int64_t HW, void* workspace, size_t workspace_bytes,
+                                   rpst_stream_t stream) {
+  RPST_REQUIRE(g && c && s && stats && dc && ds && planes > 0 && HW > 1,
+               "adain_backward: bad args");
+  if (!workspace || workspace_bytes < sizeof(float) * 2 * (size_t)planes) {
+    set_error("adain_backward: workspace too small");
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  float* sums = static_cast<float*>(workspace);
+  adain_backward_reduce_kernel<<<planes, 256, 0, st>>>(g, c, stats, sums, planes, HW);
+  if (int e = launch_status("adain_backward_reduce_kernel")) return e;
+  adain_backward_apply_kernel<<<blocks_for((int64_t)planes * HW), 256, 0, st>>>(
+      g, c, s, stats, sums, dc, ds, planes, HW);
+  return launch_status("adain_backward_apply_kernel");
+}
+
+extern "C" int rpst_style_content_loss_grad(const float* F, const float* Fc, const float* stats,
+                                            const float* weights, float* out, int planes,
+                                            int64_t HW, int accumulate, rpst_stream_t stream) {
+  RPST_REQUIRE(F && stats && weights && out && planes > 0 && HW > 1, "loss_grad: bad args");
+  loss_seed_kernel<<<blocks_for((int64_t)planes * HW), 256, 0, as_stream(stream)>>>(
+      F, Fc, stats, weights, out, planes, HW, accumulate);
+  return launch_status("loss_seed_kernel");
+}
+
+extern "C" size_t rpst_sq_diff_workspace_size(void) { return sizeof(double) * 1024; }
+
+extern "C" int rpst_sq_diff_sum(const float* a, const float* b, int64_t n, double scale,
+                                float* out, void* workspace, size_t workspace_bytes,
+                                rpst_stream_t stream) {
+  RPST_REQUIRE(a && b && out && n > 0, "sq_diff_sum: bad args");
+  if (!workspace || workspace_bytes < rpst_sq_diff_workspace_size()) {
+    set_error("sq_diff_sum: workspace too small");
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  int64_t nb = (n + 255) / 256;
+  const int parts = (int)(nb < 1024 ? nb : 1024);
+  double* part = static_cast<double*>(workspace);
+  sq_diff_partial_kernel<<<parts, 256, 0, st>>>(a, b, part, n);
+  if (int e = launch_status("sq_diff_partial_kernel")) return e;
+  sq_diff_final_kernel<<<1, 256, 0, st>>>(part, parts, scale, out);
+  return launch_status("sq_diff_final_kernel");
+}

@@ -105,9 +105,15 @@ class AdaINRPNet(BaseNet):
                     'decoder': self.rp_decoder.state_dict()}, save_path)
 
     def forward(self, content, style, alpha=1.0):
-        """Loss dict of adain_rp.py:110-138. Inference-only kernels: call it under
-        torch.no_grad() (backward kernels are SURVEY §8(f) rank 2)."""
+        """Loss dict of adain_rp.py:110-138. With autograd enabled and trainable RP
+        parameters the losses come from rpst.autograd (one autograd.Function over the
+        forward and backward kernels), so total_loss.backward() fills the RP encoder /
+        decoder gradients as in train.py:186-189; under no_grad it is evaluated op by op."""
         assert 0 <= alpha <= 1
+        if type(self) is AdaINRPNet and torch.is_grad_enabled() and any(
+                p.requires_grad for p in self.parameters()):
+            from rpst.autograd import adain_rp_losses
+            return adain_rp_losses(self, content, style)
         content_feat, style_feat = encode_both(self.rp_shared_encoder, content, style)
         stylized = self.rp_decoder(AdaIN(content_feat, style_feat))
         down_stylized_feats = self.encode_with_intermediate(stylized)

@@ -43,6 +43,16 @@ SIGNATURES = {
     "rpst_upsample_nearest2x": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "rpst_sanet_attention_workspace_size": (_SZ, [_I, _I]),
     "rpst_sanet_attention": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
+    "rpst_conv_weight_flip": (_I, [_P, _P, _I, _I, _I, _P]),
+    "rpst_relu_backward": (_I, [_P, _P, _P, _I64, _P]),
+    "rpst_maxpool2x2_ceil_backward": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "rpst_reflect_pad_border_grad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "rpst_conv_wgrad_workspace_size": (_SZ, [_I, _I, _I, _I, _I]),
+    "rpst_conv_wgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
+    "rpst_adain_backward": (_I, [_P, _P, _P, _P, _P, _P, _I, _I64, _P, _SZ, _P]),
+    "rpst_style_content_loss_grad": (_I, [_P, _P, _P, _P, _P, _I, _I64, _I, _P]),
+    "rpst_sq_diff_workspace_size": (_SZ, []),
+    "rpst_sq_diff_sum": (_I, [_P, _P, _I64, _D, _P, _P, _SZ, _P]),
     "rpst_u8hwc_to_f32nchw": (_I, [_P, _P, _I, _I, _I, _P]),
     "rpst_f32nchw_to_u8_tile": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_cosine_affinity_workspace_size": (_SZ, [_I, _I, _I]),

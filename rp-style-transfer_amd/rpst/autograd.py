@@ -1,0 +1,249 @@
+"""Training step of AdaINRPNet on the MI355X kernels.
+
+AdaINRPNet.forward (network/adain_rp.py:110-138) returns the loss dict and total_loss;
+train.py:186-189 then calls total_loss.backward() and optimizer.step(). Here the whole
+loss graph is ONE torch.autograd.Function: its forward runs the forward kernels and keeps
+the activations the backward needs, its backward runs the backward kernels
+(csrc/rpst_train.hip) and returns the gradients of the RP encoder / decoder parameters,
+so an unchanged train loop (backward + Adam) trains on the HIP path.
+
+Forward (kept activations):
+  RP encoder over [content; style] (2N)  -> every layer output (ReLU masks + wgrad inputs)
+  AdaIN (materialised: it is the decoder's first wgrad input), stats of both halves
+  RP decoder                              -> every layer output; stylized = last
+  VGG relu1_1..relu4_1 over stylized      -> every conv input / output (dgrad masks,
+                                             max-pool argmax)
+  VGG over [style; content] (constants)   -> the tap features and their statistics
+Backward:
+  loss seeds at the four taps (style: mean/std terms; content at relu4_1)
+  VGG: ReLU backward, dgrad conv (flip-transposed weights, zero pad) + reflect border
+       fold, max-pool backward                      -> d stylized (no VGG weight grads)
+  decoder: ReLU backward, wgrad + bias grad, dgrad  -> d AdaIN output
+  AdaIN backward                                    -> d content_feat, d style_feat
+  encoder (2N batch): ReLU backward, wgrad, dgrad   -> parameter gradients
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _lib, ops, plan
+from .ops import _stream
+
+
+def _ws(nbytes: int, like: torch.Tensor) -> torch.Tensor:
+    return torch.empty(max(nbytes, 16), device=like.device, dtype=torch.uint8)
+
+
+def flip_packed_weight(conv: nn.Conv2d) -> torch.Tensor:
+    """Packed flip-transposed weights (Cin, Cout, k, k) of conv for its dgrad, cached on the
+    module like plan.packed_weight (refreshed after optimizer steps)."""
+    w = conv.weight
+    key = (w.device, w.data_ptr(), w._version)
+    cached = getattr(conv, "_rpst_flip_packed", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    with torch.no_grad():
+        wd = w.detach().contiguous()
+        cout, cin, k, _ = wd.shape
+        wt = torch.empty((cin, cout, k, k), device=wd.device, dtype=torch.float32)
+        _lib.call("rpst_conv_weight_flip", wd.data_ptr(), wt.data_ptr(), cout, cin, k,
+                  _stream(wd))
+        packed = ops.pack_conv_weight(wt)
+    conv._rpst_flip_packed = (key, packed)
+    return packed
+
+
+def relu_backward(g: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    out = torch.empty_like(g)
+    _lib.call("rpst_relu_backward", g.data_ptr(), y.data_ptr(), out.data_ptr(), g.numel(),
+              _stream(g))
+    return out
+
+
+def conv_dgrad(g: torch.Tensor, step: plan.ConvStep) -> torch.Tensor:
+    """Gradient at the conv's input (after its input operator) from g at its output
+    (pre-activation)."""
+    c = step.conv
+    k = c.kernel_size[0]
+    dx = ops.conv2d(g, flip_packed_weight(c), None, c.in_channels, k, pad=ops.PAD_ZERO)
+    if k == 3 and step.pad == ops.PAD_REFLECT:
+        n, _, h, w = g.shape
+        wd = c.weight.detach().contiguous()
+        _lib.call("rpst_reflect_pad_border_grad", g.data_ptr(), wd.data_ptr(), dx.data_ptr(),
+                  n, c.in_channels, c.out_channels, h, w, _stream(g))
+    return dx
+
+
+def maxpool_backward(x: torch.Tensor, g: torch.Tensor, relu_mask: bool) -> torch.Tensor:
+    n, c, h, w = x.shape
+    dx = torch.empty_like(x)
+    _lib.call("rpst_maxpool2x2_ceil_backward", x.data_ptr(), g.data_ptr(), dx.data_ptr(), n, c,
+              h, w, int(relu_mask), _stream(x))
+    return dx
+
+
+def conv_wgrad(x: torch.Tensor, g: torch.Tensor, conv: nn.Conv2d):
+    n, cin, h, w = x.shape
+    cout = conv.out_channels
+    assert conv.kernel_size == (3, 3) and tuple(g.shape) == (n, cout, h, w)
+    dw = torch.empty_like(conv.weight, memory_format=torch.contiguous_format)
+    db = torch.empty_like(conv.bias) if conv.bias is not None else None
+    nbytes = _lib.load().rpst_conv_wgrad_workspace_size(n, cin, h, w, cout)
+    ws = _ws(nbytes, x)
+    with ops._traced(f"wgrad3x3 {cin}->{cout} {h}x{w} N{n} op0",
+                     2.0 * n * cout * cin * 9 * h * w, 4.0 * (x.numel() + g.numel())):
+        _lib.call("rpst_conv_wgrad", x.data_ptr(), g.data_ptr(), dw.data_ptr(),
+                  None if db is None else db.data_ptr(), n, cin, h, w, cout, ws.data_ptr(),
+                  nbytes, _stream(x))
+    return dw, db
+
+
+def sq_diff_mean(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """nn.MSELoss()(a, b) (mean reduction) as a 0-dim device tensor."""
+    out = torch.empty((), device=a.device, dtype=torch.float32)
+    nbytes = _lib.load().rpst_sq_diff_workspace_size()
+    ws = _ws(nbytes, a)
+    _lib.call("rpst_sq_diff_sum", a.data_ptr(), b.data_ptr(), a.numel(), 1.0 / a.numel(),
+              out.data_ptr(), ws.data_ptr(), nbytes, _stream(a))
+    return out
+
+
+def _run_steps_saving(steps, x):
+    """Run conv steps keeping (input, output) of each."""
+    saved = []
+    for s in steps:
+        assert isinstance(s, plan.ConvStep)
+        y = plan.run_conv_step(s, x)
+        saved.append((x, y))
+        x = y
+    return x, saved
+
+
+def _rp_backward(steps, saved, g, grads: Dict[int, torch.Tensor], need_input_grad: bool):
+    """Backward through an RP stack (zero-padded 3x3 convs + ReLU)."""
+    for k in range(len(steps) - 1, -1, -1):
+        s = steps[k]
+        x_in, y = saved[k]
+        if s.relu:
+            g = relu_backward(g, y)
+        dw, db = conv_wgrad(x_in, g, s.conv)
+        grads[id(s.conv.weight)] = dw
+        if db is not None:
+            grads[id(s.conv.bias)] = db
+        if k > 0 or need_input_grad:
+            g = conv_dgrad(g, s)
+    return g
+
+
+class _AdaINRPStep(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, content, style, model, cw, sw, *params):
+        n = content.shape[0]
+        enc_steps = plan.compile_layers(model.rp_shared_encoder.children())
+        dec_steps = plan.compile_layers(model.rp_decoder.children())
+        feats, enc_saved = _run_steps_saving(enc_steps, torch.cat([content, style], dim=0))
+        cf, sf = feats[:n], feats[n:]
+        mc, sc = ops.calc_mean_std(cf)
+        ms, ss = ops.calc_mean_std(sf)
+        t = ops.adaptive_instance_normalization(cf, sf)
+        stylized, dec_saved = _run_steps_saving(dec_steps, t)
+        # VGG relu1_1..relu4_1 of the stylized batch (kept) and of [style; content]
+        vgg_steps, vgg_saved, taps, x = [], [], [], stylized
+        for i in range(4):
+            st = plan.compile_layers(getattr(model, f"enc_{i + 1}").children())
+            x, sv = _run_steps_saving(st, x)
+            vgg_steps += st
+            vgg_saved += sv
+            taps.append(len(vgg_steps) - 1)
+        ref = torch.cat([style, content], dim=0)
+        targets = []
+        for i in range(4):
+            ref = getattr(model, f"enc_{i + 1}")(ref)
+            targets.append(ref)
+        # losses (calc_style_loss on the four taps, calc_content_loss on relu4_1)
+        stats, loss_s = [], []
+        for i, k in enumerate(taps):
+            F = vgg_saved[k][1]
+            mu, sd = ops.calc_mean_std(F)
+            mut, sdt = ops.calc_mean_std(targets[i][:n])
+            stats.append(torch.cat([mu.reshape(-1), sd.reshape(-1), mut.reshape(-1),
+                                    sdt.reshape(-1)]))
+            loss_s.append(sq_diff_mean(mu, mut) + sq_diff_mean(sd, sdt))
+        ls = loss_s[0] + loss_s[1] + loss_s[2] + loss_s[3]
+        content4 = targets[3][n:].contiguous()
+        lc = sq_diff_mean(vgg_saved[taps[3]][1], content4)
+        total = cw * lc + sw * ls
+        ctx.model, ctx.cw, ctx.sw, ctx.n = model, cw, sw, n
+        ctx.enc_steps, ctx.dec_steps, ctx.vgg_steps = enc_steps, dec_steps, vgg_steps
+        ctx.enc_saved, ctx.dec_saved, ctx.vgg_saved = enc_saved, dec_saved, vgg_saved
+        ctx.taps, ctx.stats, ctx.content4 = taps, stats, content4
+        ctx.adain = (cf, sf, torch.cat([mc.reshape(-1), sc.reshape(-1), ms.reshape(-1),
+                                        ss.reshape(-1)]))
+        ctx.params = params
+        return total, ls, lc
+
+    @staticmethod
+    def backward(ctx, g_total, g_ls, g_lc):
+        dev = ctx.content4.device
+        zero = torch.zeros((), device=dev)
+        g_total = zero if g_total is None else g_total
+        w_s = g_total * ctx.sw + (zero if g_ls is None else g_ls)
+        w_c = g_total * ctx.cw + (zero if g_lc is None else g_lc)
+        wts = torch.stack([w_s, w_c]).to(torch.float32).contiguous()
+        # ---- VGG (frozen): loss seeds at the taps, back to d stylized
+        vs, vsv, taps = ctx.vgg_steps, ctx.vgg_saved, ctx.taps
+        g = None
+        for k in range(len(vs) - 1, -1, -1):
+            x_in, y = vsv[k]
+            if k in taps:
+                i = taps.index(k)
+                planes = y.shape[0] * y.shape[1]
+                hw = y.shape[2] * y.shape[3]
+                if g is None:
+                    g = torch.empty_like(y)
+                acc = int(i != 3)
+                _lib.call("rpst_style_content_loss_grad", y.data_ptr(),
+                          ctx.content4.data_ptr() if i == 3 else None, ctx.stats[i].data_ptr(),
+                          wts.data_ptr(), g.data_ptr(), planes, hw, acc, _stream(y))
+            s = vs[k]
+            if s.relu:
+                g = relu_backward(g, y)
+            g = conv_dgrad(g, s)
+            if s.in_op == ops.IN_MAXPOOL2:
+                g = maxpool_backward(x_in, g, relu_mask=False)
+            elif s.in_op != ops.IN_NONE:
+                raise NotImplementedError("rpst autograd: VGG input operator")
+        # ---- RP decoder and AdaIN
+        grads: Dict[int, torch.Tensor] = {}
+        g = _rp_backward(ctx.dec_steps, ctx.dec_saved, g, grads, need_input_grad=True)
+        cf, sf, st = ctx.adain
+        dc, ds = torch.empty_like(cf), torch.empty_like(sf)
+        planes = cf.shape[0] * cf.shape[1]
+        hw = cf.shape[2] * cf.shape[3]
+        ws = torch.empty(2 * planes, device=dev, dtype=torch.float32)
+        _lib.call("rpst_adain_backward", g.data_ptr(), cf.data_ptr(), sf.data_ptr(), st.data_ptr(),
+                  dc.data_ptr(), ds.data_ptr(), planes, hw, ws.data_ptr(), ws.numel() * 4,
+                  _stream(g))
+        # ---- RP encoder over the [content; style] batch: weight grads sum both halves
+        _rp_backward(ctx.enc_steps, ctx.enc_saved, torch.cat([dc, ds], dim=0), grads,
+                     need_input_grad=False)
+        out = [grads.get(id(p)) for p in ctx.params]
+        ctx.enc_saved = ctx.dec_saved = ctx.vgg_saved = None
+        return (None, None, None, None, None, *out)
+
+
+def adain_rp_losses(model, content: torch.Tensor, style: torch.Tensor
+                    ) -> Tuple[Dict[str, torch.Tensor], torch.Tensor]:
+    """AdaINRPNet.forward with autograd: ({'style_loss', 'content_loss', 'total_loss'},
+    total_loss), differentiable w.r.t. the RP encoder / decoder parameters."""
+    ops._check(content, style)
+    params: List[torch.Tensor] = (list(model.rp_shared_encoder.parameters()) +
+                                  list(model.rp_decoder.parameters()))
+    cw = float(model.config['content_weight'])
+    sw = float(model.config['style_weight'])
+    total, ls, lc = _AdaINRPStep.apply(content.detach().contiguous(),
+                                       style.detach().contiguous(), model, cw, sw, *params)
+    return {'style_loss': ls, 'content_loss': lc, 'total_loss': total}, total

@@ -4,6 +4,7 @@ The kernels need a GPU, so these tests check the data path around them: every im
 processed exactly once, slices are contiguous and ordered, the host gather reassembles
 the batch bit-exactly, and bench.py's timing reduction takes the max over ranks.
 """
+import copy
 import os
 import socket
 
@@ -71,3 +72,36 @@ def test_gloo_shard_and_gather(world, n):
     ok, tmax = q.get(timeout=60)
     assert ok
     assert tmax == float(world)
+
+
+def _grad_worker(rank, world, port, q):
+    from rpst.shard import GradientAllReduce
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # data-parallel training: same weights, a different batch per rank; the averaged
+        # gradient equals the gradient of the mean loss over the union of the batches
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.ReLU(), torch.nn.Linear(5, 2))
+        frozen = torch.nn.Parameter(torch.ones(3), requires_grad=False)
+        xs = torch.rand(world, 4, 6, generator=torch.Generator().manual_seed(1))
+        net(xs[rank]).pow(2).mean().backward()
+        GradientAllReduce(list(net.parameters()) + [frozen])()
+        if rank == 0:
+            ref = copy.deepcopy(net)
+            ref.zero_grad()
+            torch.stack([ref(xs[r]).pow(2).mean() for r in range(world)]).mean().backward()
+            ok = all(torch.allclose(a.grad, b.grad, rtol=1e-6, atol=1e-7)
+                     for a, b in zip(net.parameters(), ref.parameters()))
+            q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_gradient_allreduce(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.spawn(_grad_worker, args=(world, _free_port(), q), nprocs=world, join=True)
+    assert q.get(timeout=60)
