@@ -8,7 +8,7 @@
 //   conv wgrad        conv_wgrad_kernel: implicit GEMM dW[co][ci][tap] = sum over (n,y,x) of
 //                       dY[n][co][y][x] X[n][ci][y+dy][x+dx] on fp32 MFMA, split over K
 //                       (pixels) with a fixed-order reduction (wgrad_reduce_kernel)
-//   bias grad         channel_sum_kernel
+//   bias grad         reduced by the wgrad kernel's first ci-tile blocks from their dY tiles
 //   ReLU / max-pool   relu_backward_kernel, maxpool2_backward_kernel (argmax = first max in
 //                       window order, NaN wins, as ATen's max_pool2d)
 //   AdaIN             adain_backward_reduce_kernel + adain_backward_apply_kernel
@@ -175,71 +175,147 @@ __global__ __launch_bounds__(64) void reflect_border_grad_kernel(
 // K = pixels, walked in row segments of 64 columns: LDS holds dY[px][co] (64 x 65) and
 // X[row][col][ci] (3 x 66 x 65, rows y-1..y+1, columns x0-1..x0+64, zero outside the image);
 // v_mfma_f32_32x32x2_f32 with A = dY (co x px) and B = X shifted by the tap (px x ci).
+// Staging: thread -> (channel c = tid / 4, quarter q = tid % 4 of the 64 columns); the next
+// segment's 16-B buffer loads (dY 4, X 12, X halo 3 per thread) are issued into registers
+// before the current segment's MFMAs and written to LDS after them (one load latency per
+// segment, hidden behind 288 MFMAs per wave). Rows / channels outside the image read the
+// out-of-range offset (0), columns at or past W are masked. Blocks of the first ci tile also
+// reduce the bias gradient (sum of dY over their pixels) from the staged dY tile.
 constexpr int kWgTile = 64, kWgPx = 64, kWgLd = 65, kWgCols = kWgPx + 2;
+constexpr unsigned kWgOOB = 0x80000000u;
 
+typedef unsigned wg_u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool VEC>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(
-    const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part, int N,
-    int Cin, int H, int W, int Cout, int splits, int64_t segs_per_split) {
+    const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part,
+    float* __restrict__ bpart, int N, int Cin, int H, int W, int Cout, int64_t segs_per_split) {
   __shared__ float Ys[kWgPx * kWgLd];
   __shared__ float Xs[3 * kWgCols * kWgLd];
   const int tilesCi = (Cin + kWgTile - 1) / kWgTile;
   const int tile = blockIdx.x, split = blockIdx.y;
   const int co0 = (tile / tilesCi) * kWgTile, ci0 = (tile % tilesCi) * kWgTile;
+  const bool bias_tile = bpart != nullptr && (tile % tilesCi) == 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, j = lane & 31;
   const int segW = (W + kWgPx - 1) / kWgPx;
   const int64_t segs = (int64_t)N * H * segW;
   const int64_t s0 = (int64_t)split * segs_per_split;
   const int64_t s1 = s0 + segs_per_split < segs ? s0 + segs_per_split : segs;
-  const int64_t HW = (int64_t)H * W;
+  const unsigned HW = (unsigned)(H * W);
+  const int c = tid >> 2, q = tid & 3;
+  const bool co_ok = co0 + c < Cout, ci_ok = ci0 + c < Cin;
 
   floatx16 acc[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float bacc = 0.f;
 
-  for (int64_t sg = s0; sg < s1; ++sg) {
-    const int xs = (int)(sg % segW);
-    const int64_t ry = sg / segW;
-    const int y = (int)(ry % H), n = (int)(ry / H);
+  wg_u32x4 ry[4], rx[3][4];
+  float rh[3];
+  // issue the loads of segment sg into registers (branch-free buffer loads)
+  auto load = [&](int64_t sg) {
+    const bool live = sg < s1;
+    const int64_t sgc = live ? sg : s0;
+    const int xs = (int)(sgc % segW);
+    const int64_t ry_ = sgc / segW;
+    const int y = (int)(ry_ % H), n = (int)(ry_ / H);
     const int x0 = xs * kWgPx;
-    // stage dY[n][co0..+63][y][x0..+63] -> Ys[px][co]
-    for (int e = tid; e < kWgTile * kWgPx; e += 256) {
-      const int c = e / kWgPx, px = e % kWgPx;
-      const int co = co0 + c, xx = x0 + px;
-      float v = 0.f;
-      if (co < Cout && xx < W) v = dy[((int64_t)n * Cout + co) * HW + (int64_t)y * W + xx];
-      Ys[px * kWgLd + c] = v;
+    const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(dy + (int64_t)n * Cout * HW), (short)0, (int)(Cout * HW * 4u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rxx = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(x + (int64_t)n * Cin * HW), (short)0, (int)(Cin * HW * 4u), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int xx = x0 + q * 16 + 4 * k;
+      const bool ok = live && co_ok && (VEC ? xx < W : true);
+      const unsigned off = ok ? ((unsigned)(co0 + c) * HW + (unsigned)y * W + xx) * 4u : kWgOOB;
+      if (VEC) {
+        ry[k] = __builtin_amdgcn_raw_buffer_load_b128(rdy, (int)off, 0, 0);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool oe = ok && xx + e < W;
+          ry[k][e] = __builtin_amdgcn_raw_buffer_load_b32(rdy, (int)(oe ? off + 4u * e : kWgOOB), 0, 0);
+        }
+      }
     }
-    // stage X[n][ci0..+63][y-1..y+1][x0-1..x0+64] -> Xs[row][col][ci]
-    for (int e = tid; e < kWgTile * 3 * kWgCols; e += 256) {
-      const int c = e / (3 * kWgCols), rc = e % (3 * kWgCols);
-      const int row = rc / kWgCols, col = rc % kWgCols;
-      const int ci = ci0 + c, yy = y - 1 + row, xx = x0 - 1 + col;
-      float v = 0.f;
-      if (ci < Cin && yy >= 0 && yy < H && xx >= 0 && xx < W)
-        v = x[((int64_t)n * Cin + ci) * HW + (int64_t)yy * W + xx];
-      Xs[(row * kWgCols + col) * kWgLd + c] = v;
+#pragma unroll
+    for (int row = 0; row < 3; ++row) {
+      const int yy = y - 1 + row;
+      const bool rok = live && ci_ok && yy >= 0 && yy < H;
+      const unsigned rbase = ((unsigned)(ci0 + c) * HW + (unsigned)(rok ? yy : 0) * W) * 4u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int xx = x0 + q * 16 + 4 * k;
+        const bool ok = rok && (VEC ? xx < W : true);
+        if (VEC) {
+          rx[row][k] = __builtin_amdgcn_raw_buffer_load_b128(
+              rxx, (int)(ok ? rbase + 4u * xx : kWgOOB), 0, 0);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool oe = ok && xx + e < W;
+            rx[row][k][e] = __builtin_amdgcn_raw_buffer_load_b32(
+                rxx, (int)(oe ? rbase + 4u * (xx + e) : kWgOOB), 0, 0);
+          }
+        }
+      }
+      // halo: column x0 - 1 (q == 0) or x0 + 64 (q == 3)
+      const int hx = q == 0 ? x0 - 1 : x0 + kWgPx;
+      const bool hok = rok && (q == 0 || q == 3) && hx >= 0 && hx < W;
+      rh[row] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(rxx, (int)(hok ? rbase + 4u * hx : kWgOOB), 0, 0));
     }
+  };
+  // columns at or past W were loaded as 0 (VEC: whole float4 out; scalar: per element)
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Ys[(q * 16 + 4 * k + e) * kWgLd + c] = __uint_as_float(ry[k][e]);
+#pragma unroll
+    for (int row = 0; row < 3; ++row) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          Xs[(row * kWgCols + 1 + q * 16 + 4 * k + e) * kWgLd + c] = __uint_as_float(rx[row][k][e]);
+      if (q == 0) Xs[(row * kWgCols) * kWgLd + c] = rh[row];
+      if (q == 3) Xs[(row * kWgCols + kWgCols - 1) * kWgLd + c] = rh[row];
+    }
+  };
+
+  load(s0);
+  for (int64_t sg = s0; sg < s1; ++sg) {
+    store();
     __syncthreads();
-    const int h = lane >> 5, j = lane & 31;
+    load(sg + 1);  // in flight during this segment's MFMAs
+    if (bias_tile && wave == 0) {
+      float t = 0.f;
+      for (int px = 0; px < kWgPx; ++px) t += Ys[px * kWgLd + lane];
+      bacc += t;
+    }
 #pragma unroll 4
     for (int kk = 0; kk < kWgPx / 2; ++kk) {
       const int px = 2 * kk + h;
-      const float a = Ys[px * kWgLd + wm * 32 + j];
+      const float av = Ys[px * kWgLd + wm * 32 + j];
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int dyy = t / 3, dxx = t % 3;
-        const float b = Xs[(dyy * kWgCols + px + dxx) * kWgLd + wn * 32 + j];
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+        const float bv = Xs[(dyy * kWgCols + px + dxx) * kWgLd + wn * 32 + j];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
       }
     }
     __syncthreads();
   }
+  if (bias_tile && wave == 0 && co0 + lane < Cout)
+    bpart[(int64_t)split * Cout + co0 + lane] = bacc;
   // partial[split][co][ci][9]; accumulator element r of lane: row (co) = (r&3) + 8(r>>2) +
   // 4h, column (ci) = j
-  const int h = lane >> 5, j = lane & 31;
   const int ci = ci0 + wn * 32 + j;
   if (ci >= Cin) return;
 #pragma unroll
@@ -260,23 +336,6 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   float s = 0.f;
   for (int k = 0; k < splits; ++k) s += part[(int64_t)k * n + i];
   dw[i] = s;
-}
-
-// ---- per-channel sums (bias gradient): out[c] = sum_n sum_hw g[n][c][hw] -----------------
-__global__ __launch_bounds__(256) void channel_sum_kernel(const float* __restrict__ g,
-                                                          float* __restrict__ out, int N, int C,
-                                                          int64_t HW) {
-  const int c = blockIdx.x;
-  double s = 0.0;
-  for (int n = 0; n < N; ++n) {
-    const float* p = g + ((int64_t)n * C + c) * HW;
-    for (int64_t i = threadIdx.x; i < HW; i += 256) s += p[i];
-  }
-  s = wave_sum(s);
-  __shared__ double red[4];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) out[c] = (float)(red[0] + red[1] + red[2] + red[3]);
 }
 
 // ---- AdaIN backward ----------------------------------------------------------------------
@@ -445,7 +504,7 @@ extern "C" size_t rpst_conv_wgrad_workspace_size(int N, int Cin, int H, int W, i
   int splits;
   int64_t sps;
   wgrad_geometry(N, Cin, H, W, Cout, &splits, &sps);
-  return sizeof(float) * (size_t)splits * Cout * Cin * 9;
+  return sizeof(float) * (size_t)splits * Cout * ((size_t)Cin * 9 + 1);
 }
 
 extern "C" int rpst_conv_wgrad(const float* x, const float* dy, float* dw, float* db, int N,
@@ -463,15 +522,23 @@ extern "C" int rpst_conv_wgrad(const float* x, const float* dy, float* dw, float
   wgrad_geometry(N, Cin, H, W, Cout, &splits, &sps);
   const int tiles = ((Cout + kWgTile - 1) / kWgTile) * ((Cin + kWgTile - 1) / kWgTile);
   float* part = static_cast<float*>(workspace);
-  conv_wgrad_kernel<<<dim3(tiles, splits), 256, 0, st>>>(x, dy, part, N, Cin, H, W, Cout,
-                                                         splits, sps);
+  float* bpart = part + (size_t)splits * Cout * Cin * 9;
+  RPST_REQUIRE((int64_t)(Cout > Cin ? Cout : Cin) * H * W * 4 < (1LL << 31),
+               "conv_wgrad: one image's tensor exceeds 2 GiB");
+  const bool vec = (W % 4) == 0;
+  if (vec)
+    conv_wgrad_kernel<true><<<dim3(tiles, splits), 256, 0, st>>>(
+        x, dy, part, db ? bpart : nullptr, N, Cin, H, W, Cout, sps);
+  else
+    conv_wgrad_kernel<false><<<dim3(tiles, splits), 256, 0, st>>>(
+        x, dy, part, db ? bpart : nullptr, N, Cin, H, W, Cout, sps);
   if (int e = launch_status("conv_wgrad_kernel")) return e;
   const int64_t n = (int64_t)Cout * Cin * 9;
   wgrad_reduce_kernel<<<blocks_for(n), 256, 0, st>>>(part, dw, n, splits);
   if (int e = launch_status("wgrad_reduce_kernel")) return e;
   if (db) {
-    channel_sum_kernel<<<Cout, 256, 0, st>>>(dy, db, N, Cout, (int64_t)H * W);
-    return launch_status("channel_sum_kernel");
+    wgrad_reduce_kernel<<<blocks_for(Cout), 256, 0, st>>>(bpart, db, Cout, splits);
+    return launch_status("wgrad_reduce_kernel(bias)");
   }
   return RPST_OK;
 }

@@ -1,0 +1,5 @@
+set -e
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 300 python bench.py --model train --no-cpu-baseline > gpurun_out/bench_train.json 2> gpurun_out/bench_train.err
