@@ -214,9 +214,12 @@ int rpst_maxpool2x2_ceil_backward(const float* x, const float* g, float* dx, int
                                   int H, int W, int relu_mask, rpst_stream_t stream);
 /* ReflectionPad2d(1) + conv3x3 backward, border part: dy (N,Cout,H,W), w (Cout,Cin,3,3);
  * dx (N,Cin,H,W) holds the zero-padded dgrad and receives the padded border's gradient
- * folded onto the rows / columns it reflects. H, W >= 2. */
+ * folded onto the rows / columns it reflects. H, W >= 2.
+ * Workspace: rpst_reflect_pad_border_grad_workspace_size(N, Cin, H, W). */
+size_t rpst_reflect_pad_border_grad_workspace_size(int N, int Cin, int H, int W);
 int rpst_reflect_pad_border_grad(const float* dy, const float* w, float* dx, int N, int Cin,
-                                 int Cout, int H, int W, rpst_stream_t stream);
+                                 int Cout, int H, int W, void* workspace, size_t workspace_bytes,
+                                 rpst_stream_t stream);
 /* conv3x3 (stride 1, zero pad 1) weight / bias gradient: x (N,Cin,H,W) the conv input, dy
  * (N,Cout,H,W) the gradient at its output -> dw (Cout,Cin,3,3), db (Cout) (db may be NULL).
  * Workspace: rpst_conv_wgrad_workspace_size(N, Cin, H, W, Cout). */

@@ -4,7 +4,7 @@
 //   conv dgrad        = the forward conv kernel on flip-transposed weights (conv_flip_kernel
 //                       here, packing by rpst_conv2d_pack); reflect-padded convs (the frozen
 //                       VGG) add the padded border's gradient folded back onto the rows /
-//                       columns it reflects (reflect_border_grad_kernel)
+//                       columns it reflects (reflect_ring_kernel + reflect_fold_kernel)
 //   conv wgrad        conv_wgrad_kernel: implicit GEMM dW[co][ci][tap] = sum over (n,y,x) of
 //                       dY[n][co][y][x] X[n][ci][y+dy][x+dx] on fp32 MFMA, split over K
 //                       (pixels) with a fixed-order reduction (wgrad_reduce_kernel)
@@ -93,46 +93,105 @@ __global__ __launch_bounds__(256) void maxpool2_backward_kernel(
 
 // ---- reflect-pad border gradient ---------------------------------------------------------
 // Forward: Y = conv3x3_valid(ReflectionPad2d(1)(X)). The zero-padded dgrad conv gives the
-// gradient of the padded input's interior, dXp[1..H][1..W]; this adds the border entries
-// dXp[p][q] (p in {0, H+1} or q in {0, W+1}) to the X element they reflect: row 0 -> 1,
-// row H+1 -> H-2, column 0 -> 1, column W+1 -> W-2 (corners both ways). One thread per
-// target element (rows {1, H-2} fully, columns {1, W-2} on the other rows): every element
-// is updated by exactly one thread, in a fixed order.
+// gradient of the padded input's interior, dXp[1..H][1..W]; the padded border ("ring":
+// rows 0 and H+1, columns 0 and W+1) is added to the X element it reflects: row 0 -> 1,
+// row H+1 -> H-2, column 0 -> 1, column W+1 -> W-2 (corners both ways).
+//   reflect_ring_kernel: dXp on the ring (four 1-D convolutions, tiled below);
+//   reflect_fold_kernel: one thread per target element (rows {1, H-2} fully, columns
+//     {1, W-2} on the other rows) sums its ring entries in a fixed order and adds them.
+// ring layout per plane: [top row q = 0..W+1 | bottom row q = 0..W+1 | left column p = 1..H |
+// right column p = 1..H].
 __device__ __forceinline__ int refl(int t, int n) { return t < 0 ? -t : (t >= n ? 2 * n - 2 - t : t); }
 
-__device__ float border_dxp(const float* __restrict__ dy, const float* __restrict__ w,
-                           int Cout, int Cin, int ci, int H, int W, int p, int q) {
-  // dXp[p][q] = sum_co sum_{kh,kw} dY[co][p-kh][q-kw] W[co][ci][kh][kw]
-  float acc = 0.f;
+// The ring is four 1-D convolutions over the image's border lines: for side 0/1 (padded
+// row 0 / H+1) the line is dY's row 0 / H-1 and the taps are the weights' row 0 / 2; for side
+// 2/3 (padded column 0 / W+1) the line is dY's column 0 / W-1 and the taps the weights'
+// column 0 / 2:  ring[ci][u] = sum_co sum_k line[co][u - k] tap[co][ci][k].
+// Block = (64 ring positions) x (64 input channels) of one image and side; co in chunks of
+// 16 staged in LDS (line segment with its 2-element halo, taps transposed ci-contiguous);
+// each thread accumulates 4 ci x 4 positions.
+__global__ __launch_bounds__(256) void reflect_ring_kernel(
+    const float* __restrict__ dy, const float* __restrict__ w, float* __restrict__ ring, int N,
+    int Cin, int Cout, int H, int W) {
+  constexpr int CC = 16;
+  __shared__ float line[CC][64 + 2];
+  __shared__ __attribute__((aligned(16))) float taps[CC][3][64];
+  const int side = blockIdx.z & 3, n = blockIdx.z >> 2;
+  const bool row = side < 2;
+  const int L = row ? W : H;                  // line length
+  const int U = row ? W + 2 : H;              // outputs on this side
+  const int u_first = row ? 0 : 1;            // u of output index 0
+  const int u0 = blockIdx.x * 64 + u_first;   // first u of the block
+  const int ci0 = blockIdx.y * 64;
+  const int tid = threadIdx.x, cg = tid >> 4, ug = tid & 15;
   const int64_t HW = (int64_t)H * W;
-  for (int co = 0; co < Cout; ++co) {
-    const float* dyc = dy + co * HW;
-    const float* wc = w + ((int64_t)co * Cin + ci) * 9;
+  const float* dyn = dy + (int64_t)n * Cout * HW;
+  float acc[4][4] = {};
+  for (int c0 = 0; c0 < Cout; c0 += CC) {
+    // line[co][t'] = line value at t = u0 - 2 + t' (0 outside [0, L))
+    for (int e = tid; e < CC * 66; e += 256) {
+      const int cc = e / 66, tt = e - cc * 66, t = u0 - 2 + tt, co = c0 + cc;
+      float v = 0.f;
+      if (co < Cout && t >= 0 && t < L) {
+        const int64_t off = row ? (int64_t)(side == 0 ? 0 : H - 1) * W + t
+                                : (int64_t)t * W + (side == 2 ? 0 : W - 1);
+        v = dyn[co * HW + off];
+      }
+      line[cc][tt] = v;
+    }
+    for (int e = tid; e < CC * 3 * 64; e += 256) {
+      const int cc = e / 192, r = e - cc * 192, k = r / 64, c = r - k * 64;
+      const int co = c0 + cc, ci = ci0 + c;
+      float v = 0.f;
+      if (co < Cout && ci < Cin) {
+        const int kh = row ? (side == 0 ? 0 : 2) : k, kw = row ? k : (side == 2 ? 0 : 2);
+        v = w[((int64_t)co * Cin + ci) * 9 + kh * 3 + kw];
+      }
+      taps[cc][k][c] = v;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int cc = 0; cc < CC; ++cc) {
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-      const int y = p - kh;
-      if (y < 0 || y >= H) continue;
+      for (int k = 0; k < 3; ++k) {
+        const float4 wv = *reinterpret_cast<const float4*>(&taps[cc][k][cg * 4]);
+        float sv[4];
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int x = q - kw;
-        if (x < 0 || x >= W) continue;
-        acc = fmaf(dyc[(int64_t)y * W + x], wc[kh * 3 + kw], acc);
+        for (int e = 0; e < 4; ++e) sv[e] = line[cc][ug * 4 + e - k + 2];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[0][e] = fmaf(sv[e], wv.x, acc[0][e]);
+          acc[1][e] = fmaf(sv[e], wv.y, acc[1][e]);
+          acc[2][e] = fmaf(sv[e], wv.z, acc[2][e]);
+          acc[3][e] = fmaf(sv[e], wv.w, acc[3][e]);
+        }
       }
     }
+    __syncthreads();
   }
-  return acc;
+  const int R = 2 * (W + 2) + 2 * H;
+  const int base = side == 0 ? 0 : (side == 1 ? W + 2 : (side == 2 ? 2 * (W + 2) - 1 : 2 * (W + 2) + H - 1));
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int ci = ci0 + cg * 4 + a;
+    if (ci >= Cin) continue;
+    float* rg = ring + ((int64_t)n * Cin + ci) * R;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int u = u0 + ug * 4 + e;
+      if (u - u_first < U) rg[base + u] = acc[a][e];
+    }
+  }
 }
 
-__global__ __launch_bounds__(64) void reflect_border_grad_kernel(
-    const float* __restrict__ dy, const float* __restrict__ w, float* __restrict__ dx, int N,
-    int Cin, int Cout, int H, int W, int nrows, int r0, int r1, int ncols, int c0, int c1) {
-  // targets per plane: nrows full rows (r0, r1) + ncols columns (c0, c1) minus those rows
+__global__ __launch_bounds__(256) void reflect_fold_kernel(
+    const float* __restrict__ ring, float* __restrict__ dx, int N, int Cin, int H, int W,
+    int nrows, int r0, int r1, int ncols, int c0, int c1) {
   const int64_t per = (int64_t)nrows * W + (int64_t)ncols * (H - nrows);
-  const int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)N * Cin * per) return;
   const int64_t plane = t / per;
   int64_t k = t - plane * per;
-  const int n = (int)(plane / Cin), ci = (int)(plane - (int64_t)n * Cin);
   int i, j;
   if (k < (int64_t)nrows * W) {
     i = (k < W) ? r0 : r1;
@@ -148,25 +207,22 @@ __global__ __launch_bounds__(64) void reflect_border_grad_kernel(
     i = rr;
     j = cidx == 0 ? c0 : c1;
   }
-  const float* dyn = dy + (int64_t)n * Cout * H * W;
+  const int R = 2 * (W + 2) + 2 * H;
+  const float* rg = ring + plane * R;
   float add = 0.f;
-  // border rows p in {0, H+1} (every column q of the padded row, corners included)
+  // padded rows p in {0, H+1}: every column q of the padded row that reflects to j
   for (int pi = 0; pi < 2; ++pi) {
     const int p = pi ? H + 1 : 0;
     if (refl(p - 1, H) != i) continue;
-    for (int qi = 0; qi < 3; ++qi) {
-      const int q = qi == 0 ? 0 : (qi == 1 ? j + 1 : W + 1);
-      if (qi != 1 && refl(q - 1, W) != j) continue;
-      add += border_dxp(dyn, w, Cout, Cin, ci, H, W, p, q);
-    }
+    const float* row = rg + pi * (W + 2);
+    if (refl(-1, W) == j) add += row[0];
+    add += row[j + 1];
+    if (refl(W, W) == j) add += row[W + 1];
   }
-  // border columns q in {0, W+1} on interior padded rows p = i + 1
-  for (int qi = 0; qi < 2; ++qi) {
-    const int q = qi ? W + 1 : 0;
-    if (refl(q - 1, W) != j) continue;
-    add += border_dxp(dyn, w, Cout, Cin, ci, H, W, i + 1, q);
-  }
-  float* d = dx + ((int64_t)n * Cin + ci) * H * W + (int64_t)i * W + j;
+  // padded columns q in {0, W+1} on the interior padded row p = i + 1
+  if (refl(-1, W) == j) add += rg[2 * (W + 2) + i];
+  if (refl(W, W) == j) add += rg[2 * (W + 2) + H + i];
+  float* d = dx + plane * H * W + (int64_t)i * W + j;
   *d = *d + add;
 }
 
@@ -333,8 +389,17 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
                                                            int splits) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
+  // 8 independent loads in flight, summed in split order
   float s = 0.f;
-  for (int k = 0; k < splits; ++k) s += part[(int64_t)k * n + i];
+  int k = 0;
+  for (; k + 8 <= splits; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(k + u) * n + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; k < splits; ++k) s += part[(int64_t)k * n + i];
   dw[i] = s;
 }
 
@@ -473,18 +538,33 @@ extern "C" int rpst_maxpool2x2_ceil_backward(const float* x, const float* g, flo
   return launch_status("maxpool2_backward_kernel");
 }
 
+extern "C" size_t rpst_reflect_pad_border_grad_workspace_size(int N, int Cin, int H, int W) {
+  if (N <= 0 || Cin <= 0 || H <= 0 || W <= 0) return 0;
+  return sizeof(float) * (size_t)N * Cin * (2 * (size_t)(W + 2) + 2 * (size_t)H);
+}
+
 extern "C" int rpst_reflect_pad_border_grad(const float* dy, const float* w, float* dx, int N,
-                                            int Cin, int Cout, int H, int W,
-                                            rpst_stream_t stream) {
+                                            int Cin, int Cout, int H, int W, void* workspace,
+                                            size_t workspace_bytes, rpst_stream_t stream) {
   RPST_REQUIRE(dy && w && dx && N > 0 && Cin > 0 && Cout > 0, "reflect_border_grad: bad args");
   RPST_REQUIRE(H >= 2 && W >= 2, "reflect_border_grad: ReflectionPad2d(1) needs H, W >= 2");
+  if (!workspace || workspace_bytes < rpst_reflect_pad_border_grad_workspace_size(N, Cin, H, W)) {
+    set_error("reflect_border_grad: workspace too small");
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  float* ring = static_cast<float*>(workspace);
+  RPST_REQUIRE((int64_t)N * 4 <= 65535, "reflect_border_grad: batch too large");
+  const int umax = (W + 2 > H ? W + 2 : H);
+  reflect_ring_kernel<<<dim3((umax + 63) / 64, (Cin + 63) / 64, N * 4), 256, 0, st>>>(
+      dy, w, ring, N, Cin, Cout, H, W);
+  if (int e = launch_status("reflect_ring_kernel")) return e;
   const int r0 = 1, r1 = H - 2, c0 = 1, c1 = W - 2;
   const int nrows = (r0 == r1) ? 1 : 2, ncols = (c0 == c1) ? 1 : 2;
   const int64_t per = (int64_t)nrows * W + (int64_t)ncols * (H - nrows);
-  const int64_t n = (int64_t)N * Cin * per;
-  reflect_border_grad_kernel<<<blocks_for(n, 64), 64, 0, as_stream(stream)>>>(
-      dy, w, dx, N, Cin, Cout, H, W, nrows, r0, r1, ncols, c0, c1);
-  return launch_status("reflect_border_grad_kernel");
+  reflect_fold_kernel<<<blocks_for((int64_t)N * Cin * per), 256, 0, st>>>(
+      ring, dx, N, Cin, H, W, nrows, r0, r1, ncols, c0, c1);
+  return launch_status("reflect_fold_kernel");
 }
 
 static void wgrad_geometry(int N, int Cin, int H, int W, int Cout, int* splits,

@@ -72,8 +72,10 @@ def conv_dgrad(g: torch.Tensor, step: plan.ConvStep) -> torch.Tensor:
     if k == 3 and step.pad == ops.PAD_REFLECT:
         n, _, h, w = g.shape
         wd = c.weight.detach().contiguous()
+        nbytes = _lib.load().rpst_reflect_pad_border_grad_workspace_size(n, c.in_channels, h, w)
+        ws = _ws(nbytes, g)
         _lib.call("rpst_reflect_pad_border_grad", g.data_ptr(), wd.data_ptr(), dx.data_ptr(),
-                  n, c.in_channels, c.out_channels, h, w, _stream(g))
+                  n, c.in_channels, c.out_channels, h, w, ws.data_ptr(), nbytes, _stream(g))
     return dx
 
 
