@@ -168,11 +168,12 @@ def roofline_from_trace(summary):
         return None
     name, a = best
     avg_ms = a["ms"] / a["launches"]
-    wino = name.startswith("wino")
-    # Winograd F(2x2,3x3) performs 16 instead of 36 multiply-adds per 2x2 output tile and
-    # (ci, co): its algorithmic FLOPs are 4/9 of the direct convolution's. "achieved" is
-    # priced on the algorithm that ran; "effective" on the direct-convolution FLOPs.
-    flop = a["flops"] * (4.0 / 9.0 if wino else 1.0)
+    wino4, wino = name.startswith("wino4"), name.startswith("wino")
+    # Winograd F(2x2,3x3) performs 16 and F(4x4,3x3) 36 multiply-adds per 2x2 / 4x4 output
+    # tile and (ci, co) instead of 36 / 144: their algorithmic FLOPs are 4/9 and 1/4 of the
+    # direct convolution's. "achieved" is priced on the algorithm that ran; "effective" on
+    # the direct-convolution FLOPs.
+    flop = a["flops"] * (0.25 if wino4 else (4.0 / 9.0 if wino else 1.0))
     achieved = flop / (avg_ms * 1e-3) / 1e12
     effective = a["flops"] / (avg_ms * 1e-3) / 1e12
     # "conv3x3 128->256 512x512 N64 op0" -> launch geometry -> PMC record
@@ -184,13 +185,14 @@ def roofline_from_trace(summary):
     if name.startswith("wgrad"):  # weight gradient (training): not in the PMC table
         kname, traffic = "conv_wgrad_kernel", None
     else:
-        grid = _lib.load().rpst_conv2d_grid_threads(n, hs, ws, cout, ks, in_op)
-        kname = "wino_mfma_kernel" if wino else "conv_mfma_kernel"
+        grid = _lib.load().rpst_conv2d_grid_threads(n, cin, hs, ws, cout, ks, in_op)
+        kname = ("wino4_mfma_kernel" if wino4 else "wino_mfma_kernel") if wino else "conv_mfma_kernel"
         traffic = pmc_lookup(kname, grid)
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
             "traffic": traffic, "kernel": f"{kname} [{name}]",
-            "algorithm": "winograd F(2x2,3x3) fp32" if wino else (
+            "algorithm": ("winograd F(4x4,3x3) fp32" if wino4 else "winograd F(2x2,3x3) fp32")
+            if wino else (
                 "weight-gradient implicit GEMM fp32" if name.startswith("wgrad")
                 else "direct implicit GEMM fp32"),
             "effective_tflops": round(effective, 2),

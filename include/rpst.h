@@ -107,8 +107,9 @@ int rpst_conv2d(const float* input, const float* aux, const float* packed_weight
 /* Same conv, additionally returning calc_mean_std (base.py:399-407) of its OUTPUT per
  * (n, co): the statistics are reduced in the conv epilogue from registers and merged in
  * fp64, so an AdaIN consumer never re-reads the feature. mean/std_out: N*Cout floats.
- * Workspace: rpst_conv2d_stats_workspace_size(N, Hs, Ws, Cout, ksize, in_op). */
-size_t rpst_conv2d_stats_workspace_size(int N, int Hs, int Ws, int Cout, int ksize, int in_op);
+ * Workspace: rpst_conv2d_stats_workspace_size(N, Cin, Hs, Ws, Cout, ksize, in_op). */
+size_t rpst_conv2d_stats_workspace_size(int N, int Cin, int Hs, int Ws, int Cout, int ksize,
+                                        int in_op);
 int rpst_conv2d_stats(const float* input, const float* aux, const float* packed_weight,
                       const float* bias, const float* residual, float* out, int N, int Cin,
                       int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
@@ -126,14 +127,18 @@ int rpst_conv2d_skip_adain(const float* stylized, const float* content, const fl
 
 /* Launch geometry (total threads) rpst_conv2d would use for this shape — host-only; lets
  * profilers match rocprofv3 per-dispatch records (Grid_Size) to a layer. */
-int64_t rpst_conv2d_grid_threads(int N, int Hs, int Ws, int Cout, int ksize, int in_op);
+int64_t rpst_conv2d_grid_threads(int N, int Cin, int Hs, int Ws, int Cout, int ksize,
+                                 int in_op);
 
 /* Algorithm rpst_conv2d uses for this layer — host-only: RPST_CONV_DIRECT (implicit GEMM,
- * all 1x1 and 16-wide 3x3 layers) or RPST_CONV_WINOGRAD (F(2x2,3x3) in fp32, 3x3 layers
- * with Cout >= 32). The environment variable RPST_CONV_ALGO=direct|winograd overrides. */
+ * all 1x1 and 16-wide 3x3 layers), RPST_CONV_WINOGRAD4 (F(4x4,3x3) in fp32, 3x3 layers with
+ * Cout >= 32 whose loader operator is NONE / ADAIN / UPSAMPLE2) or RPST_CONV_WINOGRAD
+ * (F(2x2,3x3) in fp32, the other 3x3 layers with Cout >= 32). The environment variable
+ * RPST_CONV_ALGO=direct|winograd|winograd4 overrides. */
 #define RPST_CONV_DIRECT 0
 #define RPST_CONV_WINOGRAD 1
-int rpst_conv2d_algorithm(int Cout, int ksize);
+#define RPST_CONV_WINOGRAD4 2
+int rpst_conv2d_algorithm(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op);
 
 /* ---- stand-alone pool / upsample (same semantics as the conv input operators) ----- */
 int rpst_maxpool2x2_ceil(const float* in, float* out, int N, int C, int H, int W,

@@ -226,4 +226,15 @@ int wino_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);
 // fields (Cout_pad, nchunks, tiles_*, co_tiles, stat_P) and launches.
 int wino_launch(ConvArgs& a, int in_op, hipStream_t st);
 
+// ---- Winograd F(4x4,3x3) path (rpst_wino4.hip) ----------------------------------------
+// 16 x 64 outputs x 32 channels per 256-thread block; statistics partials per wave
+// (4 rows x 64 columns each).
+constexpr int kW4Rows = 16, kW4Cols = 64, kW4Co = 32;
+bool wino4_supports(int in_op);
+bool wino4_fits(int N, int Cin, int Hs, int Ws, int in_op);
+int wino4_persist();
+size_t wino4_packed_floats(int Cout, int Cin);
+int wino4_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);
+int wino4_launch(ConvArgs& a, int in_op, hipStream_t st);
+
 }  // namespace rpst

@@ -27,6 +27,7 @@
 #include "rpst_conv.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace rpst {
 
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(256) void stat_merge_kernel(const float2* __restric
                                                          float* __restrict__ mean,
                                                          float* __restrict__ stdv, int planes,
                                                          int P, int tiles_x, int WN, int NT,
-                                                         int H, int W, float eps) {
+                                                         int TW, int H, int W, float eps) {
   const int plane = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (plane >= planes) return;
@@ -312,7 +313,7 @@ __global__ __launch_bounds__(256) void stat_merge_kernel(const float2* __restric
     const int tile = p / WN, wn = p - tile * WN;
     const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
     const int rows = max(0, min(NT, H - (ty * NT * WN + wn * NT)));
-    const int cols = max(0, min(kTW, W - tx * kTW));
+    const int cols = max(0, min(TW, W - tx * TW));
     const double nb = (double)(rows * cols);
     if (nb == 0.0) continue;
     const float2 v = part[(int64_t)plane * P + p];
@@ -467,16 +468,22 @@ static int conv_variant(int BM, int ksize, int in_op) {
   return v;
 }
 
-// Algorithm for a 3x3 conv: Winograd F(2x2,3x3) (rpst_wino.hip) where it pays, else the
-// direct implicit GEMM. RPST_CONV_ALGO=direct|winograd overrides (tests, A/B benches).
-static bool use_winograd(int Cout, int ksize) {
-  if (ksize != 3) return false;
+// Algorithm for a 3x3 conv: Winograd F(4x4,3x3) (rpst_wino4.hip) for the loader
+// operators it implements, F(2x2,3x3) (rpst_wino.hip) for the others, the direct implicit
+// GEMM for the 16-wide layers and every 1x1. RPST_CONV_ALGO=direct|winograd|winograd4
+// overrides (tests, A/B benches; winograd4 falls back to winograd where unsupported).
+static constexpr bool kW4Default = false;  // F(4x4) opt-in until it outruns F(2x2)
+static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
+  if (ksize != 3) return RPST_CONV_DIRECT;
+  const bool w4 = wino4_supports(in_op) && wino4_fits(1, Cin, Hs, Ws, in_op);
   const char* e = getenv("RPST_CONV_ALGO");
   if (e && *e) {
-    if (e[0] == 'd') return false;
-    if (e[0] == 'w') return true;
+    if (e[0] == 'd') return RPST_CONV_DIRECT;
+    if (!strcmp(e, "winograd")) return RPST_CONV_WINOGRAD;
+    if (!strcmp(e, "winograd4")) return w4 ? RPST_CONV_WINOGRAD4 : RPST_CONV_WINOGRAD;
   }
-  return Cout >= 32;  // measured: the 16-wide output layers run faster direct
+  if (Cout < 32) return RPST_CONV_DIRECT;  // measured: the 16-wide output layers run faster direct
+  return (kW4Default && w4) ? RPST_CONV_WINOGRAD4 : RPST_CONV_WINOGRAD;
 }
 
 static void logical_hw(int Hs, int Ws, int in_op, int* H, int* W) {
@@ -494,20 +501,32 @@ static void logical_hw(int Hs, int Ws, int in_op, int* H, int* W) {
 // Launch geometry shared by the entry points: blocks, threads per block, statistics
 // partials per plane and their (rows per partial, partials per tile row) layout.
 struct ConvGeom {
-  bool wino;
+  int algo;
   int64_t blocks;
-  int nth, stat_P, stat_nt, stat_wn, tiles_x;
+  int nth, stat_P, stat_nt, stat_wn, stat_tw, tiles_x;
 };
 
-static ConvGeom conv_geom(int N, int Hs, int Ws, int Cout, int ksize, int in_op) {
+static ConvGeom conv_geom(int N, int Cin, int Hs, int Ws, int Cout, int ksize, int in_op) {
   int H, W;
   logical_hw(Hs, Ws, in_op, &H, &W);
   ConvGeom g{};
+  g.algo = conv_algo(Cout, Cin, Hs, Ws, ksize, in_op);
   g.tiles_x = (W + kTW - 1) / kTW;
-  if (use_winograd(Cout, ksize)) {
+  g.stat_tw = kTW;
+  if (g.algo == RPST_CONV_WINOGRAD4) {
+    g.tiles_x = (W + kW4Cols - 1) / kW4Cols;
+    const int ty = (H + kW4Rows - 1) / kW4Rows;
+    g.blocks = (int64_t)g.tiles_x * ty * N * (wino4_persist() ? 1 : (Cout + kW4Co - 1) / kW4Co);
+    g.nth = 512;
+    g.stat_P = g.tiles_x * ty * 4;
+    g.stat_nt = 4;
+    g.stat_wn = 4;
+    g.stat_tw = kW4Cols;
+    return g;
+  }
+  if (g.algo == RPST_CONV_WINOGRAD) {
     const int th = wino_th(), bm = wino_bm();
     const int ty = (H + th - 1) / th;
-    g.wino = true;
     g.blocks = (int64_t)g.tiles_x * ty * N * (wino_persist(in_op) ? 1 : (Cout + bm - 1) / bm);
     g.nth = kWinoNTH;
     g.stat_P = g.tiles_x * ty;
@@ -537,24 +556,25 @@ static size_t direct_packed_floats(int Cout, int Cin, int ksize) {
 
 using namespace rpst;
 
-// 3x3 weights are packed twice: the direct image followed by the Winograd image (the
-// algorithm is chosen per launch; both are small).
+// 3x3 weights are packed three times: the direct image, the F(2x2) Winograd image and
+// the F(4x4) Winograd image (the algorithm is chosen per launch; all are small).
 extern "C" size_t rpst_conv2d_packed_size(int Cout, int Cin, int ksize) {
   if (Cout <= 0 || Cin <= 0 || (ksize != 1 && ksize != 3)) return 0;
   size_t f = direct_packed_floats(Cout, Cin, ksize);
-  if (ksize == 3) f += wino_packed_floats(Cout, Cin);
+  if (ksize == 3) f += wino_packed_floats(Cout, Cin) + wino4_packed_floats(Cout, Cin);
   return f * sizeof(float);
 }
 
-extern "C" int64_t rpst_conv2d_grid_threads(int N, int Hs, int Ws, int Cout, int ksize,
-                                            int in_op) {
-  if (N <= 0 || Hs <= 0 || Ws <= 0 || Cout <= 0 || (ksize != 1 && ksize != 3)) return 0;
-  const ConvGeom g = conv_geom(N, Hs, Ws, Cout, ksize, in_op);
+extern "C" int64_t rpst_conv2d_grid_threads(int N, int Cin, int Hs, int Ws, int Cout,
+                                            int ksize, int in_op) {
+  if (N <= 0 || Cin <= 0 || Hs <= 0 || Ws <= 0 || Cout <= 0 || (ksize != 1 && ksize != 3))
+    return 0;
+  const ConvGeom g = conv_geom(N, Cin, Hs, Ws, Cout, ksize, in_op);
   return g.blocks * g.nth;
 }
 
-extern "C" int rpst_conv2d_algorithm(int Cout, int ksize) {
-  return use_winograd(Cout, ksize) ? RPST_CONV_WINOGRAD : RPST_CONV_DIRECT;
+extern "C" int rpst_conv2d_algorithm(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
+  return conv_algo(Cout, Cin, Hs, Ws, ksize, in_op);
 }
 
 extern "C" int rpst_conv2d_pack(const float* weight, float* packed, int Cout, int Cin,
@@ -568,7 +588,11 @@ extern "C" int rpst_conv2d_pack(const float* weight, float* packed, int Cout, in
                      as_stream(stream)>>>(weight, packed, Cout, Cin, ksize, ck_of(ksize),
                                           pad_cout(Cout), total);
   if (int e = launch_status("conv_pack_kernel")) return e;
-  if (ksize == 3) return wino_pack(weight, packed + total, Cout, Cin, as_stream(stream));
+  if (ksize == 3) {
+    if (int e = wino_pack(weight, packed + total, Cout, Cin, as_stream(stream))) return e;
+    return wino4_pack(weight, packed + total + wino_packed_floats(Cout, Cin), Cout, Cin,
+                      as_stream(stream));
+  }
   return RPST_OK;
 }
 
@@ -636,7 +660,16 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   // buffer offset
   RPST_REQUIRE(((int64_t)Cin + 16) * Hs * Ws * 4 < (1LL << 31),
                "conv2d: one image's input exceeds 2 GiB");
-  if (use_winograd(Cout, ksize)) {
+  const int algo = conv_algo(Cout, Cin, Hs, Ws, ksize, in_op);
+  if (algo == RPST_CONV_WINOGRAD4) {
+    a.wpk = packed_weight + direct_packed_floats(Cout, Cin, ksize) + wino_packed_floats(Cout, Cin);
+    a.stat_part = stat_part;
+    if (int e = wino4_launch(a, in_op, st)) return e;
+    if (stat_P) *stat_P = a.stat_P;
+    if (args_out) *args_out = a;
+    return RPST_OK;
+  }
+  if (algo == RPST_CONV_WINOGRAD) {
     a.wpk = packed_weight + direct_packed_floats(Cout, Cin, ksize);
     a.stat_part = stat_part;
     if (int e = wino_launch(a, in_op, st)) return e;
@@ -700,10 +733,10 @@ extern "C" int rpst_conv2d_skip_adain(const float* stylized, const float* conten
                      as_stream(stream));
 }
 
-extern "C" size_t rpst_conv2d_stats_workspace_size(int N, int Hs, int Ws, int Cout, int ksize,
-                                                   int in_op) {
-  if (N <= 0 || Hs <= 0 || Ws <= 0 || Cout <= 0 || (ksize != 1 && ksize != 3)) return 0;
-  const ConvGeom g = conv_geom(N, Hs, Ws, Cout, ksize, in_op);
+extern "C" size_t rpst_conv2d_stats_workspace_size(int N, int Cin, int Hs, int Ws, int Cout,
+                                                   int ksize, int in_op) {
+  if (N <= 0 || Cin <= 0 || Hs <= 0 || Ws <= 0 || Cout <= 0 || (ksize != 1 && ksize != 3)) return 0;
+  const ConvGeom g = conv_geom(N, Cin, Hs, Ws, Cout, ksize, in_op);
   return (size_t)N * Cout * g.stat_P * sizeof(float2);
 }
 
@@ -714,7 +747,7 @@ extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
                                  float* mean, float* std_out, float eps, void* workspace,
                                  size_t workspace_bytes, rpst_stream_t stream) {
   RPST_REQUIRE(mean && std_out, "conv2d_stats: null statistics pointer");
-  const size_t need = rpst_conv2d_stats_workspace_size(N, Hs, Ws, Cout, ksize, in_op);
+  const size_t need = rpst_conv2d_stats_workspace_size(N, Cin, Hs, Ws, Cout, ksize, in_op);
   if (!workspace || workspace_bytes < need) {
     set_error("conv2d_stats: workspace %zu < %zu bytes", workspace_bytes, need);
     return RPST_EWORKSPACE;
@@ -722,9 +755,9 @@ extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
   hipStream_t st = as_stream(stream);
   ConvArgs a{};
   int P = 0;
-  const ConvGeom g = conv_geom(N, Hs, Ws, Cout, ksize, in_op);
+  const ConvGeom g = conv_geom(N, Cin, Hs, Ws, Cout, ksize, in_op);
   const int planes = N * Cout;
-  if (!g.wino && g.stat_nt < 4) {  // tile without the fused statistics epilogue
+  if (g.algo == RPST_CONV_DIRECT && g.stat_nt < 4) {  // tile without the fused statistics epilogue
     if (int e = conv_common(input, aux, nullptr, packed_weight, bias, residual, out, N, Cin, Hs,
                             Ws, Cout, ksize, pad_mode, in_op, relu, nullptr, &P, &a, st))
       return e;
@@ -736,7 +769,7 @@ extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
     return e;
   stat_merge_kernel<<<(planes + 3) / 4, 256, 0, st>>>(static_cast<const float2*>(workspace), mean,
                                                       std_out, planes, P, a.tiles_x, g.stat_wn,
-                                                      g.stat_nt, a.H, a.W, eps);
+                                                      g.stat_nt, g.stat_tw, a.H, a.W, eps);
   return launch_status("stat_merge_kernel");
 }
 

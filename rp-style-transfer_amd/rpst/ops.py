@@ -169,12 +169,17 @@ def conv_out_hw(h: int, w: int, in_op: int) -> Tuple[int, int]:
     return h, w
 
 
-def _conv_name(ksize, cin, cout, h, w, n, in_op):
-    """Trace key of a conv launch; 'wino3x3' when the library runs it as Winograd
-    F(2x2,3x3) (the recorded FLOPs stay the direct-convolution count)."""
+_ALGO_TAG = {0: "conv", 1: "wino", 2: "wino4"}
+
+
+def _conv_name(ksize, cin, cout, hs, ws, n, in_op):
+    """Trace key of a conv launch: 'wino3x3' / 'wino43x3' when the library runs it as
+    Winograd F(2x2,3x3) / F(4x4,3x3) (the recorded FLOPs stay the direct-convolution
+    count). hs, ws: the SOURCE size; the key carries the output size."""
     algo = "conv"
-    if TRACE is not None and _lib.load().rpst_conv2d_algorithm(cout, ksize) == 1:
-        algo = "wino"
+    if TRACE is not None:
+        algo = _ALGO_TAG[_lib.load().rpst_conv2d_algorithm(cout, cin, hs, ws, ksize, in_op)]
+    h, w = conv_out_hw(hs, ws, in_op)
     return f"{algo}{ksize}x{ksize} {cin}->{cout} {h}x{w} N{n} op{in_op}"
 
 
@@ -201,7 +206,7 @@ def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], 
             assert aux.numel() == 4 * n * cin, "ADAIN aux = [mean_c|mean_s|std_c|std_s]"
         else:
             assert tuple(aux.shape) == (n, cin, h // 2, w // 2)
-    with _traced(_conv_name(ksize, cin, cout, h, w, n, in_op),
+    with _traced(_conv_name(ksize, cin, cout, hs, ws, n, in_op),
                  2.0 * n * cout * h * w * cin * ksize * ksize,
                  4.0 * (x.numel() + n * cout * h * w)):
         _lib.call("rpst_conv2d", x.data_ptr(), _ptr(aux), packed.data_ptr(),
@@ -225,7 +230,7 @@ def conv2d_skip_adain(x: torch.Tensor, content: torch.Tensor, params: torch.Tens
     assert params.numel() == 4 * n * cin, "params = [mean_c|mean_s|std_c|std_s]"
     if out is None:
         out = torch.empty((n, cout, h, w), device=x.device, dtype=torch.float32)
-    with _traced(_conv_name(ksize, cin, cout, h, w, n, IN_ADD_ADAIN),
+    with _traced(_conv_name(ksize, cin, cout, hs, ws, n, IN_ADD_ADAIN),
                  2.0 * n * cout * h * w * cin * ksize * ksize,
                  4.0 * (2 * x.numel() + n * cout * h * w)):
         _lib.call("rpst_conv2d_skip_adain", x.data_ptr(), content.data_ptr(), params.data_ptr(),
@@ -248,9 +253,9 @@ def conv2d_stats(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Ten
     mean = torch.empty((n, cout, 1, 1), device=x.device, dtype=torch.float32)
     std = torch.empty_like(mean)
     lib = _lib.load()
-    nbytes = lib.rpst_conv2d_stats_workspace_size(n, hs, ws, cout, ksize, in_op)
+    nbytes = lib.rpst_conv2d_stats_workspace_size(n, cin, hs, ws, cout, ksize, in_op)
     ws_t = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
-    with _traced(_conv_name(ksize, cin, cout, h, w, n, in_op), 2.0 * n * cout * h * w * cin * ksize * ksize,
+    with _traced(_conv_name(ksize, cin, cout, hs, ws, n, in_op), 2.0 * n * cout * h * w * cin * ksize * ksize,
                  4.0 * (x.numel() + n * cout * h * w)):
         _lib.call("rpst_conv2d_stats", x.data_ptr(), _ptr(aux), packed.data_ptr(),
                   _ptr(None if bias is None else _c(bias.detach())), None, out.data_ptr(), n,

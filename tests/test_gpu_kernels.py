@@ -133,12 +133,16 @@ CONV_CASES = [
     (1, 512, 16, 16, 512, 1, 0, 0, False),
     (1, 40, 7, 33, 72, 3, 0, 0, True),      # odd channel counts
     (1, 8, 2, 2, 8, 3, 1, 0, True),         # tiny reflect
+    (1, 40, 37, 70, 72, 3, 0, 0, True),     # ragged 16x64 F(4x4) blocks, 3 co tiles, 5 chunks
+    (1, 24, 18, 130, 40, 3, 1, 0, False),   # reflect, W % 4 != 0
+    (2, 16, 9, 35, 64, 3, 1, 2, True),      # upsample of an odd source
 ]
 
 
-@pytest.fixture(params=["direct", "winograd"])
+@pytest.fixture(params=["direct", "winograd", "winograd4"])
 def conv_algo(request, monkeypatch):
-    """Run a 3x3 conv test on both algorithms (librpst reads RPST_CONV_ALGO per launch)."""
+    """Run a 3x3 conv test on every algorithm (librpst reads RPST_CONV_ALGO per launch;
+    winograd4 falls back to winograd for the loader operators it does not implement)."""
     monkeypatch.setenv("RPST_CONV_ALGO", request.param)
     return request.param
 

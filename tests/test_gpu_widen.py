@@ -29,7 +29,7 @@ def gen(seed, shape, scale=1.0, offset=0.0):
     return (torch.rand(shape, generator=g) * 2 - 1) * scale + offset
 
 
-@pytest.fixture(params=["direct", "winograd"])
+@pytest.fixture(params=["direct", "winograd", "winograd4"])
 def conv_algo(request, monkeypatch):
     monkeypatch.setenv("RPST_CONV_ALGO", request.param)
     return request.param

@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--only", default=None, help="substring filter on 'cin->cout'")
-    ap.add_argument("--algo", default=None, choices=["direct", "winograd"],
+    ap.add_argument("--algo", default=None, choices=["direct", "winograd", "winograd4"],
                     help="time one algorithm only (profiling)")
     ap.add_argument("--default-only", action="store_true",
                     help="direct default variant vs Winograd only")
@@ -73,13 +73,15 @@ def main():
         times = {("d", v): [] for v in variants}
         if k == 3:
             times[("w", None)] = []
+            times[("w4", None)] = []
         if args.algo:
-            times = {key: [] for key in times if (key[0] == "w") == (args.algo == "winograd")}
+            want = {"direct": "d", "winograd": "w", "winograd4": "w4"}[args.algo]
+            times = {key: [] for key in times if key[0] == want}
         ref = None
         for rnd in range(args.rounds):
             for key in times:
                 algo, v = key
-                os.environ["RPST_CONV_ALGO"] = "winograd" if algo == "w" else "direct"
+                os.environ["RPST_CONV_ALGO"] = {"w": "winograd", "w4": "winograd4"}.get(algo, "direct")
                 if v is None:
                     os.environ.pop("RPST_CONV_VARIANT", None)
                 else:
@@ -103,9 +105,9 @@ def main():
         row = {"layer": f"{cin}->{cout} k{k} {h}x{wd} N{n} pad{pad} op{in_op}"}
         for (algo, v), ts in times.items():
             ms = min(ts)
-            name = "wino" if algo == "w" else ("direct" if v is None else f"v{v}")
+            name = {"w": "wino", "w4": "wino4"}.get(algo, "direct" if v is None else f"v{v}")
             row[f"{name}_ms"] = round(ms, 3)
-            # effective TF/s: direct-convolution FLOPs / time (Winograd executes 4/9 of them)
+            # effective TF/s: direct-convolution FLOPs / time (F(2x2) executes 4/9, F(4x4) 1/4)
             row[f"{name}_tf"] = round(flops / ms / 1e9, 1)
         results.append(row)
         print(json.dumps(row), flush=True)
