@@ -140,6 +140,13 @@ int64_t rpst_conv2d_grid_threads(int N, int Cin, int Hs, int Ws, int Cout, int k
 #define RPST_CONV_WINOGRAD4 2
 int rpst_conv2d_algorithm(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op);
 
+/* Precise mode for the CALLING THREAD (host-only): while on, the default choice never picks
+ * F(4x4,3x3) (its fp32 rounding, ~1e-6 per conv, compounds through the ~30 convolutions of
+ * a training step's backward chain); F(2x2) runs instead. Returns the previous setting.
+ * The training autograd path (rpst/autograd.py) turns it on; an explicit
+ * RPST_CONV_ALGO still wins. */
+int rpst_conv2d_set_precise(int on);
+
 /* ---- stand-alone pool / upsample (same semantics as the conv input operators) ----- */
 int rpst_maxpool2x2_ceil(const float* in, float* out, int N, int C, int H, int W,
                          rpst_stream_t stream);

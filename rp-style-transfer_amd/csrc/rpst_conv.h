@@ -227,8 +227,8 @@ int wino_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);
 int wino_launch(ConvArgs& a, int in_op, hipStream_t st);
 
 // ---- Winograd F(4x4,3x3) path (rpst_wino4.hip) ----------------------------------------
-// 16 x 64 outputs x 32 channels per 256-thread block; statistics partials per wave
-// (4 rows x 64 columns each).
+// 16 x 64 outputs x 32 channels per 512-thread block; statistics partials per tile row
+// of 4 rows x 64 columns.
 constexpr int kW4Rows = 16, kW4Cols = 64, kW4Co = 32;
 bool wino4_supports(int in_op);
 bool wino4_fits(int N, int Cin, int Hs, int Ws, int in_op);

@@ -472,7 +472,9 @@ static int conv_variant(int BM, int ksize, int in_op) {
 // operators it implements, F(2x2,3x3) (rpst_wino.hip) for the others, the direct implicit
 // GEMM for the 16-wide layers and every 1x1. RPST_CONV_ALGO=direct|winograd|winograd4
 // overrides (tests, A/B benches; winograd4 falls back to winograd where unsupported).
-static constexpr bool kW4Default = false;  // F(4x4) opt-in until it outruns F(2x2)
+// rpst_conv2d_set_precise: this thread's launches keep to F(2x2) where F(4x4) would run
+static thread_local int t_conv_precise = 0;
+
 static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
   if (ksize != 3) return RPST_CONV_DIRECT;
   const bool w4 = wino4_supports(in_op) && wino4_fits(1, Cin, Hs, Ws, in_op);
@@ -482,8 +484,12 @@ static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
     if (!strcmp(e, "winograd")) return RPST_CONV_WINOGRAD;
     if (!strcmp(e, "winograd4")) return w4 ? RPST_CONV_WINOGRAD4 : RPST_CONV_WINOGRAD;
   }
-  if (Cout < 32) return RPST_CONV_DIRECT;  // measured: the 16-wide output layers run faster direct
-  return (kW4Default && w4) ? RPST_CONV_WINOGRAD4 : RPST_CONV_WINOGRAD;
+  // measured (profiles/r01_bench_conv_wino4.log): F(4x4) wins every layer with >= 16 input
+  // channels it supports, the 16-wide 32->16 / 16->3 decoder layers included; the 3-channel
+  // input layer and the remaining 16-wide outputs run faster direct
+  if (w4 && Cin >= 16 && !t_conv_precise) return RPST_CONV_WINOGRAD4;
+  if (w4 && Cin >= 16) return RPST_CONV_WINOGRAD;  // precise mode, same shapes as F(4x4)
+  return Cout >= 32 ? RPST_CONV_WINOGRAD : RPST_CONV_DIRECT;
 }
 
 static void logical_hw(int Hs, int Ws, int in_op, int* H, int* W) {
@@ -571,6 +577,12 @@ extern "C" int64_t rpst_conv2d_grid_threads(int N, int Cin, int Hs, int Ws, int 
     return 0;
   const ConvGeom g = conv_geom(N, Cin, Hs, Ws, Cout, ksize, in_op);
   return g.blocks * g.nth;
+}
+
+extern "C" int rpst_conv2d_set_precise(int on) {
+  const int old = t_conv_precise;
+  t_conv_precise = on != 0;
+  return old;
 }
 
 extern "C" int rpst_conv2d_algorithm(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {

@@ -14,15 +14,21 @@
 // (tests/test_gpu_kernels.py, fixture conv_algo).
 //
 // Block = 8 waves, two per SIMD: an output region of 16 rows x 64 columns = 4 x 16
-// Winograd tiles and 32 output channels. Wave w owns tile row w & 3 and the 16 channels of
-// half w >> 2: 16 tiles x 16 channels x all 36 transformed positions = 144 accumulator
-// registers, so the output transform is lane-local (no exchange). Per K step of 4 channels
-// a lane (k = lane >> 4, tile n = lane & 15) reads its 6x6 input window from the LDS patch,
-// transforms it to V (144 VALU), and issues 36 v_mfma_f32_16x16x4_f32 (one per position):
-// A = U (LDS, one ds_read_b128 per 4 MFMAs), B = V.
-// Per chunk of 8 channels: the raw patch of the NEXT chunk is loaded into registers and the
-// next weight slice (36 KiB) streams into LDS by LDS-DMA while this chunk computes; one
-// barrier per chunk. One block loops over the co tiles of its spatial tile (a.persist).
+// Winograd tiles and 32 output channels. Wave w owns tile row w & 3 and the transformed
+// rows 3h..3h+2 (h = w >> 2) of all 32 channels: 16 tiles x 32 channels x 18 positions =
+// 144 accumulator registers. Per K step of 4 channels a lane (k = lane >> 4, tile
+// n = lane & 15) reads 5 rows of its 6x6 input window from the LDS patch, forms its three
+// rows of V = B^T d B (72 VALU) and issues 36 v_mfma_f32_16x16x4_f32 (18 positions x 2
+// channel halves sharing each V value): A = U (LDS, one ds_read_b128 per 4 MFMAs).
+// Per chunk of 8 channels the next chunk's patch and weight slice stream into LDS by
+// LDS-DMA while this one computes (patch: 19 pieces of 64 floats per channel, per-lane
+// source offsets resolved against the padding once per block; weights: 36 pieces of
+// 1 KiB); one barrier per chunk. One block loops over the co tiles of its spatial tile.
+// The output transform splits like the positions: each wave applies A^T . A to its three
+// rows (a partial 4x4 tile), the two waves of a tile row swap the partials of the channel
+// half the other one finishes through LDS, and each adds, biases, activates and stores 16
+// channels. Measured against the alternatives (profiles/r01_wino4_variants.log): a 4-wave
+// one-per-SIMD software-pipelined form and register-staged patches were slower.
 #include "rpst_conv.h"
 
 namespace rpst {
@@ -33,19 +39,21 @@ constexpr int kW4CK = 8;                   // input channels per chunk
 constexpr int kW4BM = 32;                  // output channels per co tile
 constexpr int kW4TH = 16, kW4TW = 64;      // output rows x columns per block
 constexpr int kW4PH = kW4TH + 2;           // patch rows
-constexpr int kW4PS = 68;                  // patch row stride (floats, 16-B aligned rows)
-constexpr int kW4CS = 1280;                // patch channel stride (= 0 mod 64 banks)
+constexpr int kW4PS = 66;                  // patch row stride (floats): rows are contiguous
+constexpr int kW4CS = 1218;                // channel stride: >= 19 x 64 (LDS-DMA pieces), = 2 mod 4
+constexpr int kW4DMA = 19;                 // 64-float LDS-DMA pieces per patch channel
 constexpr int kW4PATCH = kW4CK * kW4CS;    // floats per patch buffer
 constexpr int kW4WCH = 36 * kW4BM * kW4CK; // weight floats per (co tile, chunk) = 9216
 constexpr int kW4NTH = 512;
-static_assert(kW4PH * kW4PS <= kW4CS, "patch channel fits its stride");
+static_assert(kW4PH * kW4PS <= kW4DMA * 64 && kW4DMA * 64 <= kW4CS, "patch channel pieces");
 static_assert(kW4WCH % (64 * 4) == 0, "weight slice = whole 1-KiB LDS-DMA pieces");
 
 // ---- weight transform + packing -------------------------------------------------------
-// packed[(((((ct * nch + c) * 2 + s) * 2 + mt) * 9 + q) * 64 + l) * 4 + e] = U_xi[co][ci]
-// with xi = 4q + e (= 6 i + jj), co = ct*32 + mt*16 + (l & 15), ci = c*8 + 4s + (l >> 4):
-// lane l's A operands of positions 4q..4q+3 are one 16-B word, and one (co tile, chunk)
-// slice is contiguous (the LDS-DMA copies it verbatim).
+// packed[(((((ct * nch + c) * 2 + s) * 2 + h) * 9 + q) * 64 + l) * 4 + e] = U_xi[co][ci]
+// with f = 4q + e, xi = 18 h + (f >> 1) (= 6 i + jj), co = ct*32 + (f & 1)*16 + (l & 15),
+// ci = c*8 + 4s + (l >> 4): lane l's A operands of positions 2q, 2q+1 (both channel halves)
+// are one 16-B word, and one (co tile, chunk) slice is contiguous (the LDS-DMA copies it
+// verbatim).
 __global__ void wino4_pack_kernel(const float* __restrict__ w, float* __restrict__ pk, int Cout,
                                   int Cin, int nch, int64_t total) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -56,13 +64,13 @@ __global__ void wino4_pack_kernel(const float* __restrict__ w, float* __restrict
   r >>= 6;
   const int q = (int)(r % 9);
   r /= 9;
-  const int mt = (int)(r & 1);
+  const int h = (int)(r & 1);
   r >>= 1;
   const int s = (int)(r & 1);
   r >>= 1;
   const int c = (int)(r % nch);
   const int ct = (int)(r / nch);
-  const int xi = 4 * q + e;
+  const int f = 4 * q + e, xi = 18 * h + (f >> 1), mt = f & 1;
   const int i = xi / 6, jj = xi % 6;
   const int co = ct * kW4BM + mt * 16 + (l & 15);
   const int ci = c * kW4CK + 4 * s + (l >> 4);
@@ -147,7 +155,10 @@ __device__ __forceinline__ bool resolve_bf(int& v, int n, bool zero_pad) {
   return in || !zero_pad;
 }
 
-template <int INOP, bool PERSIST>
+// DBG (timing experiments only, tools/wino4_dbg.sh; results are wrong): bit0 no patch
+// loads, bit1 no weight DMA, bit2 no patch stores, bit3 no input transform, bit4 no
+// barriers in the main loop, bit5 no epilogue, bit6 no weight LDS reads.
+template <int INOP, bool PERSIST, int DBG = 0>
 __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   static_assert(RawN<INOP>::R == 1, "one raw load per patch element");
   __shared__ __attribute__((aligned(16))) float smem[2 * kW4PATCH + 2 * kW4WCH];
@@ -171,75 +182,96 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int k = lane >> 4, tn = lane & 15;
-  const int wr = wave & 3, wm = wave >> 2;  // tile row, channel half
+  const int wr = wave & 3, ph = wave >> 2;  // tile row, transformed-row half
 
   const bool pooled = INOP == RPST_IN_UPSAMPLE2;
   const unsigned in_plane = pooled ? (unsigned)(a.Hs * a.Ws) : (unsigned)(a.H * a.W);
-  // out-of-range offset for a padding position: the image's byte size, added either to
-  // the column (VGPR) or the row (SGPR) part; wino4_launch checks that two of them plus the
-  // largest channel offset stay below 2^32
+  // out-of-range offset for a padding position: the image's byte size, added to the
+  // channel offset (wino4_fits keeps two of them plus the largest channel offset < 2^32)
   const unsigned oob = a.Cin * in_plane * 4u;
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.in + (int64_t)n * a.Cin * in_plane), (short)0, (int)oob, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.wpk, (short)0, (int)((unsigned)(a.co_tiles * nch * kW4WCH) * 4u), 0x00020000);
 
-  // patch loader: wave -> channel cg of the chunk, lane -> column x0 + lane of all 18 patch
-  // rows (one 256-B row segment per wave-instruction); lanes < 36 also load one halo
-  // element (row lane >> 1, left / right). Row offsets are wave-uniform (soffset), column
-  // offsets per lane; a zero-padding position reads out of range (returns 0).
+  // ---- patch of one chunk: channel cg = wave, [18 rows][66 columns] contiguous at stride
+  // 1218. One-load operators (NONE, UPSAMPLE2) stream it by LDS-DMA: lane l of piece i
+  // fetches patch element 64 i + l; ADAIN stages through registers (lane -> column 1 + lane
+  // of every row, lanes < 36 one halo element) to apply its affine inside the image.
   const int cg = wave;
   const bool zp = a.pad == RPST_PAD_ZERO;
   const int rs = pooled ? a.Ws : a.W;  // source row stride
+  constexpr bool kDMA = INOP != RPST_IN_ADAIN;
+  unsigned poff[kDMA ? kW4DMA : 1];
+  if constexpr (kDMA) {
+#pragma unroll
+    for (int i = 0; i < kW4DMA; ++i) {
+      const int f = 64 * i + lane;
+      const int row = min(f / kW4PS, kW4PH - 1), col = f - (f / kW4PS) * kW4PS;
+      int y = y0 - 1 + row, x = x0 - 1 + col;
+      const bool ok = resolve_bf(y, a.H, zp) & resolve_bf(x, a.W, zp);
+      poff[i] = ok ? ((unsigned)((pooled ? y >> 1 : y) * rs) + (unsigned)(pooled ? x >> 1 : x)) * 4u
+                   : oob;
+    }
+  }
   int bx = x0 + lane;
   const bool okx = resolve_bf(bx, a.W, zp);
-  const unsigned cx = okx ? (unsigned)(pooled ? bx >> 1 : bx) * 4u : oob;
+  const unsigned cx = okx ? (unsigned)bx * 4u : oob;
   const bool has_halo = lane < 2 * kW4PH;
   const int hrw = lane >> 1;  // halo patch row
   int hy = y0 - 1 + (has_halo ? hrw : 0), hx = (lane & 1) ? x0 + kW4TW : x0 - 1;
   const bool h_ok = has_halo && resolve_bf(hy, a.H, zp) && resolve_bf(hx, a.W, zp);
-  const unsigned hoff =
-      h_ok ? ((unsigned)((pooled ? hy >> 1 : hy) * rs) + (unsigned)(pooled ? hx >> 1 : hx)) * 4u
-           : oob;
+  const unsigned hoff = h_ok ? ((unsigned)(hy * rs) + (unsigned)hx) * 4u : oob;
   const int hcol = (lane & 1) ? kW4TW + 1 : 0;
 
-  float X[kW4PH + 1];
+  float X[kDMA ? 1 : kW4PH + 1];
   AdainP ap{};
 
-  auto load = [&](int c) {
+  // chunk c's patch into pbuf: LDS-DMA pieces, or register loads (written by store())
+  auto load = [&](int c, float* pbuf) {
     const unsigned ch = (unsigned)(c * kW4CK + cg);
-    const unsigned pb = ch * in_plane * 4u;  // >= the range for a padding channel
-    const unsigned v0 = pb + cx;
-    if constexpr (INOP == RPST_IN_ADAIN) ap = adain_params(a.aux, n, (int)ch, a);
+    if (DBG & 1) return;
+    if constexpr (kDMA) {
+      const int so = __builtin_amdgcn_readfirstlane((int)(ch * in_plane * 4u));
+      float* xs = pbuf + cg * kW4CS;
 #pragma unroll
-    for (int py = 0; py < kW4PH; ++py) {
-      int y = y0 - 1 + py;
-      const bool yok = resolve_bf(y, a.H, zp);
-      const int ro = __builtin_amdgcn_readfirstlane(yok ? (int)((pooled ? y >> 1 : y) * rs * 4)
-                                                        : (int)oob);
-      X[py] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (int)v0, ro, 0));
+      for (int i = 0; i < kW4DMA; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(xs + 64 * i), 4, (int)poff[i],
+                                                 so, 0, 0);
+    } else {
+      const unsigned pb = ch * in_plane * 4u;  // >= the range for a padding channel
+      const unsigned v0 = pb + cx;
+      ap = adain_params(a.aux, n, (int)ch, a);
+#pragma unroll
+      for (int py = 0; py < kW4PH; ++py) {
+        int y = y0 - 1 + py;
+        const bool yok = resolve_bf(y, a.H, zp);
+        const int ro = __builtin_amdgcn_readfirstlane(yok ? (int)(y * rs * 4) : (int)oob);
+        X[py] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (int)v0, ro, 0));
+      }
+      X[kW4PH] =
+          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (int)(pb + hoff), 0, 0));
     }
-    X[kW4PH] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (int)(pb + hoff), 0, 0));
   };
-  // AdaIN on load: ((v - mean_c) / std_c) * std_s + mean_s, zero at padding positions
-  auto comb = [&](float v, bool ok) {
-    if constexpr (INOP == RPST_IN_ADAIN) return ok ? fmaf(v - ap.mc, ap.scale, ap.ms) : 0.f;
-    else return v;
-  };
+  // ADAIN: ((v - mean_c) / std_c) * std_s + mean_s inside the image, 0 at padding positions
   auto store = [&](int c, float* pbuf) {
-    float* xs = pbuf + cg * kW4CS;
-    const bool chok = c * kW4CK + cg < a.Cin;
+    if constexpr (!kDMA) {
+      if (DBG & 4) return;
+      float* xs = pbuf + cg * kW4CS;
+      const bool chok = c * kW4CK + cg < a.Cin;
 #pragma unroll
-    for (int py = 0; py < kW4PH; ++py) {
-      int y = y0 - 1 + py;
-      const bool rok = chok && resolve_bf(y, a.H, zp);
-      xs[py * kW4PS + 1 + lane] = comb(X[py], rok && okx);
+      for (int py = 0; py < kW4PH; ++py) {
+        int y = y0 - 1 + py;
+        const bool rok = chok && resolve_bf(y, a.H, zp) && okx;
+        xs[py * kW4PS + 1 + lane] = rok ? fmaf(X[py] - ap.mc, ap.scale, ap.ms) : 0.f;
+      }
+      const float hv = (chok && h_ok) ? fmaf(X[kW4PH] - ap.mc, ap.scale, ap.ms) : 0.f;
+      if (has_halo) xs[hrw * kW4PS + hcol] = hv;
     }
-    const float hv = comb(X[kW4PH], chok && h_ok);
-    if (has_halo) xs[hrw * kW4PS + hcol] = hv;
   };
   // weight slice of (co tile ct, chunk c) -> LDS by LDS-DMA: 36 pieces of 1 KiB over 8 waves
   auto wdma = [&](int ct, int c, float* wbuf) {
+    if (DBG & 2) return;
     const unsigned base = (unsigned)((ct * nch + c) * kW4WCH) * 4u + (unsigned)lane * 16u;
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
@@ -250,142 +282,225 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     }
   };
 
-  floatx4 acc[36];
+  floatx4 acc[18][2];
 #pragma unroll
-  for (int x = 0; x < 36; ++x) acc[x] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // one chunk: 2 K steps of 4 channels, each 144 VALU of input transform + 36 MFMAs
+  // one chunk: 2 K steps of 4 channels, each 72 VALU of input transform + 36 MFMAs
   auto compute = [&](const float* pbuf, const float* wbuf) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const float* pr = pbuf + (4 * s + k) * kW4CS + 4 * wr * kW4PS + 4 * tn;
-      float d[6][6];
+      const float* wq = wbuf + (s * 2 + ph) * 9 * 256 + lane * 4;
+      float4 w4[9];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        const float4 u = *reinterpret_cast<const float4*>(pr + r * kW4PS);
-        const float4 v = *reinterpret_cast<const float4*>(pr + r * kW4PS + 4);
-        d[r][0] = u.x;
-        d[r][1] = u.y;
-        d[r][2] = u.z;
-        d[r][3] = u.w;
-        d[r][4] = v.x;
-        d[r][5] = v.y;
+      for (int q = 0; q < 3; ++q)
+        w4[q] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
+                           : *reinterpret_cast<const float4*>(wq + q * 256);
+      // input rows ph .. ph + 4 of this lane's 6x6 window
+      const float* pr = pbuf + (4 * s + k) * kW4CS + (4 * wr + ph) * kW4PS + 4 * tn;
+      float d[5][6];
+#pragma unroll
+      for (int r = 0; r < 5; ++r) {
+        const float2 u0 = *reinterpret_cast<const float2*>(pr + r * kW4PS);
+        const float2 u1 = *reinterpret_cast<const float2*>(pr + r * kW4PS + 2);
+        const float2 u2 = *reinterpret_cast<const float2*>(pr + r * kW4PS + 4);
+        d[r][0] = u0.x;
+        d[r][1] = u0.y;
+        d[r][2] = u1.x;
+        d[r][3] = u1.y;
+        d[r][4] = u2.x;
+        d[r][5] = u2.y;
+      }
+      // rows 3ph..3ph+2 of B^T d (d[r] = input row ph + r), then B along each row
+      float t[3][6];
+      if (DBG & 8) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int c = 0; c < 6; ++c) t[i][c] = d[i][c];
+      } else if (ph == 0) {
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          const float A = fmaf(-4.f, d[2][c], d[4][c]), B = fmaf(-4.f, d[1][c], d[3][c]);
+          t[0][c] = fmaf(4.f, d[0][c], fmaf(-5.f, d[2][c], d[4][c]));
+          t[1][c] = A + B;
+          t[2][c] = A - B;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          const float C = d[3][c] - d[1][c], E = d[2][c] - d[0][c];
+          t[0][c] = fmaf(2.f, E, C);
+          t[1][c] = fmaf(-2.f, E, C);
+          t[2][c] = fmaf(4.f, d[0][c], fmaf(-5.f, d[2][c], d[4][c]));
+        }
       }
 #pragma unroll
-      for (int c = 0; c < 6; ++c) bt6(d[0][c], d[1][c], d[2][c], d[3][c], d[4][c], d[5][c]);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) bt6(d[i][0], d[i][1], d[i][2], d[i][3], d[i][4], d[i][5]);
-      const float* wq = wbuf + (s * 2 + wm) * 9 * 256 + lane * 4;
+      for (int i = 0; i < 3; ++i)
+        if (!(DBG & 8)) bt6(t[i][0], t[i][1], t[i][2], t[i][3], t[i][4], t[i][5]);
 #pragma unroll
       for (int q = 0; q < 9; ++q) {
-        const float4 w4 = *reinterpret_cast<const float4*>(wq + q * 256);
-        const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int xi = 4 * q + e;
-          acc[xi] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[e], d[xi / 6][xi % 6], acc[xi], 0, 0, 0);
-        }
+        if (q + 3 < 9)
+          w4[q + 3] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
+                                 : *reinterpret_cast<const float4*>(wq + (q + 3) * 256);
+        const int p0 = 2 * q, p1 = 2 * q + 1;
+        const float v0 = t[p0 / 6][p0 % 6], v1 = t[p1 / 6][p1 % 6];
+        acc[p0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].x, v0, acc[p0][0], 0, 0, 0);
+        acc[p0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].y, v0, acc[p0][1], 0, 0, 0);
+        acc[p1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].z, v1, acc[p1][0], 0, 0, 0);
+        acc[p1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].w, v1, acc[p1][1], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the next K step's reads below these MFMAs
     }
   };
 
-  // output transform, bias, activation, store and the optional per-wave statistics of one
-  // co tile; lane (k, tn) holds channels co0 + 16 wm + 4k + r of tile (wr, tn)
-  const int gy0 = y0 + 4 * wr, gx0 = x0 + 4 * tn;
-  const bool vec = (a.W & 3) == 0 && gx0 + 3 < a.W;
-  auto epilogue = [&](int ct) {
-    const int rows = max(0, min(4, a.H - gy0)), cols = max(0, min(kW4TW, a.W - x0));
-    const int cnt = rows * cols;
-    const float inv = cnt > 0 ? 1.f / (float)cnt : 0.f;
+  // this wave's partial output tile of channel half mt, accumulator element r:
+  // sum over its transformed rows i = 3ph + i' of A^T[:, i] (M[i, :] A)
+  auto partial = [&](int mt, int r, float (&Y)[16]) {
+    float P[3][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float P[6][4];
+    for (int i = 0; i < 3; ++i) {
+      float m[6];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        float m[6];
+      for (int jj = 0; jj < 6; ++jj) m[jj] = acc[6 * i + jj][mt][r];
+      at6(m, P[i]);
+    }
 #pragma unroll
-        for (int jj = 0; jj < 6; ++jj) m[jj] = acc[6 * i + jj][r];
-        at6(m, P[i]);
-      }
-      float Y[4][4];
-#pragma unroll
-      for (int xx = 0; xx < 4; ++xx) {
-        float m[6], p[4];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) m[i] = P[i][xx];
-        at6(m, p);
-#pragma unroll
-        for (int yy = 0; yy < 4; ++yy) Y[yy][xx] = p[yy];
-      }
-      const int co = ct * kW4BM + 16 * wm + 4 * k + r;
-      const bool cok = co < a.Cout;
-      const float b = (a.bias && cok) ? a.bias[co] : 0.f;
-      float sum = 0.f;
-#pragma unroll
-      for (int yy = 0; yy < 4; ++yy)
-#pragma unroll
-        for (int xx = 0; xx < 4; ++xx) {
-          const float v = activate(Y[yy][xx] + b, a.relu);
-          Y[yy][xx] = v;
-          sum += (yy < rows && gx0 + xx < a.W) ? v : 0.f;
-        }
-      if (cok) {
-        float* o = a.out + (((int64_t)n * a.Cout + co) * a.H + gy0) * a.W + gx0;
-#pragma unroll
-        for (int yy = 0; yy < 4; ++yy) {
-          if (yy < rows) {
-            if (vec) {
-              *reinterpret_cast<float4*>(o + yy * a.W) =
-                  make_float4(Y[yy][0], Y[yy][1], Y[yy][2], Y[yy][3]);
-            } else {
-#pragma unroll
-              for (int xx = 0; xx < 4; ++xx)
-                if (gx0 + xx < a.W) o[yy * a.W + xx] = Y[yy][xx];
-            }
-          }
-        }
-      }
-      if (a.stat_part) {
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) sum += __shfl_xor(sum, m, 64);
-        const float mean = sum * inv;
-        float m2 = 0.f;
-#pragma unroll
-        for (int yy = 0; yy < 4; ++yy)
-#pragma unroll
-          for (int xx = 0; xx < 4; ++xx) {
-            const float dv = Y[yy][xx] - mean;
-            m2 += (yy < rows && gx0 + xx < a.W) ? dv * dv : 0.f;
-          }
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) m2 += __shfl_xor(m2, m, 64);
-        if (tn == 0 && cok)
-          a.stat_part[((int64_t)n * a.Cout + co) * a.stat_P + (ty * a.tiles_x + tx) * 4 + wr] =
-              make_float2(mean, m2);
+    for (int x = 0; x < 4; ++x) {
+      if (ph == 0) {
+        const float s12 = P[1][x] + P[2][x], d12 = P[1][x] - P[2][x];
+        Y[0 * 4 + x] = P[0][x] + s12;
+        Y[1 * 4 + x] = d12;
+        Y[2 * 4 + x] = s12;
+        Y[3 * 4 + x] = d12;
+      } else {
+        const float s34 = P[0][x] + P[1][x], d34 = P[0][x] - P[1][x];
+        Y[0 * 4 + x] = s34;
+        Y[1 * 4 + x] = 2.f * d34;
+        Y[2 * 4 + x] = 4.f * s34;
+        Y[3 * 4 + x] = fmaf(8.f, d34, P[2][x]);
       }
     }
   };
 
+  // bias, activation, store and the optional per-wave statistics of one finished tile:
+  // channel co of tile (wr, tn)
+  const int gy0 = y0 + 4 * wr, gx0 = x0 + 4 * tn;
+  const bool vec = (a.W & 3) == 0 && gx0 + 3 < a.W;
+  const int rows = max(0, min(4, a.H - gy0)), cols = max(0, min(kW4TW, a.W - x0));
+  const float inv = rows * cols > 0 ? 1.f / (float)(rows * cols) : 0.f;
+  auto finish = [&](int co, float (&Y)[16]) {
+    const bool cok = co < a.Cout;
+    const float bv = (a.bias && cok) ? a.bias[co] : 0.f;
+    float sum = 0.f;
+#pragma unroll
+    for (int yy = 0; yy < 4; ++yy)
+#pragma unroll
+      for (int xx = 0; xx < 4; ++xx) {
+        const float v = activate(Y[yy * 4 + xx] + bv, a.relu);
+        Y[yy * 4 + xx] = v;
+        sum += (yy < rows && gx0 + xx < a.W) ? v : 0.f;
+      }
+    if (cok) {
+      float* o = a.out + (((int64_t)n * a.Cout + co) * a.H + gy0) * a.W + gx0;
+#pragma unroll
+      for (int yy = 0; yy < 4; ++yy) {
+        if (yy < rows) {
+          if (vec) {
+            *reinterpret_cast<float4*>(o + yy * a.W) =
+                make_float4(Y[yy * 4], Y[yy * 4 + 1], Y[yy * 4 + 2], Y[yy * 4 + 3]);
+          } else {
+#pragma unroll
+            for (int xx = 0; xx < 4; ++xx)
+              if (gx0 + xx < a.W) o[yy * a.W + xx] = Y[yy * 4 + xx];
+          }
+        }
+      }
+    }
+    if (a.stat_part) {
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) sum += __shfl_xor(sum, m, 64);
+      const float mean = sum * inv;
+      float m2 = 0.f;
+#pragma unroll
+      for (int yy = 0; yy < 4; ++yy)
+#pragma unroll
+        for (int xx = 0; xx < 4; ++xx) {
+          const float dv = Y[yy * 4 + xx] - mean;
+          m2 += (yy < rows && gx0 + xx < a.W) ? dv * dv : 0.f;
+        }
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) m2 += __shfl_xor(m2, m, 64);
+      if (tn == 0 && cok)
+        a.stat_part[((int64_t)n * a.Cout + co) * a.stat_P + (ty * a.tiles_x + tx) * 4 + wr] =
+            make_float2(mean, m2);
+    }
+  };
+
+  // epilogue of co tile ct after the compute of chunk buffers b; the partials travel
+  // through the consumed buffers patch[b] (tile rows 0, 1) and weights[b] (rows 2, 3): per
+  // pass 2 accumulator elements r, 16 KiB per tile row laid out
+  // [writer half][rr][float4 group][lane] (conflict-free 16-B accesses)
+  auto epilogue = [&](int ct, int b) {
+    __syncthreads();  // every wave is done reading patch[b] / weights[b]
+    float* xb = (wr < 2 ? smem + b * kW4PATCH : wl + b * kW4WCH) + (wr & 1) * 4096;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      float own[2][16];
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        float y0v[16], y1v[16];
+        partial(0, 2 * pass + rr, y0v);
+        partial(1, 2 * pass + rr, y1v);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) own[rr][v] = ph ? y1v[v] : y0v[v];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          float4 o4;
+          o4.x = ph ? y0v[4 * g4] : y1v[4 * g4];
+          o4.y = ph ? y0v[4 * g4 + 1] : y1v[4 * g4 + 1];
+          o4.z = ph ? y0v[4 * g4 + 2] : y1v[4 * g4 + 2];
+          o4.w = ph ? y0v[4 * g4 + 3] : y1v[4 * g4 + 3];
+          *reinterpret_cast<float4*>(xb + (((ph * 2 + rr) * 4 + g4) * 64 + lane) * 4) = o4;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 o4 =
+              *reinterpret_cast<const float4*>(xb + ((((1 - ph) * 2 + rr) * 4 + g4) * 64 + lane) * 4);
+          own[rr][4 * g4] += o4.x;
+          own[rr][4 * g4 + 1] += o4.y;
+          own[rr][4 * g4 + 2] += o4.z;
+          own[rr][4 * g4 + 3] += o4.w;
+        }
+        finish(ct * kW4BM + 16 * ph + 4 * k + 2 * pass + rr, own[rr]);
+      }
+      if (pass == 0) __syncthreads();  // pass 1 overwrites the exchange buffer
+    }
+  };
+
   // ---- pipeline: chunk g computes from buffers g & 1 while chunk g + 1 is fetched -------
-  load(0);
+  load(0, smem);
   wdma(ct0, 0, wl);
   store(0, smem);
   for (int g = 0; g < G; ++g) {
     const int b = g & 1;
-    __syncthreads();  // chunk g's patch and weights are in LDS; buffers b ^ 1 are free
+    if (!(DBG & 16)) __syncthreads();  // chunk g's patch and weights are in LDS; b ^ 1 free
     const int gn = g + 1;
     const bool more = gn < G;
     const int ctn = ct0 + gn / nch, cn = gn % nch;
     if (more) {
-      load(cn);
+      load(cn, smem + (b ^ 1) * kW4PATCH);
       wdma(ctn, cn, wl + (b ^ 1) * kW4WCH);
     }
     compute(smem + b * kW4PATCH, wl + b * kW4WCH);
     if (gn % nch == 0) {
-      epilogue(ct0 + g / nch);
+      if (!(DBG & 32) || a.N < 0) epilogue(ct0 + g / nch, b);
 #pragma unroll
-      for (int x = 0; x < 36; ++x) acc[x] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
     if (more) store(cn, smem + (b ^ 1) * kW4PATCH);
   }
@@ -407,6 +522,19 @@ int wino4_launch(ConvArgs& a, int in_op, hipStream_t st) {
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.N * (a.persist ? 1 : a.co_tiles);
   RPST_REQUIRE(blocks <= 0x7fffffffLL, "conv2d: grid too large");
   const unsigned nb = (unsigned)blocks;
+  const char* dbg = getenv("RPST_WINO4_DBG");
+  if (dbg && *dbg && in_op == RPST_IN_NONE && a.persist) {
+    switch (atoi(dbg)) {
+#define RPST_W4_DBGCASE(D) \
+  case D: wino4_mfma_kernel<RPST_IN_NONE, true, D><<<nb, kW4NTH, 0, st>>>(a); break;
+      RPST_W4_DBGCASE(1) RPST_W4_DBGCASE(2) RPST_W4_DBGCASE(4) RPST_W4_DBGCASE(8)
+      RPST_W4_DBGCASE(16) RPST_W4_DBGCASE(32) RPST_W4_DBGCASE(64) RPST_W4_DBGCASE(7)
+      RPST_W4_DBGCASE(23) RPST_W4_DBGCASE(87) RPST_W4_DBGCASE(95) RPST_W4_DBGCASE(256)
+#undef RPST_W4_DBGCASE
+      default: break;
+    }
+    return launch_status("wino4_mfma_kernel(debug)");
+  }
 #define RPST_W4_GO(OP)                                                                     \
   (a.persist ? (void)(wino4_mfma_kernel<OP, true><<<nb, kW4NTH, 0, st>>>(a))                \
              : (void)(wino4_mfma_kernel<OP, false><<<nb, kW4NTH, 0, st>>>(a)))

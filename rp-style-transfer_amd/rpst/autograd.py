@@ -143,6 +143,16 @@ def _rp_backward(steps, saved, g, grads: Dict[int, torch.Tensor], need_input_gra
 class _AdaINRPStep(torch.autograd.Function):
     @staticmethod
     def forward(ctx, content, style, model, cw, sw, *params):
+        with ops.precise_convs():
+            return _AdaINRPStep._forward(ctx, content, style, model, cw, sw, *params)
+
+    @staticmethod
+    def backward(ctx, g_total, g_ls, g_lc):
+        with ops.precise_convs():  # the autograd engine runs this on its own thread
+            return _AdaINRPStep._backward(ctx, g_total, g_ls, g_lc)
+
+    @staticmethod
+    def _forward(ctx, content, style, model, cw, sw, *params):
         n = content.shape[0]
         enc_steps = plan.compile_layers(model.rp_shared_encoder.children())
         dec_steps = plan.compile_layers(model.rp_decoder.children())
@@ -188,7 +198,7 @@ class _AdaINRPStep(torch.autograd.Function):
         return total, ls, lc
 
     @staticmethod
-    def backward(ctx, g_total, g_ls, g_lc):
+    def _backward(ctx, g_total, g_ls, g_lc):
         dev = ctx.content4.device
         zero = torch.zeros((), device=dev)
         g_total = zero if g_total is None else g_total

@@ -183,6 +183,19 @@ def _conv_name(ksize, cin, cout, hs, ws, n, in_op):
     return f"{algo}{ksize}x{ksize} {cin}->{cout} {h}x{w} N{n} op{in_op}"
 
 
+class precise_convs:
+    """Context manager: this thread's convolutions avoid F(4x4,3x3) (rpst_conv2d_set_precise,
+    include/rpst.h) — used by the training step, whose gradients pass ~30 convolutions."""
+
+    def __enter__(self):
+        self._old = _lib.load().rpst_conv2d_set_precise(1)
+        return self
+
+    def __exit__(self, *exc):
+        _lib.load().rpst_conv2d_set_precise(self._old)
+        return False
+
+
 def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], cout: int,
            ksize: int, pad: int = PAD_ZERO, in_op: int = IN_NONE, relu: bool = False,
            aux: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
@@ -230,7 +243,7 @@ def conv2d_skip_adain(x: torch.Tensor, content: torch.Tensor, params: torch.Tens
     assert params.numel() == 4 * n * cin, "params = [mean_c|mean_s|std_c|std_s]"
     if out is None:
         out = torch.empty((n, cout, h, w), device=x.device, dtype=torch.float32)
-    with _traced(_conv_name(ksize, cin, cout, hs, ws, n, IN_ADD_ADAIN),
+    with _traced(_conv_name(ksize, cin, cout, h, w, n, IN_ADD_ADAIN),
                  2.0 * n * cout * h * w * cin * ksize * ksize,
                  4.0 * (2 * x.numel() + n * cout * h * w)):
         _lib.call("rpst_conv2d_skip_adain", x.data_ptr(), content.data_ptr(), params.data_ptr(),

@@ -83,3 +83,28 @@ def test_cpu_tensors_raise_no_fallback():
     m = net.AdaINRPNet({"rp_blocks": 3, "hidden_dim": 2}, net.vgg)
     with pytest.raises(RuntimeError, match="ROCm GPU"):
         m.test(torch.rand(1, 3, 8, 8), torch.rand(1, 3, 8, 8))
+
+
+def test_conv_algorithm_choice_is_host_only(monkeypatch):
+    """rpst_conv2d_algorithm: F(4x4) for the NONE / ADAIN / UPSAMPLE2 loaders with >= 16
+    input channels, F(2x2) for the other 3x3 layers with Cout >= 32, direct otherwise;
+    precise mode (training) and RPST_CONV_ALGO override."""
+    monkeypatch.delenv("RPST_CONV_ALGO", raising=False)
+    lib = _lib.load()
+    D, W2, W4 = 0, 1, 2
+    assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == W4
+    assert lib.rpst_conv2d_algorithm(128, 256, 512, 512, 3, 4) == W4   # AdaIN-in-loader
+    assert lib.rpst_conv2d_algorithm(256, 256, 32, 32, 3, 2) == W4     # upsample
+    assert lib.rpst_conv2d_algorithm(128, 64, 64, 64, 3, 1) == W2      # max-pool loader
+    assert lib.rpst_conv2d_algorithm(64, 3, 512, 512, 3, 0) == W2
+    assert lib.rpst_conv2d_algorithm(16, 3, 512, 512, 3, 0) == D
+    assert lib.rpst_conv2d_algorithm(16, 32, 512, 512, 3, 0) == W4
+    assert lib.rpst_conv2d_algorithm(512, 512, 64, 64, 1, 0) == D
+    old = lib.rpst_conv2d_set_precise(1)
+    try:
+        assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == W2
+    finally:
+        lib.rpst_conv2d_set_precise(old)
+    assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == W4
+    monkeypatch.setenv("RPST_CONV_ALGO", "direct")
+    assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == D

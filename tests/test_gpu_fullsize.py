@@ -96,8 +96,12 @@ def test_samodel_512(cuda):
     assert max_abs_ratio(out, ref) < TOL_NET_MAXABS
 
 
-def test_conv_128_256_full_res(cuda):
-    """The dominant layer at full resolution against a float64 CPU reference."""
+@pytest.mark.parametrize("algo", ["winograd4", "winograd", "direct"])
+def test_conv_128_256_full_res(cuda, algo, monkeypatch):
+    """The dominant layer at full resolution against a float64 CPU reference, on every
+    algorithm: the single-conv bar is 1e-5 rel-L2 (tests/helpers.py); the F(4x4,3x3)
+    transforms (coefficients up to 8) leave ~1.1e-6 in fp32, F(2x2) and direct ~4e-7."""
+    monkeypatch.setenv("RPST_CONV_ALGO", algo)
     import torch.nn.functional as F
     from rpst import ops
     g = torch.Generator().manual_seed(3)
@@ -106,4 +110,4 @@ def test_conv_128_256_full_res(cuda):
     b = (torch.rand((256,), generator=g) - 0.5) * 0.1
     out = ops.conv2d(x.to(cuda), ops.pack_conv_weight(w.to(cuda)), b.to(cuda), 256, 3, relu=True)
     ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), padding=1))
-    assert rel_l2(out, ref) < 1e-6
+    assert rel_l2(out, ref) < (2e-6 if algo == "winograd4" else 1e-6)
