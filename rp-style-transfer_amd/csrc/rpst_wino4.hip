@@ -39,13 +39,16 @@ constexpr int kW4CK = 8;                   // input channels per chunk
 constexpr int kW4BM = 32;                  // output channels per co tile
 constexpr int kW4TH = 16, kW4TW = 64;      // output rows x columns per block
 constexpr int kW4PH = kW4TH + 2;           // patch rows
-constexpr int kW4PS = 66;                  // patch row stride (floats): rows are contiguous
-constexpr int kW4CS = 1218;                // channel stride: >= 19 x 64 (LDS-DMA pieces), = 2 mod 4
-constexpr int kW4DMA = 19;                 // 64-float LDS-DMA pieces per patch channel
+constexpr int kW4PS = 68;                  // patch row stride (floats): 66 columns + 2 spare
+constexpr int kW4CS = 1280;                // channel stride (floats)
+constexpr int kW4DMA = 20;                 // 4-B LDS-DMA pieces per patch channel (64 floats)
+constexpr int kW4DMA4 = 5;                 // 16-B pieces (256 floats) on interior blocks
 constexpr int kW4PATCH = kW4CK * kW4CS;    // floats per patch buffer
 constexpr int kW4WCH = 36 * kW4BM * kW4CK; // weight floats per (co tile, chunk) = 9216
 constexpr int kW4NTH = 512;
 static_assert(kW4PH * kW4PS <= kW4DMA * 64 && kW4DMA * 64 <= kW4CS, "patch channel pieces");
+static_assert(kW4PH * kW4PS <= kW4DMA4 * 256 && kW4DMA4 * 256 <= kW4CS && kW4PS % 4 == 0,
+              "16-B pieces never straddle a patch row");
 static_assert(kW4WCH % (64 * 4) == 0, "weight slice = whole 1-KiB LDS-DMA pieces");
 
 // ---- weight transform + packing -------------------------------------------------------
@@ -194,24 +197,39 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.wpk, (short)0, (int)((unsigned)(a.co_tiles * nch * kW4WCH) * 4u), 0x00020000);
 
-  // ---- patch of one chunk: channel cg = wave, [18 rows][66 columns] contiguous at stride
-  // 1218. One-load operators (NONE, UPSAMPLE2) stream it by LDS-DMA: lane l of piece i
-  // fetches patch element 64 i + l; ADAIN stages through registers (lane -> column 1 + lane
-  // of every row, lanes < 36 one halo element) to apply its affine inside the image.
+  // ---- patch of one chunk: channel cg = wave, [18 rows][68] (66 columns + 2 spare) at
+  // channel stride 1280. One-load operators (NONE, UPSAMPLE2) stream it by LDS-DMA: on
+  // interior blocks (every patch column inside the image, no upsampling) lane l of piece
+  // i < 5 fetches the 16 B of patch elements 4 (64 i + l) ..+3 (68 = 4 x 17: a piece never
+  // straddles a row; the source is only 4-B aligned); elsewhere lane l of piece i < 20
+  // fetches element 64 i + l, resolved against the padding. Offsets are computed once per
+  // block. ADAIN stages through registers (lane -> column 1 + lane of every row, lanes < 36
+  // one halo element) to apply its affine.
   const int cg = wave;
   const bool zp = a.pad == RPST_PAD_ZERO;
   const int rs = pooled ? a.Ws : a.W;  // source row stride
   constexpr bool kDMA = INOP != RPST_IN_ADAIN;
   unsigned poff[kDMA ? kW4DMA : 1];
+  const bool wide = kDMA && !pooled && x0 >= 1 && x0 + kW4TW < a.W;
   if constexpr (kDMA) {
+    if (wide) {
+#pragma unroll
+      for (int i = 0; i < kW4DMA4; ++i) {
+        const int f = 64 * i + lane, row = min(f / 17, kW4PH - 1), j = f - (f / 17) * 17;
+        int y = y0 - 1 + row;
+        const bool ok = f < kW4PH * 17 && resolve_bf(y, a.H, zp);
+        poff[i] = ok ? ((unsigned)(y * rs) + (unsigned)(x0 - 1 + 4 * j)) * 4u : oob;
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < kW4DMA; ++i) {
       const int f = 64 * i + lane;
       const int row = min(f / kW4PS, kW4PH - 1), col = f - (f / kW4PS) * kW4PS;
       int y = y0 - 1 + row, x = x0 - 1 + col;
-      const bool ok = resolve_bf(y, a.H, zp) & resolve_bf(x, a.W, zp);
+      const bool ok = col < kW4TW + 2 && resolve_bf(y, a.H, zp) & resolve_bf(x, a.W, zp);
       poff[i] = ok ? ((unsigned)((pooled ? y >> 1 : y) * rs) + (unsigned)(pooled ? x >> 1 : x)) * 4u
                    : oob;
+    }
     }
   }
   int bx = x0 + lane;
@@ -234,10 +252,17 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     if constexpr (kDMA) {
       const int so = __builtin_amdgcn_readfirstlane((int)(ch * in_plane * 4u));
       float* xs = pbuf + cg * kW4CS;
+      if (wide) {
 #pragma unroll
-      for (int i = 0; i < kW4DMA; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(xs + 64 * i), 4, (int)poff[i],
-                                                 so, 0, 0);
+        for (int i = 0; i < kW4DMA4; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(xs + 256 * i), 16,
+                                                   (int)poff[i], so, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < kW4DMA; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(xs + 64 * i), 4,
+                                                   (int)poff[i], so, 0, 0);
+      }
     } else {
       const unsigned pb = ch * in_plane * 4u;  // >= the range for a padding channel
       const unsigned v0 = pb + cx;
@@ -301,15 +326,14 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
       float d[5][6];
 #pragma unroll
       for (int r = 0; r < 5; ++r) {
-        const float2 u0 = *reinterpret_cast<const float2*>(pr + r * kW4PS);
-        const float2 u1 = *reinterpret_cast<const float2*>(pr + r * kW4PS + 2);
-        const float2 u2 = *reinterpret_cast<const float2*>(pr + r * kW4PS + 4);
-        d[r][0] = u0.x;
-        d[r][1] = u0.y;
-        d[r][2] = u1.x;
-        d[r][3] = u1.y;
-        d[r][4] = u2.x;
-        d[r][5] = u2.y;
+        const float4 u = *reinterpret_cast<const float4*>(pr + r * kW4PS);
+        const float2 v = *reinterpret_cast<const float2*>(pr + r * kW4PS + 4);
+        d[r][0] = u.x;
+        d[r][1] = u.y;
+        d[r][2] = u.z;
+        d[r][3] = u.w;
+        d[r][4] = v.x;
+        d[r][5] = v.y;
       }
       // rows 3ph..3ph+2 of B^T d (d[r] = input row ph + r), then B along each row
       float t[3][6];
