@@ -16,6 +16,8 @@ The JSON line also carries:
                its mean launch time, measured with HIP events on the launch stream
                during the timed steps, against the MI355X peak;
   roofline_adain  the same for the AdaIN statistics+apply path (HBM-bound);
+  roofline_adain_stats  calc_mean_std alone (the AdaIN statistics path: one read of the
+               feature, 4 B per element) against the HBM peak;
   cpu_baseline the CPU oracle (PyTorch-CPU restatement of the reference) timed on this
                host on a bounded sample (rank 0, N=1 only).
 """
@@ -210,14 +212,29 @@ def measure_adain_standalone(dev, n, c, hw, reps=3):
     y = torch.rand((n, c, hw), device=dev, generator=g).view(n, c, hw, 1)
     out = torch.empty_like(x)
     ops.adaptive_instance_normalization(x, y, out=out)
+    ops.calc_mean_std(x)
     ops.TRACE = ops.Trace()
     for _ in range(reps):
         ops.adaptive_instance_normalization(x, y, out=out)
+    for _ in range(reps):
+        ops.calc_mean_std(x)
     summary = ops.TRACE.summary()
     ops.TRACE = None
     del x, y, out
     torch.cuda.empty_cache()
     return summary
+
+
+def stats_roofline(summary):
+    for name, a in summary.items():
+        if name.startswith("stats"):
+            avg_ms = a["ms"] / a["launches"]
+            gbs = a["bytes"] / (avg_ms * 1e-3) / 1e9
+            return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                    "kernel": f"plane_stats_kernel + stat merge [{name}]",
+                    "launch_ms": round(avg_ms, 4), "bytes_per_launch": a["bytes"]}
+    return None
 
 
 def adain_roofline(summary):
@@ -318,10 +335,11 @@ def main():
                                        "all-reduce per step") if args.model == "train" else
                        f"per-image batch split over {world} GPU(s), no collectives"},
             "roofline": roofline_from_trace(summary),
-            "roofline_adain": adain_roofline(
-                summary if any(k.startswith("adain") for k in summary)
-                else measure_adain_standalone(dev, B, 256, args.size * args.size)),
         }
+        adain_summary = measure_adain_standalone(dev, B, 256, args.size * args.size)
+        rec["roofline_adain"] = adain_roofline(
+            summary if any(k.startswith("adain") for k in summary) else adain_summary)
+        rec["roofline_adain_stats"] = stats_roofline(adain_summary)
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(args.model, args.size)
         else:

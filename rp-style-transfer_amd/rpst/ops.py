@@ -108,8 +108,9 @@ def calc_mean_std(feat: torch.Tensor, eps: float = 1e-5) -> Tuple[torch.Tensor, 
     hw = feat.numel() // (N * C)
     mean = torch.empty((N, C, 1, 1), device=feat.device, dtype=torch.float32)
     std = torch.empty_like(mean)
-    _lib.call("rpst_calc_mean_std", feat.data_ptr(), mean.data_ptr(), std.data_ptr(),
-              N, C, hw, eps, _stream(feat))
+    with _traced(f"stats C{C} {hw}px N{N}", 0.0, 4.0 * N * C * hw):
+        _lib.call("rpst_calc_mean_std", feat.data_ptr(), mean.data_ptr(), std.data_ptr(),
+                  N, C, hw, eps, _stream(feat))
     return mean, std
 
 

@@ -136,6 +136,8 @@ CONV_CASES = [
     (1, 40, 37, 70, 72, 3, 0, 0, True),     # ragged 16x64 F(4x4) blocks, 3 co tiles, 5 chunks
     (1, 24, 18, 130, 40, 3, 1, 0, False),   # reflect, W % 4 != 0
     (2, 16, 9, 35, 64, 3, 1, 2, True),      # upsample of an odd source
+    (2, 64, 33, 130, 96, 3, 0, 0, True),    # F(4x4) interior (16-B DMA) block + edges, ragged H
+    (1, 32, 20, 200, 64, 3, 1, 0, False),   # reflect: two interior blocks, partial last block
 ]
 
 
@@ -284,7 +286,7 @@ def test_vgg_and_decoder_golden(cuda, golden):
 
 # ---- fused AdaIN (statistics in the producing conv's epilogue, apply in the consumer's loader)
 @pytest.mark.parametrize("shape", [(2, 16, 64, 96, 256), (1, 8, 17, 45, 64), (3, 3, 9, 7, 32),
-                                   (2, 64, 40, 40, 128)])
+                                   (2, 64, 40, 40, 128), (2, 32, 40, 200, 64)])
 def test_conv2d_stats_equal_calc_mean_std(cuda, shape, conv_algo):
     from rpst import ops
     n, cin, h, w, cout = shape
