@@ -43,8 +43,13 @@ constexpr int kW4PS = 68;                  // patch row stride (floats): 66 colu
 constexpr int kW4CS = 1280;                // channel stride (floats)
 constexpr int kW4DMA = 20;                 // 4-B LDS-DMA pieces per patch channel (64 floats)
 constexpr int kW4DMA4 = 5;                 // 16-B pieces (256 floats) on interior blocks
-constexpr int kW4PATCH = kW4CK * kW4CS;    // floats per patch buffer
-constexpr int kW4WCH = 36 * kW4BM * kW4CK; // weight floats per (co tile, chunk) = 9216
+constexpr int kW4WCH = 36 * kW4BM * kW4CK; // weight floats per (co tile, 8-channel chunk) = 9216
+// LDS ring of 4 stages, one K step (4 input channels) each: patch [4][1280] + weights
+// [2 halves][9][64 lanes][4] = 4608; plus a 1 KiB target for the padding DMA pieces
+constexpr int kW4STG = 4;
+constexpr int kW4SPATCH = 4 * kW4CS;       // 5120
+constexpr int kW4SW = kW4WCH / 2;          // 4608
+constexpr int kW4STAGE = kW4SPATCH + kW4SW;  // 9728 floats = 38 KiB
 constexpr int kW4NTH = 512;
 static_assert(kW4PH * kW4PS <= kW4DMA * 64 && kW4DMA * 64 <= kW4CS, "patch channel pieces");
 static_assert(kW4PH * kW4PS <= kW4DMA4 * 256 && kW4DMA4 * 256 <= kW4CS && kW4PS % 4 == 0,
@@ -164,8 +169,14 @@ __device__ __forceinline__ bool resolve_bf(int& v, int n, bool zero_pad) {
 template <int INOP, bool PERSIST, int DBG = 0>
 __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   static_assert(RawN<INOP>::R == 1, "one raw load per patch element");
-  __shared__ __attribute__((aligned(16))) float smem[2 * kW4PATCH + 2 * kW4WCH];
-  float* const wl = smem + 2 * kW4PATCH;
+  // one __shared__ object per ring stage: the stage a K step reads and the one its DMA
+  // fills are then distinct objects, so the compiler's wait insertion does not drain the
+  // in-flight DMA before every LDS read (the loop below is unrolled by the ring size)
+  __shared__ __attribute__((aligned(16))) float smem0[kW4STAGE];
+  __shared__ __attribute__((aligned(16))) float smem1[kW4STAGE];
+  __shared__ __attribute__((aligned(16))) float smem2[kW4STAGE];
+  __shared__ __attribute__((aligned(16))) float smem3[kW4STAGE];
+  __shared__ __attribute__((aligned(16))) float dummy[256];  // target of padding DMA pieces
 
   // block -> (column tile, row tile, image), XCD-swizzled (neighbouring spatial tiles share
   // halo rows and every block of an XCD streams the same weight slices through its L2)
@@ -179,7 +190,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   const int ty = bid % a.tiles_y;
   const int n = bid / a.tiles_y;
   const int nct = PERSIST ? a.co_tiles : 1;
-  const int nch = a.nchunks, G = nct * nch;
+  const int nch = a.nchunks, K4 = 2 * nch, G = nct * K4;  // K steps per co tile / in total
   const int y0 = ty * kW4TH, x0 = tx * kW4TW;
 
   const int tid = threadIdx.x;
@@ -194,116 +205,131 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   const unsigned oob = a.Cin * in_plane * 4u;
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.in + (int64_t)n * a.Cin * in_plane), (short)0, (int)oob, 0x00020000);
+  const unsigned wbytes = (unsigned)(a.co_tiles * nch * kW4WCH) * 4u;
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.wpk, (short)0, (int)((unsigned)(a.co_tiles * nch * kW4WCH) * 4u), 0x00020000);
+      (void*)a.wpk, (short)0, (int)wbytes, 0x00020000);
 
-  // ---- patch of one chunk: channel cg = wave, [18 rows][68] (66 columns + 2 spare) at
-  // channel stride 1280. One-load operators (NONE, UPSAMPLE2) stream it by LDS-DMA: on
-  // interior blocks (every patch column inside the image, no upsampling) lane l of piece
-  // i < 5 fetches the 16 B of patch elements 4 (64 i + l) ..+3 (68 = 4 x 17: a piece never
-  // straddles a row; the source is only 4-B aligned); elsewhere lane l of piece i < 20
-  // fetches element 64 i + l, resolved against the padding. Offsets are computed once per
-  // block. ADAIN stages through registers (lane -> column 1 + lane of every row, lanes < 36
-  // one halo element) to apply its affine.
-  const int cg = wave;
+  // ---- patch of one K step: 4 channels, [18 rows][68] (66 columns + 2 spare) at channel
+  // stride 1280; wave w fills half w & 1 of channel w >> 1. One-load operators (NONE,
+  // UPSAMPLE2) stream it by LDS-DMA: on interior blocks (every patch column inside the
+  // image, no upsampling) piece p < 5 of a channel = 16 B per lane of patch elements
+  // 4 (64 p + l)..+3 (68 = 4 x 17: a piece never straddles a row; the source is only 4-B
+  // aligned), half 0 taking pieces 0-2, half 1 pieces 3-4 (+ one padding piece); elsewhere
+  // 20 pieces of 4 B per lane (element 64 p + l resolved against the padding), 10 per half.
+  // Offsets are computed once per block. ADAIN stages through registers (half h: rows
+  // 9h..9h+8, lane -> column x0 + lane; lanes < 18 one halo element) to apply its affine.
+  const int chl = wave >> 1, hf = wave & 1;
   const bool zp = a.pad == RPST_PAD_ZERO;
   const int rs = pooled ? a.Ws : a.W;  // source row stride
   constexpr bool kDMA = INOP != RPST_IN_ADAIN;
-  unsigned poff[kDMA ? kW4DMA : 1];
+  constexpr int kSlow = 10;
+  unsigned poff[kDMA ? kSlow : 1];
   const bool wide = kDMA && !pooled && x0 >= 1 && x0 + kW4TW < a.W;
   if constexpr (kDMA) {
     if (wide) {
 #pragma unroll
-      for (int i = 0; i < kW4DMA4; ++i) {
-        const int f = 64 * i + lane, row = min(f / 17, kW4PH - 1), j = f - (f / 17) * 17;
+      for (int i = 0; i < 3; ++i) {
+        const int p = 3 * hf + i;
+        const int f = 64 * p + lane, row = min(f / 17, kW4PH - 1), j = f - (f / 17) * 17;
         int y = y0 - 1 + row;
-        const bool ok = f < kW4PH * 17 && resolve_bf(y, a.H, zp);
+        const bool ok = p < kW4DMA4 && f < kW4PH * 17 && resolve_bf(y, a.H, zp);
         poff[i] = ok ? ((unsigned)(y * rs) + (unsigned)(x0 - 1 + 4 * j)) * 4u : oob;
       }
     } else {
 #pragma unroll
-    for (int i = 0; i < kW4DMA; ++i) {
-      const int f = 64 * i + lane;
-      const int row = min(f / kW4PS, kW4PH - 1), col = f - (f / kW4PS) * kW4PS;
-      int y = y0 - 1 + row, x = x0 - 1 + col;
-      const bool ok = col < kW4TW + 2 && resolve_bf(y, a.H, zp) & resolve_bf(x, a.W, zp);
-      poff[i] = ok ? ((unsigned)((pooled ? y >> 1 : y) * rs) + (unsigned)(pooled ? x >> 1 : x)) * 4u
-                   : oob;
-    }
+      for (int i = 0; i < kSlow; ++i) {
+        const int f = 64 * (kSlow * hf + i) + lane;
+        const int row = min(f / kW4PS, kW4PH - 1), col = f - (f / kW4PS) * kW4PS;
+        int y = y0 - 1 + row, x = x0 - 1 + col;
+        const bool ok = col < kW4TW + 2 && resolve_bf(y, a.H, zp) & resolve_bf(x, a.W, zp);
+        poff[i] = ok ? ((unsigned)((pooled ? y >> 1 : y) * rs) + (unsigned)(pooled ? x >> 1 : x)) * 4u
+                     : oob;
+      }
     }
   }
   int bx = x0 + lane;
   const bool okx = resolve_bf(bx, a.W, zp);
   const unsigned cx = okx ? (unsigned)bx * 4u : oob;
-  const bool has_halo = lane < 2 * kW4PH;
-  const int hrw = lane >> 1;  // halo patch row
+  const bool has_halo = lane < kW4PH;
+  const int hrw = 9 * hf + (lane >> 1);  // halo patch row (lanes < 18)
   int hy = y0 - 1 + (has_halo ? hrw : 0), hx = (lane & 1) ? x0 + kW4TW : x0 - 1;
   const bool h_ok = has_halo && resolve_bf(hy, a.H, zp) && resolve_bf(hx, a.W, zp);
   const unsigned hoff = h_ok ? ((unsigned)(hy * rs) + (unsigned)hx) * 4u : oob;
   const int hcol = (lane & 1) ? kW4TW + 1 : 0;
 
-  float X[kDMA ? 1 : kW4PH + 1];
+  float X[kDMA ? 1 : 10];
   AdainP ap{};
 
-  // chunk c's patch into pbuf: LDS-DMA pieces, or register loads (written by store())
-  auto load = [&](int c, float* pbuf) {
-    const unsigned ch = (unsigned)(c * kW4CK + cg);
-    if (DBG & 1) return;
+  // K step g (co tile ct0 + g / K4, channels 4 (g % K4)..+3): weight slice (18 pieces of
+  // 1 KiB, pieces w, w + 8, w + 16 of wave w) and patch into its stage by LDS-DMA; every
+  // wave issues the same number of pieces per step (the padding ones read out of range
+  // into the dummy target), so the ring's waits are counted: kPer per step
+  auto issue = [&](int g, float* st) {
+    const int ct = ct0 + g / K4, ks = g - (g / K4) * K4;
+    if (!(DBG & 2)) {
+      const unsigned base = (unsigned)(ct * K4 + ks) * (unsigned)kW4SW * 4u + (unsigned)lane * 16u;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int p = wave + 8 * i;
+        const bool real = p < 18;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rw, (lds_ptr_t)(real ? st + kW4SPATCH + p * 256 : dummy), 16,
+            (int)(real ? base + (unsigned)p * 1024u : wbytes), 0, 0, 0);
+      }
+    }
     if constexpr (kDMA) {
+      if (DBG & 1) return;
+      const unsigned ch = (unsigned)(4 * ks + chl);
       const int so = __builtin_amdgcn_readfirstlane((int)(ch * in_plane * 4u));
-      float* xs = pbuf + cg * kW4CS;
+      float* xs = st + chl * kW4CS;
       if (wide) {
 #pragma unroll
-        for (int i = 0; i < kW4DMA4; ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(xs + 256 * i), 16,
-                                                   (int)poff[i], so, 0, 0);
+        for (int i = 0; i < 3; ++i) {
+          const int p = 3 * hf + i;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rin, (lds_ptr_t)(p < kW4DMA4 ? xs + 256 * p : dummy), 16, (int)poff[i], so, 0, 0);
+        }
       } else {
 #pragma unroll
-        for (int i = 0; i < kW4DMA; ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(xs + 64 * i), 4,
-                                                   (int)poff[i], so, 0, 0);
+        for (int i = 0; i < kSlow; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(xs + 64 * (kSlow * hf + i)),
+                                                   4, (int)poff[i], so, 0, 0);
       }
-    } else {
+    }
+  };
+  // ADAIN: register loads of K step g's patch half, and their store with the affine
+  // ((v - mean_c) / std_c) * std_s + mean_s inside the image (0 at padding positions)
+  auto load = [&](int g) {
+    if constexpr (!kDMA) {
+      const int ks = g - (g / K4) * K4;
+      const unsigned ch = (unsigned)(4 * ks + chl);
       const unsigned pb = ch * in_plane * 4u;  // >= the range for a padding channel
-      const unsigned v0 = pb + cx;
       ap = adain_params(a.aux, n, (int)ch, a);
+      if (DBG & 1) return;
 #pragma unroll
-      for (int py = 0; py < kW4PH; ++py) {
-        int y = y0 - 1 + py;
+      for (int r = 0; r < 9; ++r) {
+        int y = y0 - 1 + 9 * hf + r;
         const bool yok = resolve_bf(y, a.H, zp);
         const int ro = __builtin_amdgcn_readfirstlane(yok ? (int)(y * rs * 4) : (int)oob);
-        X[py] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (int)v0, ro, 0));
+        X[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (int)(pb + cx), ro, 0));
       }
-      X[kW4PH] =
-          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (int)(pb + hoff), 0, 0));
+      X[9] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (int)(pb + hoff), 0, 0));
     }
   };
-  // ADAIN: ((v - mean_c) / std_c) * std_s + mean_s inside the image, 0 at padding positions
-  auto store = [&](int c, float* pbuf) {
+  auto store = [&](int g, float* st) {
     if constexpr (!kDMA) {
       if (DBG & 4) return;
-      float* xs = pbuf + cg * kW4CS;
-      const bool chok = c * kW4CK + cg < a.Cin;
+      const int ks = g - (g / K4) * K4;
+      float* xs = st + chl * kW4CS;
+      const bool chok = 4 * ks + chl < a.Cin;
 #pragma unroll
-      for (int py = 0; py < kW4PH; ++py) {
-        int y = y0 - 1 + py;
+      for (int r = 0; r < 9; ++r) {
+        int y = y0 - 1 + 9 * hf + r;
         const bool rok = chok && resolve_bf(y, a.H, zp) && okx;
-        xs[py * kW4PS + 1 + lane] = rok ? fmaf(X[py] - ap.mc, ap.scale, ap.ms) : 0.f;
+        xs[(9 * hf + r) * kW4PS + 1 + lane] = rok ? fmaf(X[r] - ap.mc, ap.scale, ap.ms) : 0.f;
       }
-      const float hv = (chok && h_ok) ? fmaf(X[kW4PH] - ap.mc, ap.scale, ap.ms) : 0.f;
+      const float hv = (chok && h_ok) ? fmaf(X[9] - ap.mc, ap.scale, ap.ms) : 0.f;
       if (has_halo) xs[hrw * kW4PS + hcol] = hv;
-    }
-  };
-  // weight slice of (co tile ct, chunk c) -> LDS by LDS-DMA: 36 pieces of 1 KiB over 8 waves
-  auto wdma = [&](int ct, int c, float* wbuf) {
-    if (DBG & 2) return;
-    const unsigned base = (unsigned)((ct * nch + c) * kW4WCH) * 4u + (unsigned)lane * 16u;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      const int p = wave + 8 * i;
-      if (i < 4 || p < 36)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(wbuf + p * 256), 16,
-                                                 (int)(base + (unsigned)p * 1024u), 0, 0, 0);
     }
   };
 
@@ -311,18 +337,17 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
 #pragma unroll
   for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // one chunk: 2 K steps of 4 channels, each 72 VALU of input transform + 36 MFMAs
-  auto compute = [&](const float* pbuf, const float* wbuf) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const float* wq = wbuf + (s * 2 + ph) * 9 * 256 + lane * 4;
+  // one K step of 4 channels from a stage: 72 VALU of input transform + 36 MFMAs
+  auto compute = [&](const float* pbuf) {
+    {
+      const float* wq = pbuf + kW4SPATCH + ph * 9 * 256 + lane * 4;
       float4 w4[9];
 #pragma unroll
       for (int q = 0; q < 3; ++q)
         w4[q] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
                            : *reinterpret_cast<const float4*>(wq + q * 256);
       // input rows ph .. ph + 4 of this lane's 6x6 window
-      const float* pr = pbuf + (4 * s + k) * kW4CS + (4 * wr + ph) * kW4PS + 4 * tn;
+      const float* pr = pbuf + k * kW4CS + (4 * wr + ph) * kW4PS + 4 * tn;
       float d[5][6];
 #pragma unroll
       for (int r = 0; r < 5; ++r) {
@@ -374,7 +399,6 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         acc[p1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].z, v1, acc[p1][0], 0, 0, 0);
         acc[p1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].w, v1, acc[p1][1], 0, 0, 0);
       }
-      __builtin_amdgcn_sched_barrier(0);  // keep the next K step's reads below these MFMAs
     }
   };
 
@@ -461,23 +485,26 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     }
   };
 
-  // epilogue of co tile ct after the compute of chunk buffers b; the partials travel
-  // through the consumed buffers patch[b] (tile rows 0, 1) and weights[b] (rows 2, 3): per
-  // pass 2 accumulator elements r, 16 KiB per tile row laid out
-  // [writer half][rr][float4 group][lane] (conflict-free 16-B accesses)
-  auto epilogue = [&](int ct, int b) {
-    __syncthreads();  // every wave is done reading patch[b] / weights[b]
-    float* xb = (wr < 2 ? smem + b * kW4PATCH : wl + b * kW4WCH) + (wr & 1) * 4096;
+  // epilogue of co tile ct after the K step that used stage xs: the partials travel through
+  // that consumed stage, one accumulator element r per pass: 2 KiB-float region per tile
+  // row laid out [writer half][float4 group][lane] (conflict-free 16-B accesses). Raw
+  // barriers (LDS only): the DMA prefetch of the next steps stays in flight.
+  auto lds_barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  auto epilogue = [&](int ct, float* xs) {
+    lds_barrier();  // every wave is done reading the stage
+    float* xb = xs + wr * 2048;
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      float own[2][16];
-#pragma unroll
-      for (int rr = 0; rr < 2; ++rr) {
+    for (int r = 0; r < 4; ++r) {
+      float own[16];
+      {
         float y0v[16], y1v[16];
-        partial(0, 2 * pass + rr, y0v);
-        partial(1, 2 * pass + rr, y1v);
+        partial(0, r, y0v);
+        partial(1, r, y1v);
 #pragma unroll
-        for (int v = 0; v < 16; ++v) own[rr][v] = ph ? y1v[v] : y0v[v];
+        for (int v = 0; v < 16; ++v) own[v] = ph ? y1v[v] : y0v[v];
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           float4 o4;
@@ -485,48 +512,67 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
           o4.y = ph ? y0v[4 * g4 + 1] : y1v[4 * g4 + 1];
           o4.z = ph ? y0v[4 * g4 + 2] : y1v[4 * g4 + 2];
           o4.w = ph ? y0v[4 * g4 + 3] : y1v[4 * g4 + 3];
-          *reinterpret_cast<float4*>(xb + (((ph * 2 + rr) * 4 + g4) * 64 + lane) * 4) = o4;
+          *reinterpret_cast<float4*>(xb + ((ph * 4 + g4) * 64 + lane) * 4) = o4;
         }
       }
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr) {
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 o4 =
-              *reinterpret_cast<const float4*>(xb + ((((1 - ph) * 2 + rr) * 4 + g4) * 64 + lane) * 4);
-          own[rr][4 * g4] += o4.x;
-          own[rr][4 * g4 + 1] += o4.y;
-          own[rr][4 * g4 + 2] += o4.z;
-          own[rr][4 * g4 + 3] += o4.w;
-        }
-        finish(ct * kW4BM + 16 * ph + 4 * k + 2 * pass + rr, own[rr]);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 o4 =
+            *reinterpret_cast<const float4*>(xb + (((1 - ph) * 4 + g4) * 64 + lane) * 4);
+        own[4 * g4] += o4.x;
+        own[4 * g4 + 1] += o4.y;
+        own[4 * g4 + 2] += o4.z;
+        own[4 * g4 + 3] += o4.w;
       }
-      if (pass == 0) __syncthreads();  // pass 1 overwrites the exchange buffer
+      finish(ct * kW4BM + 16 * ph + 4 * k + r, own);
+      if (r < 3) lds_barrier();  // the next pass overwrites the exchange region
     }
   };
 
-  // ---- pipeline: chunk g computes from buffers g & 1 while chunk g + 1 is fetched -------
-  load(0, smem);
-  wdma(ct0, 0, wl);
-  store(0, smem);
-  for (int g = 0; g < G; ++g) {
-    const int b = g & 1;
-    if (!(DBG & 16)) __syncthreads();  // chunk g's patch and weights are in LDS; b ^ 1 free
-    const int gn = g + 1;
-    const bool more = gn < G;
-    const int ctn = ct0 + gn / nch, cn = gn % nch;
-    if (more) {
-      load(cn, smem + (b ^ 1) * kW4PATCH);
-      wdma(ctn, cn, wl + (b ^ 1) * kW4WCH);
+  // ---- pipeline: ring of 4 stages, K step g in stage g % 4, issued 3 steps ahead --------
+  // Before the barrier that opens step g each wave retires its own DMA pieces of step g
+  // with a counted vmcnt (the pieces of steps g + 1, g + 2 stay in flight; ADAIN's register
+  // loads drain everything at their use, so its count is only ever conservative).
+  constexpr int kPerW = 3;                                 // weight pieces per step and wave
+  const int per = kPerW + (kDMA ? (wide ? 3 : kSlow) : 0);  // all pieces per step and wave
+  auto wait_step = [&](int g) {
+    const int ahead = min(2, G - 1 - g);  // steps issued after g
+    const int allowed = ahead * per;
+    if (allowed >= 26) asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
+    else if (allowed >= 13) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+    else if (allowed >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (allowed >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (allowed >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  issue(0, smem0);
+  if (G > 1) issue(1, smem1);
+  if (G > 2) issue(2, smem2);
+  load(0);
+  store(0, smem0);
+  // K step g from stage `cur`; step g + 3's DMA into `nx3` (the stage step g - 1 used),
+  // step g + 1's ADAIN registers into `nx1`
+  auto step = [&](int g, float* cur, float* nx1, float* nx3) {
+    if (!(DBG & 16)) {
+      wait_step(g);
+      lds_barrier();  // step g's stage is complete; nx3 is free
     }
-    compute(smem + b * kW4PATCH, wl + b * kW4WCH);
-    if (gn % nch == 0) {
-      if (!(DBG & 32) || a.N < 0) epilogue(ct0 + g / nch, b);
+    if (g + 3 < G) issue(g + 3, nx3);
+    if (g + 1 < G) load(g + 1);
+    compute(cur);
+    if ((g + 1) % K4 == 0) {
+      if (!(DBG & 32) || a.N < 0) epilogue(ct0 + g / K4, cur);
 #pragma unroll
       for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
-    if (more) store(cn, smem + (b ^ 1) * kW4PATCH);
+    if (g + 1 < G) store(g + 1, nx1);
+  };
+  for (int g = 0; g < G; g += kW4STG) {
+    step(g, smem0, smem1, smem3);
+    if (g + 1 < G) step(g + 1, smem1, smem2, smem0);
+    if (g + 2 < G) step(g + 2, smem2, smem3, smem1);
+    if (g + 3 < G) step(g + 3, smem3, smem0, smem2);
   }
 }
 
