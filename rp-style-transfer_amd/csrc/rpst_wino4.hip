@@ -50,6 +50,7 @@ constexpr int kW4STG = 4;
 constexpr int kW4SPATCH = 4 * kW4CS;       // 5120
 constexpr int kW4SW = kW4WCH / 2;          // 4608
 constexpr int kW4STAGE = kW4SPATCH + kW4SW;  // 9728 floats = 38 KiB
+constexpr int kW4AffC = 512;               // ADAIN: input channels whose parameters fit LDS
 constexpr int kW4NTH = 512;
 static_assert(kW4PH * kW4PS <= kW4DMA * 64 && kW4DMA * 64 <= kW4CS, "patch channel pieces");
 static_assert(kW4PH * kW4PS <= kW4DMA4 * 256 && kW4DMA4 * 256 <= kW4CS && kW4PS % 4 == 0,
@@ -120,7 +121,7 @@ bool wino4_supports(int in_op) {
 // padding offsets (rpst_wino4 loader): (Cin + 8) planes + 2 x Cin planes < 2^32 bytes
 bool wino4_fits(int N, int Cin, int Hs, int Ws, int in_op) {
   (void)N;
-  (void)in_op;
+  if (in_op == RPST_IN_ADAIN && Cin > kW4AffC) return false;
   const int64_t plane = (int64_t)Hs * Ws * 4;
   return (int64_t)(3 * Cin + 8) * plane < (1LL << 32) - (1LL << 20);
 }
@@ -216,16 +217,17 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // 4 (64 p + l)..+3 (68 = 4 x 17: a piece never straddles a row; the source is only 4-B
   // aligned), half 0 taking pieces 0-2, half 1 pieces 3-4 (+ one padding piece); elsewhere
   // 20 pieces of 4 B per lane (element 64 p + l resolved against the padding), 10 per half.
-  // Offsets are computed once per block. ADAIN stages through registers (half h: rows
-  // 9h..9h+8, lane -> column x0 + lane; lanes < 18 one halo element) to apply its affine.
+  // Offsets are computed once per block. ADAIN streams the raw feature the same way and
+  // applies its affine in place (fix()) one step ahead: half h of a channel = rows
+  // 9h..9h+8 (lane -> column x0 + lane) and lanes < 18 one halo element of those rows.
   const int chl = wave >> 1, hf = wave & 1;
   const bool zp = a.pad == RPST_PAD_ZERO;
   const int rs = pooled ? a.Ws : a.W;  // source row stride
-  constexpr bool kDMA = INOP != RPST_IN_ADAIN;
+  constexpr bool kAff = INOP == RPST_IN_ADAIN;
   constexpr int kSlow = 10;
-  unsigned poff[kDMA ? kSlow : 1];
-  const bool wide = kDMA && !pooled && x0 >= 1 && x0 + kW4TW < a.W;
-  if constexpr (kDMA) {
+  unsigned poff[kSlow];
+  const bool wide = !pooled && x0 >= 1 && x0 + kW4TW < a.W;
+  {
     if (wide) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
@@ -249,16 +251,23 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   }
   int bx = x0 + lane;
   const bool okx = resolve_bf(bx, a.W, zp);
-  const unsigned cx = okx ? (unsigned)bx * 4u : oob;
   const bool has_halo = lane < kW4PH;
   const int hrw = 9 * hf + (lane >> 1);  // halo patch row (lanes < 18)
   int hy = y0 - 1 + (has_halo ? hrw : 0), hx = (lane & 1) ? x0 + kW4TW : x0 - 1;
   const bool h_ok = has_halo && resolve_bf(hy, a.H, zp) && resolve_bf(hx, a.W, zp);
-  const unsigned hoff = h_ok ? ((unsigned)(hy * rs) + (unsigned)hx) * 4u : oob;
   const int hcol = (lane & 1) ? kW4TW + 1 : 0;
-
-  float X[kDMA ? 1 : 10];
-  AdainP ap{};
+  // ADAIN: (mean_c, std_s / std_c, mean_s) of every input channel of image n, in LDS (its
+  // global loads happen before any DMA is in flight)
+  __shared__ float aparm[kAff ? 3 * kW4AffC : 1];
+  if constexpr (kAff) {
+    for (int c = tid; c < a.Cin; c += kW4NTH) {
+      const AdainP p = adain_params(a.aux, n, c, a);
+      aparm[c] = p.mc;
+      aparm[kW4AffC + c] = p.scale;
+      aparm[2 * kW4AffC + c] = p.ms;
+    }
+    __syncthreads();
+  }
 
   // K step g (co tile ct0 + g / K4, channels 4 (g % K4)..+3): weight slice (18 pieces of
   // 1 KiB, pieces w, w + 8, w + 16 of wave w) and patch into its stage by LDS-DMA; every
@@ -277,7 +286,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
             (int)(real ? base + (unsigned)p * 1024u : wbytes), 0, 0, 0);
       }
     }
-    if constexpr (kDMA) {
+    {
       if (DBG & 1) return;
       const unsigned ch = (unsigned)(4 * ks + chl);
       const int so = __builtin_amdgcn_readfirstlane((int)(ch * in_plane * 4u));
@@ -297,39 +306,27 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
       }
     }
   };
-  // ADAIN: register loads of K step g's patch half, and their store with the affine
-  // ((v - mean_c) / std_c) * std_s + mean_s inside the image (0 at padding positions)
-  auto load = [&](int g) {
-    if constexpr (!kDMA) {
-      const int ks = g - (g / K4) * K4;
-      const unsigned ch = (unsigned)(4 * ks + chl);
-      const unsigned pb = ch * in_plane * 4u;  // >= the range for a padding channel
-      ap = adain_params(a.aux, n, (int)ch, a);
-      if (DBG & 1) return;
-#pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        int y = y0 - 1 + 9 * hf + r;
-        const bool yok = resolve_bf(y, a.H, zp);
-        const int ro = __builtin_amdgcn_readfirstlane(yok ? (int)(y * rs * 4) : (int)oob);
-        X[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (int)(pb + cx), ro, 0));
-      }
-      X[9] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rin, (int)(pb + hoff), 0, 0));
-    }
-  };
-  auto store = [&](int g, float* st) {
-    if constexpr (!kDMA) {
+  // ADAIN, in place on step g's landed raw patch: ((v - mean_c) / std_c) * std_s + mean_s
+  // inside the image, 0 at padding positions (the raw padding reads are 0)
+  auto fix = [&](int g, float* st) {
+    if constexpr (kAff) {
       if (DBG & 4) return;
-      const int ks = g - (g / K4) * K4;
+      const int ks = g - (g / K4) * K4, ch = 4 * ks + chl;
+      const bool chok = ch < a.Cin;
+      const int cc = chok ? ch : 0;
+      const float mc = aparm[cc], sc = aparm[kW4AffC + cc], ms = aparm[2 * kW4AffC + cc];
       float* xs = st + chl * kW4CS;
-      const bool chok = 4 * ks + chl < a.Cin;
 #pragma unroll
       for (int r = 0; r < 9; ++r) {
         int y = y0 - 1 + 9 * hf + r;
         const bool rok = chok && resolve_bf(y, a.H, zp) && okx;
-        xs[(9 * hf + r) * kW4PS + 1 + lane] = rok ? fmaf(X[r] - ap.mc, ap.scale, ap.ms) : 0.f;
+        float* e = xs + (9 * hf + r) * kW4PS + 1 + lane;
+        *e = rok ? fmaf(*e - mc, sc, ms) : 0.f;
       }
-      const float hv = (chok && h_ok) ? fmaf(X[9] - ap.mc, ap.scale, ap.ms) : 0.f;
-      if (has_halo) xs[hrw * kW4PS + hcol] = hv;
+      if (has_halo) {
+        float* e = xs + hrw * kW4PS + hcol;
+        *e = (chok && h_ok) ? fmaf(*e - mc, sc, ms) : 0.f;
+      }
     }
   };
 
@@ -534,39 +531,41 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // Before the barrier that opens step g each wave retires its own DMA pieces of step g
   // with a counted vmcnt (the pieces of steps g + 1, g + 2 stay in flight; ADAIN's register
   // loads drain everything at their use, so its count is only ever conservative).
-  constexpr int kPerW = 3;                                 // weight pieces per step and wave
-  const int per = kPerW + (kDMA ? (wide ? 3 : kSlow) : 0);  // all pieces per step and wave
-  auto wait_step = [&](int g) {
-    const int ahead = min(2, G - 1 - g);  // steps issued after g
+  constexpr int kPerW = 3;                          // weight pieces per step and wave
+  const int per = kPerW + (wide ? 3 : kSlow);       // all pieces per step and wave
+  // wait until at most `ahead` steps' pieces issued after the awaited one are in flight
+  auto wait_ahead = [&](int ahead) {
     const int allowed = ahead * per;
     if (allowed >= 26) asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
     else if (allowed >= 13) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
     else if (allowed >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     else if (allowed >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (allowed >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
   issue(0, smem0);
   if (G > 1) issue(1, smem1);
   if (G > 2) issue(2, smem2);
-  load(0);
-  store(0, smem0);
-  // K step g from stage `cur`; step g + 3's DMA into `nx3` (the stage step g - 1 used),
-  // step g + 1's ADAIN registers into `nx1`
+  if constexpr (kAff) {  // step 0's affine before its compute
+    wait_ahead(min(2, G - 1));
+    lds_barrier();
+    fix(0, smem0);
+  }
+  // K step g from stage `cur`; step g + 3's DMA into `nx3` (the stage step g - 1 used);
+  // ADAIN: step g + 1's affine in `nx1` (its DMA is awaited one step earlier)
   auto step = [&](int g, float* cur, float* nx1, float* nx3) {
     if (!(DBG & 16)) {
-      wait_step(g);
+      if constexpr (kAff) wait_ahead(g + 2 < G ? 1 : 0);
+      else wait_ahead(min(2, G - 1 - g));
       lds_barrier();  // step g's stage is complete; nx3 is free
     }
     if (g + 3 < G) issue(g + 3, nx3);
-    if (g + 1 < G) load(g + 1);
     compute(cur);
     if ((g + 1) % K4 == 0) {
       if (!(DBG & 32) || a.N < 0) epilogue(ct0 + g / K4, cur);
 #pragma unroll
       for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
-    if (g + 1 < G) store(g + 1, nx1);
+    if (g + 1 < G) fix(g + 1, nx1);
   };
   for (int g = 0; g < G; g += kW4STG) {
     step(g, smem0, smem1, smem3);
