@@ -218,14 +218,14 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // aligned), half 0 taking pieces 0-2, half 1 pieces 3-4 (+ one padding piece); elsewhere
   // 20 pieces of 4 B per lane (element 64 p + l resolved against the padding), 10 per half.
   // Offsets are computed once per block. ADAIN streams the raw feature the same way and
-  // applies its affine in place (fix()) one step ahead: half h of a channel = rows
-  // 9h..9h+8 (lane -> column x0 + lane) and lanes < 18 one halo element of those rows.
+  // each lane applies the affine in place to the elements its own pieces wrote (fix_own).
   const int chl = wave >> 1, hf = wave & 1;
   const bool zp = a.pad == RPST_PAD_ZERO;
   const int rs = pooled ? a.Ws : a.W;  // source row stride
   constexpr bool kAff = INOP == RPST_IN_ADAIN;
   constexpr int kSlow = 10;
   unsigned poff[kSlow];
+  unsigned pvalid = 0;  // bit i: slot i of this lane holds image data (ADAIN's affine applies)
   const bool wide = !pooled && x0 >= 1 && x0 + kW4TW < a.W;
   {
     if (wide) {
@@ -236,6 +236,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         int y = y0 - 1 + row;
         const bool ok = p < kW4DMA4 && f < kW4PH * 17 && resolve_bf(y, a.H, zp);
         poff[i] = ok ? ((unsigned)(y * rs) + (unsigned)(x0 - 1 + 4 * j)) * 4u : oob;
+        pvalid |= ok ? (1u << i) : 0u;
       }
     } else {
 #pragma unroll
@@ -246,16 +247,10 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         const bool ok = col < kW4TW + 2 && resolve_bf(y, a.H, zp) & resolve_bf(x, a.W, zp);
         poff[i] = ok ? ((unsigned)((pooled ? y >> 1 : y) * rs) + (unsigned)(pooled ? x >> 1 : x)) * 4u
                      : oob;
+        pvalid |= ok ? (1u << i) : 0u;
       }
     }
   }
-  int bx = x0 + lane;
-  const bool okx = resolve_bf(bx, a.W, zp);
-  const bool has_halo = lane < kW4PH;
-  const int hrw = 9 * hf + (lane >> 1);  // halo patch row (lanes < 18)
-  int hy = y0 - 1 + (has_halo ? hrw : 0), hx = (lane & 1) ? x0 + kW4TW : x0 - 1;
-  const bool h_ok = has_halo && resolve_bf(hy, a.H, zp) && resolve_bf(hx, a.W, zp);
-  const int hcol = (lane & 1) ? kW4TW + 1 : 0;
   // ADAIN: (mean_c, std_s / std_c, mean_s) of every input channel of image n, in LDS (its
   // global loads happen before any DMA is in flight)
   __shared__ float aparm[kAff ? 3 * kW4AffC : 1];
@@ -306,9 +301,10 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
       }
     }
   };
-  // ADAIN, in place on step g's landed raw patch: ((v - mean_c) / std_c) * std_s + mean_s
-  // inside the image, 0 at padding positions (the raw padding reads are 0)
-  auto fix = [&](int g, float* st) {
+  // ADAIN, in place on the elements this lane's own DMA pieces of step g wrote (so a wave
+  // needs only its own counted wait, no barrier): ((v - mean_c) / std_c) * std_s + mean_s
+  // inside the image, 0 at padding positions (a padding piece lane read 0)
+  auto fix_own = [&](int g, float* st) {
     if constexpr (kAff) {
       if (DBG & 4) return;
       const int ks = g - (g / K4) * K4, ch = 4 * ks + chl;
@@ -316,16 +312,25 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
       const int cc = chok ? ch : 0;
       const float mc = aparm[cc], sc = aparm[kW4AffC + cc], ms = aparm[2 * kW4AffC + cc];
       float* xs = st + chl * kW4CS;
+      if (wide) {
 #pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        int y = y0 - 1 + 9 * hf + r;
-        const bool rok = chok && resolve_bf(y, a.H, zp) && okx;
-        float* e = xs + (9 * hf + r) * kW4PS + 1 + lane;
-        *e = rok ? fmaf(*e - mc, sc, ms) : 0.f;
-      }
-      if (has_halo) {
-        float* e = xs + hrw * kW4PS + hcol;
-        *e = (chok && h_ok) ? fmaf(*e - mc, sc, ms) : 0.f;
+        for (int i = 0; i < 3; ++i) {
+          const int p = 3 * hf + i;
+          if (p < kW4DMA4) {
+            float4* e = reinterpret_cast<float4*>(xs + 4 * (64 * p + lane));
+            const bool ok = chok && ((pvalid >> i) & 1u);
+            const float4 v = *e;
+            *e = make_float4(ok ? fmaf(v.x - mc, sc, ms) : 0.f, ok ? fmaf(v.y - mc, sc, ms) : 0.f,
+                             ok ? fmaf(v.z - mc, sc, ms) : 0.f, ok ? fmaf(v.w - mc, sc, ms) : 0.f);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kSlow; ++i) {
+          float* e = xs + 64 * (kSlow * hf + i) + lane;
+          const bool ok = chok && ((pvalid >> i) & 1u);
+          *e = ok ? fmaf(*e - mc, sc, ms) : 0.f;
+        }
       }
     }
   };
@@ -545,17 +550,15 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   issue(0, smem0);
   if (G > 1) issue(1, smem1);
   if (G > 2) issue(2, smem2);
-  if constexpr (kAff) {  // step 0's affine before its compute
+  if constexpr (kAff) {  // step 0's affine (published by the first step's barrier)
     wait_ahead(min(2, G - 1));
-    lds_barrier();
-    fix(0, smem0);
+    fix_own(0, smem0);
   }
   // K step g from stage `cur`; step g + 3's DMA into `nx3` (the stage step g - 1 used);
-  // ADAIN: step g + 1's affine in `nx1` (its DMA is awaited one step earlier)
+  // ADAIN: step g + 1's affine on this wave's own pieces in `nx1`, after the MFMAs
   auto step = [&](int g, float* cur, float* nx1, float* nx3) {
     if (!(DBG & 16)) {
-      if constexpr (kAff) wait_ahead(g + 2 < G ? 1 : 0);
-      else wait_ahead(min(2, G - 1 - g));
+      wait_ahead(min(2, G - 1 - g));
       lds_barrier();  // step g's stage is complete; nx3 is free
     }
     if (g + 3 < G) issue(g + 3, nx3);
@@ -565,7 +568,12 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
-    if (g + 1 < G) fix(g + 1, nx1);
+    if constexpr (kAff) {
+      if (g + 1 < G) {
+        wait_ahead(min(2, G - 2 - g));  // this wave's pieces of step g + 1 have landed
+        fix_own(g + 1, nx1);
+      }
+    }
   };
   for (int g = 0; g < G; g += kW4STG) {
     step(g, smem0, smem1, smem3);
