@@ -197,6 +197,15 @@ class precise_convs:
         return False
 
 
+def pool_pass_pays(x: torch.Tensor, cout: int, ksize: int) -> bool:
+    """For a conv whose input is max_pool2d(x, 2, 2, ceil_mode=True): True when the library
+    would run the pooled map's conv as F(4x4,3x3) (measured: pool pass + F(4x4) is faster
+    than the F(2x2) conv with the pool fused into its loader, profiles/r01_bench_sanet_w4*)."""
+    n, cin, h, w = x.shape
+    return ksize == 3 and _lib.load().rpst_conv2d_algorithm(
+        cout, cin, (h + 1) // 2, (w + 1) // 2, ksize, IN_NONE) == 2
+
+
 def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], cout: int,
            ksize: int, pad: int = PAD_ZERO, in_op: int = IN_NONE, relu: bool = False,
            aux: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,

@@ -152,6 +152,11 @@ def run(steps: List[object], x: torch.Tensor, first_aux=None, first_in_op=None,
                     raise NotImplementedError("rpst plan: first conv already has an input op")
                 in_op, aux = first_in_op, first_aux
             c = s.conv
+            if in_op == ops.IN_MAXPOOL2 and ops.pool_pass_pays(x, c.out_channels,
+                                                               c.kernel_size[0]):
+                # F(4x4,3x3) has no max-pool loader: a separate pool pass (one read of the
+                # source, one write of the pooled map) + F(4x4) beats the fused F(2x2)
+                x, in_op = ops.maxpool2x2_ceil(x), ops.IN_NONE
             if in_op == ops.IN_ADD_ADAIN:
                 if stats_last and i == len(steps) - 1:
                     raise NotImplementedError("rpst plan: skip-AdaIN conv with statistics")

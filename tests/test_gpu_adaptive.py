@@ -124,8 +124,11 @@ def test_adaptive_transform_golden(cuda, golden, mode):
 
 def _cond_tol(ref32, ref64):
     """Network tolerance against the float64 oracle: the fp32 reference's own error there
-    (the problem's conditioning) x 3, at least TOL_NET."""
-    return max(TOL_NET, 3.0 * rel_l2(ref32, ref64))
+    (the problem's conditioning) x 5, at least TOL_NET. The factor: the VGG convs run as
+    Winograd F(4x4,3x3), whose fp32 rounding is ~2.8x the direct convolution's per layer
+    (1.1e-6 vs 4e-7 rel-L2, tests/test_gpu_fullsize.py); measured 3.5x on the 'aea' model
+    (sigmoid slope 50 on a peaked softmax), 2.4x with F(2x2)."""
+    return max(TOL_NET, 5.0 * rel_l2(ref32, ref64))
 
 
 @pytest.mark.parametrize("mode", MODES)
