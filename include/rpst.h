@@ -130,10 +130,11 @@ int rpst_conv2d_skip_adain(const float* stylized, const float* content, const fl
 int64_t rpst_conv2d_grid_threads(int N, int Cin, int Hs, int Ws, int Cout, int ksize,
                                  int in_op);
 
-/* Algorithm rpst_conv2d uses for this layer — host-only: RPST_CONV_DIRECT (implicit GEMM,
- * all 1x1 and 16-wide 3x3 layers), RPST_CONV_WINOGRAD4 (F(4x4,3x3) in fp32, 3x3 layers with
- * Cout >= 32 whose loader operator is NONE / ADAIN / UPSAMPLE2) or RPST_CONV_WINOGRAD
- * (F(2x2,3x3) in fp32, the other 3x3 layers with Cout >= 32). The environment variable
+/* Algorithm rpst_conv2d uses for this layer — host-only: RPST_CONV_DIRECT (implicit GEMM:
+ * every 1x1 layer and 3x3 layers with < 16 input channels), RPST_CONV_WINOGRAD4 (F(4x4,3x3)
+ * in fp32: 3x3 layers with >= 16 input channels whose loader operator is NONE / ADAIN /
+ * UPSAMPLE2) or RPST_CONV_WINOGRAD (F(2x2,3x3) in fp32: the other 3x3 layers with >= 16
+ * input and >= 32 output channels). The environment variable
  * RPST_CONV_ALGO=direct|winograd|winograd4 overrides. */
 #define RPST_CONV_DIRECT 0
 #define RPST_CONV_WINOGRAD 1

@@ -485,10 +485,12 @@ static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
     if (!strcmp(e, "winograd4")) return w4 ? RPST_CONV_WINOGRAD4 : RPST_CONV_WINOGRAD;
   }
   // measured (profiles/r01_bench_conv_wino4.log): F(4x4) wins every layer with >= 16 input
-  // channels it supports, the 16-wide 32->16 / 16->3 decoder layers included; the 3-channel
-  // input layer and the remaining 16-wide outputs run faster direct
-  if (w4 && Cin >= 16 && !t_conv_precise) return RPST_CONV_WINOGRAD4;
-  if (w4 && Cin >= 16) return RPST_CONV_WINOGRAD;  // precise mode, same shapes as F(4x4)
+  // channels it supports, the 16-wide 32->16 / 16->3 decoder layers included; the
+  // 3-channel input layers (3->16, VGG 3->64) and the remaining 16-wide outputs run
+  // faster direct
+  if (Cin < 16) return RPST_CONV_DIRECT;
+  if (w4 && !t_conv_precise) return RPST_CONV_WINOGRAD4;
+  if (w4) return RPST_CONV_WINOGRAD;  // precise mode, same shapes as F(4x4)
   return Cout >= 32 ? RPST_CONV_WINOGRAD : RPST_CONV_DIRECT;
 }
 

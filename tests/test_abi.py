@@ -86,8 +86,9 @@ def test_cpu_tensors_raise_no_fallback():
 
 
 def test_conv_algorithm_choice_is_host_only(monkeypatch):
-    """rpst_conv2d_algorithm: F(4x4) for the NONE / ADAIN / UPSAMPLE2 loaders with >= 16
-    input channels, F(2x2) for the other 3x3 layers with Cout >= 32, direct otherwise;
+    """rpst_conv2d_algorithm: direct below 16 input channels, else F(4x4) for the NONE /
+    ADAIN / UPSAMPLE2 loaders, F(2x2) for the other 3x3 layers with Cout >= 32, direct
+    otherwise;
     precise mode (training) and RPST_CONV_ALGO override."""
     monkeypatch.delenv("RPST_CONV_ALGO", raising=False)
     lib = _lib.load()
@@ -96,7 +97,7 @@ def test_conv_algorithm_choice_is_host_only(monkeypatch):
     assert lib.rpst_conv2d_algorithm(128, 256, 512, 512, 3, 4) == W4   # AdaIN-in-loader
     assert lib.rpst_conv2d_algorithm(256, 256, 32, 32, 3, 2) == W4     # upsample
     assert lib.rpst_conv2d_algorithm(128, 64, 64, 64, 3, 1) == W2      # max-pool loader
-    assert lib.rpst_conv2d_algorithm(64, 3, 512, 512, 3, 0) == W2
+    assert lib.rpst_conv2d_algorithm(64, 3, 512, 512, 3, 0) == D        # 3-channel input
     assert lib.rpst_conv2d_algorithm(16, 3, 512, 512, 3, 0) == D
     assert lib.rpst_conv2d_algorithm(16, 32, 512, 512, 3, 0) == W4
     assert lib.rpst_conv2d_algorithm(512, 512, 64, 64, 1, 0) == D

@@ -29,6 +29,7 @@ FUSED = [  # AdaIN-in-loader decoder conv (in_op 4) of the fused AdaIN-RP path
     (32, 256, 512, 512, 128, 3, 0, 4),
 ]
 VGG = [
+    (64, 3, 512, 512, 64, 3, 1, 0),
     (64, 64, 512, 512, 64, 3, 1, 0), (64, 64, 512, 512, 128, 3, 1, 1),
     (64, 128, 256, 256, 128, 3, 1, 0), (64, 128, 256, 256, 256, 3, 1, 1),
     (64, 256, 128, 128, 256, 3, 1, 0), (64, 256, 128, 128, 512, 3, 1, 1),
