@@ -139,7 +139,7 @@ def cpu_baseline(kind, size, budget_s=12.0):
                       f"{threads} threads, {dt:.1f}s"}
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic_w4.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic_final.json")
 
 
 def pmc_lookup(kernel_substr, grid=None):
