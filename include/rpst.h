@@ -104,6 +104,19 @@ int rpst_conv2d(const float* input, const float* aux, const float* packed_weight
                 int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
                 rpst_stream_t stream);
 
+/* Same conv with a caller-provided workspace (rpst_conv2d_workspace_size bytes, 0 when the
+ * layer needs none). With RPST_IN_ADAIN on the F(4x4) path the workspace holds per-image
+ * weights with the AdaIN scale std_s/std_c folded in along Cin and a per-(n, co) bias by
+ * border class carrying mean_s - mean_c*std_s/std_c, so the conv streams the raw feature
+ * (conv(pad0(s*x + b)) = conv_{W*s}(pad0(x)) + sum over in-image taps of W*b). Same result
+ * as rpst_conv2d within fp32 rounding; rpst_conv2d applies the affine in its tile loader. */
+size_t rpst_conv2d_workspace_size(int N, int Cin, int Hs, int Ws, int Cout, int ksize,
+                                  int in_op);
+int rpst_conv2d_ws(const float* input, const float* aux, const float* packed_weight,
+                   const float* bias, const float* residual, float* out, int N, int Cin,
+                   int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
+                   void* workspace, size_t workspace_bytes, rpst_stream_t stream);
+
 /* Same conv, additionally returning calc_mean_std (base.py:399-407) of its OUTPUT per
  * (n, co): the statistics are reduced in the conv epilogue from registers and merged in
  * fp64, so an AdaIN consumer never re-reads the feature. mean/std_out: N*Cout floats.

@@ -23,6 +23,11 @@ struct ConvArgs {
   int persist;        // Winograd: one block loops over all co tiles of its spatial tile
   float2* stat_part;  // optional: per-(n, co, wave tile) (mean, M2) of the output
   int stat_P;         // partials per (n, co) = tiles_x * tiles_y * WN
+  // F(4x4) with AdaIN folded into per-image weights (wino4_fold): image n's packed weights
+  // start at wpk + n * wstride (0: shared); btab = per-(n, co) bias by border class
+  // [n][co][3 row classes][3 column classes] replacing `bias` (nullptr: use `bias`)
+  int64_t wstride;
+  const float* btab;
 };
 
 template <int KS>
@@ -236,5 +241,8 @@ int wino4_persist();
 size_t wino4_packed_floats(int Cout, int Cin);
 int wino4_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);
 int wino4_launch(ConvArgs& a, int in_op, hipStream_t st);
+size_t wino4_fold_floats(int N, int Cin, int Cout);
+int wino4_fold(ConvArgs& a, const float* direct_packed, int direct_cout_pad, float* ws,
+               hipStream_t st);
 
 }  // namespace rpst

@@ -614,7 +614,8 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
                        const float* packed_weight,
                        const float* bias, const float* residual, float* out, int N, int Cin,
                        int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
-                       float2* stat_part, int* stat_P, ConvArgs* args_out, hipStream_t st) {
+                       float2* stat_part, int* stat_P, ConvArgs* args_out, hipStream_t st,
+                       float* fold_ws = nullptr) {
   RPST_REQUIRE(input && packed_weight && out, "conv2d: null pointer");
   RPST_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && Hs > 0 && Ws > 0, "conv2d: bad shape");
   RPST_REQUIRE(ksize == 1 || ksize == 3, "conv2d: ksize must be 1 or 3, got %d", ksize);
@@ -678,7 +679,12 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   if (algo == RPST_CONV_WINOGRAD4) {
     a.wpk = packed_weight + direct_packed_floats(Cout, Cin, ksize) + wino_packed_floats(Cout, Cin);
     a.stat_part = stat_part;
-    if (int e = wino4_launch(a, in_op, st)) return e;
+    int op = in_op;
+    if (in_op == RPST_IN_ADAIN && fold_ws && a.H >= 2 && a.W >= 2) {  // AdaIN in the weights
+      if (int e = wino4_fold(a, packed_weight, pad_cout(Cout), fold_ws, st)) return e;
+      op = RPST_IN_NONE;
+    }
+    if (int e = wino4_launch(a, op, st)) return e;
     if (stat_P) *stat_P = a.stat_P;
     if (args_out) *args_out = a;
     return RPST_OK;
@@ -736,6 +742,36 @@ extern "C" int rpst_conv2d(const float* input, const float* aux, const float* pa
                      as_stream(stream));
 }
 
+// workspace of the F(4x4) conv with RPST_IN_ADAIN folded into per-image weights (0 for
+// every other layer)
+static size_t fold_bytes(int N, int Cin, int Hs, int Ws, int Cout, int ksize, int in_op) {
+  if (N <= 0 || Cin <= 0 || Hs < 2 || Ws < 2 || Cout <= 0 || ksize != 3 || in_op != RPST_IN_ADAIN)
+    return 0;
+  if (conv_algo(Cout, Cin, Hs, Ws, ksize, in_op) != RPST_CONV_WINOGRAD4) return 0;
+  return wino4_fold_floats(N, Cin, Cout) * sizeof(float);
+}
+
+extern "C" size_t rpst_conv2d_workspace_size(int N, int Cin, int Hs, int Ws, int Cout, int ksize,
+                                             int in_op) {
+  return fold_bytes(N, Cin, Hs, Ws, Cout, ksize, in_op);
+}
+
+extern "C" int rpst_conv2d_ws(const float* input, const float* aux, const float* packed_weight,
+                              const float* bias, const float* residual, float* out, int N,
+                              int Cin, int Hs, int Ws, int Cout, int ksize, int pad_mode,
+                              int in_op, int relu, void* workspace, size_t workspace_bytes,
+                              rpst_stream_t stream) {
+  RPST_REQUIRE(in_op != RPST_IN_ADD_ADAIN, "conv2d: ADD_ADAIN goes through rpst_conv2d_skip_adain");
+  const size_t need = fold_bytes(N, Cin, Hs, Ws, Cout, ksize, in_op);
+  if (need && (!workspace || workspace_bytes < need)) {
+    set_error("conv2d: workspace %zu < %zu bytes", workspace_bytes, need);
+    return RPST_EWORKSPACE;
+  }
+  return conv_common(input, aux, nullptr, packed_weight, bias, residual, out, N, Cin, Hs, Ws,
+                     Cout, ksize, pad_mode, in_op, relu, nullptr, nullptr, nullptr,
+                     as_stream(stream), need ? static_cast<float*>(workspace) : nullptr);
+}
+
 extern "C" int rpst_conv2d_skip_adain(const float* stylized, const float* content,
                                       const float* params, const float* packed_weight,
                                       const float* bias, float* out, int N, int Cin, int H, int W,
@@ -751,7 +787,8 @@ extern "C" size_t rpst_conv2d_stats_workspace_size(int N, int Cin, int Hs, int W
                                                    int ksize, int in_op) {
   if (N <= 0 || Cin <= 0 || Hs <= 0 || Ws <= 0 || Cout <= 0 || (ksize != 1 && ksize != 3)) return 0;
   const ConvGeom g = conv_geom(N, Cin, Hs, Ws, Cout, ksize, in_op);
-  return (size_t)N * Cout * g.stat_P * sizeof(float2);
+  const size_t stats = ((size_t)N * Cout * g.stat_P * sizeof(float2) + 255) / 256 * 256;
+  return stats + fold_bytes(N, Cin, Hs, Ws, Cout, ksize, in_op);
 }
 
 extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
@@ -777,9 +814,12 @@ extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
       return e;
     return rpst_calc_mean_std(out, mean, std_out, N, Cout, (int64_t)a.H * a.W, eps, stream);
   }
+  const size_t fb = fold_bytes(N, Cin, Hs, Ws, Cout, ksize, in_op);
+  float* fold_ws = fb ? reinterpret_cast<float*>(static_cast<char*>(workspace) + (need - fb))
+                      : nullptr;
   if (int e = conv_common(input, aux, nullptr, packed_weight, bias, residual, out, N, Cin, Hs, Ws,
                           Cout, ksize, pad_mode, in_op, relu, static_cast<float2*>(workspace), &P,
-                          &a, st))
+                          &a, st, fold_ws))
     return e;
   stat_merge_kernel<<<(planes + 3) / 4, 256, 0, st>>>(static_cast<const float2*>(workspace), mean,
                                                       std_out, planes, P, a.tiles_x, g.stat_wn,

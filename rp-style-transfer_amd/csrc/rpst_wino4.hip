@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
       (void*)(a.in + (int64_t)n * a.Cin * in_plane), (short)0, (int)oob, 0x00020000);
   const unsigned wbytes = (unsigned)(a.co_tiles * nch * kW4WCH) * 4u;
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.wpk, (short)0, (int)wbytes, 0x00020000);
+      (void*)(a.wpk + (int64_t)n * a.wstride), (short)0, (int)wbytes, 0x00020000);
 
   // ---- patch of one K step: 4 channels, [18 rows][68] (66 columns + 2 spare) at channel
   // stride 1280; wave w fills half w & 1 of channel w >> 1. One-load operators (NONE,
@@ -441,13 +441,25 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   const float inv = rows * cols > 0 ? 1.f / (float)(rows * cols) : 0.f;
   auto finish = [&](int co, float (&Y)[16]) {
     const bool cok = co < a.Cout;
-    const float bv = (a.bias && cok) ? a.bias[co] : 0.f;
+    float bv = (a.bias && cok) ? a.bias[co] : 0.f;
+    // folded AdaIN: the bias depends on which taps of the zero-padded input were inside
+    // the image (border class); interior tiles take the interior entry
+    const float* bt = a.btab ? a.btab + ((int64_t)n * a.Cout + (cok ? co : 0)) * 9 : nullptr;
+    if (bt) bv = cok ? bt[4] : 0.f;
+    const bool edge = bt && (gy0 == 0 || gy0 + 4 >= a.H || gx0 == 0 || gx0 + 4 >= a.W);
     float sum = 0.f;
 #pragma unroll
     for (int yy = 0; yy < 4; ++yy)
 #pragma unroll
       for (int xx = 0; xx < 4; ++xx) {
-        const float v = activate(Y[yy * 4 + xx] + bv, a.relu);
+        float b = bv;
+        if (edge) {
+          const int gy = gy0 + yy, gx = gx0 + xx;
+          const int rc = gy == 0 ? 0 : (gy >= a.H - 1 ? 2 : 1);
+          const int cc = gx == 0 ? 0 : (gx >= a.W - 1 ? 2 : 1);
+          b = cok ? bt[rc * 3 + cc] : 0.f;
+        }
+        const float v = activate(Y[yy * 4 + xx] + b, a.relu);
         Y[yy * 4 + xx] = v;
         sum += (yy < rows && gx0 + xx < a.W) ? v : 0.f;
       }
@@ -581,6 +593,90 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     if (g + 2 < G) step(g + 2, smem2, smem3, smem1);
     if (g + 3 < G) step(g + 3, smem3, smem0, smem2);
   }
+}
+
+// ---- AdaIN folded into the weights (RPST_IN_ADAIN through the plain NONE loader) -------
+// conv(pad0(s * x + b)) = conv_{W s}(pad0(x)) + sum_ci b_ci sum_{taps inside} W[co][ci][tap]
+// with s = std_s / std_c and b = mean_s - mean_c * s per (n, ci): image n gets its own
+// copy of the packed U scaled by s along ci (U is linear in g), and a bias per (n, co) and
+// border class (which rows / columns of the 3x3 window fall on zero padding; with reflect
+// padding every tap sees s * x + b, so all nine classes are equal). The conv itself then
+// streams the raw feature by plain LDS-DMA: no per-element affine, no extra LDS traffic.
+size_t wino4_fold_floats(int N, int Cin, int Cout) {
+  return (size_t)N * (wino4_packed_floats(Cout, Cin) + (size_t)Cout * 9);
+}
+
+__global__ void wino4_fold_w_kernel(const float4* __restrict__ pk, float4* __restrict__ out,
+                                    const float* __restrict__ aux, int N, int Cin, int nch,
+                                    int64_t per4) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * per4) return;
+  const int n = (int)(t / per4);
+  const int64_t u = t - (int64_t)n * per4;  // float4 index = element index >> 2
+  const int l = (int)(u & 63);
+  int64_t r = (u >> 6) / 9;  // ((ct * nch + c) * 2 + s) * 2 + h
+  const int s = (int)((r >> 1) & 1);
+  const int c = (int)((r >> 2) % nch);
+  const int ci = c * kW4CK + 4 * s + (l >> 4);
+  const int64_t nc = (int64_t)N * Cin, i = (int64_t)n * Cin + (ci < Cin ? ci : 0);
+  const float sc = ci < Cin ? aux[3 * nc + i] / aux[2 * nc + i] : 0.f;
+  const float4 v = pk[u];
+  out[t] = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
+}
+
+// btab[(n * Cout + co) * 9 + 3 rc + cc]: rc / cc = 0 first row / column (tap 0 on padding),
+// 1 interior, 2 last; direct-packed weights [chunk][tap][ci % 8][cout_pad]
+__global__ void wino4_fold_b_kernel(const float* __restrict__ dpk, const float* __restrict__ bias,
+                                    const float* __restrict__ aux, float* __restrict__ btab,
+                                    int N, int Cin, int Cout, int cout_pad, int reflect) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * Cout * 9) return;
+  const int co = (int)(t % Cout);
+  const int64_t r = t / Cout;
+  const int cls = (int)(r % 9), n = (int)(r / 9);
+  const int rc = cls / 3, cc = cls % 3;
+  const int64_t nc = (int64_t)N * Cin;
+  double acc = 0.0;
+  for (int ci = 0; ci < Cin; ++ci) {
+    const int64_t i = (int64_t)n * Cin + ci;
+    const float sc = aux[3 * nc + i] / aux[2 * nc + i];
+    const double b = (double)aux[nc + i] - (double)aux[i] * (double)sc;
+    const float* w = dpk + ((int64_t)(ci >> 3) * 9 * 8 + (ci & 7)) * cout_pad + co;
+    double tap = 0.0;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const bool in = reflect || ((rc != 0 || u != 0) && (rc != 2 || u != 2) &&
+                                    (cc != 0 || p != 0) && (cc != 2 || p != 2));
+        if (in) tap += (double)w[(int64_t)(u * 3 + p) * 8 * cout_pad];
+      }
+    acc += b * tap;
+  }
+  btab[((int64_t)n * Cout + co) * 9 + cls] = (float)((bias ? (double)bias[co] : 0.0) + acc);
+}
+
+int wino4_fold(ConvArgs& a, const float* direct_packed, int direct_cout_pad, float* ws,
+               hipStream_t st) {
+  RPST_REQUIRE(a.H >= 2 && a.W >= 2, "conv2d: folded AdaIN needs H, W >= 2");
+  const int nch = (a.Cin + kW4CK - 1) / kW4CK;
+  const int64_t per = (int64_t)wino4_packed_floats(a.Cout, a.Cin);
+  const int64_t n4 = (int64_t)a.N * (per / 4);
+  float* wf = ws;
+  float* bt = ws + (int64_t)a.N * per;
+  wino4_fold_w_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(
+      reinterpret_cast<const float4*>(a.wpk), reinterpret_cast<float4*>(wf), a.aux, a.N, a.Cin,
+      nch, per / 4);
+  if (int e = launch_status("wino4_fold_w_kernel")) return e;
+  const int64_t nb = (int64_t)a.N * a.Cout * 9;
+  wino4_fold_b_kernel<<<(unsigned)((nb + 127) / 128), 128, 0, st>>>(
+      direct_packed, a.bias, a.aux, bt, a.N, a.Cin, a.Cout, direct_cout_pad,
+      a.pad == RPST_PAD_REFLECT);
+  if (int e = launch_status("wino4_fold_b_kernel")) return e;
+  a.wpk = wf;
+  a.wstride = per;
+  a.btab = bt;
+  return RPST_OK;
 }
 
 int wino4_launch(ConvArgs& a, int in_op, hipStream_t st) {

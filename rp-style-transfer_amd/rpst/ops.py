@@ -209,8 +209,10 @@ def pool_pass_pays(x: torch.Tensor, cout: int, ksize: int) -> bool:
 def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], cout: int,
            ksize: int, pad: int = PAD_ZERO, in_op: int = IN_NONE, relu: bool = False,
            aux: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
-           out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out = act(conv_k(in_op(x)) + bias) [+ residual]; see include/rpst.h."""
+           out: Optional[torch.Tensor] = None, fold: bool = True) -> torch.Tensor:
+    """out = act(conv_k(in_op(x)) + bias) [+ residual]; see include/rpst.h. fold: let the
+    library fold an ADAIN loader into per-image weights when it has a workspace for it
+    (rpst_conv2d_ws); False keeps the affine in the tile loader (rpst_conv2d)."""
     assert x.dim() == 4
     if in_op == IN_ADD_ADAIN:
         raise ValueError("rpst: the skip-AdaIN operator takes two inputs: use conv2d_skip_adain")
@@ -232,10 +234,19 @@ def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], 
     with _traced(_conv_name(ksize, cin, cout, hs, ws, n, in_op),
                  2.0 * n * cout * h * w * cin * ksize * ksize,
                  4.0 * (x.numel() + n * cout * h * w)):
-        _lib.call("rpst_conv2d", x.data_ptr(), _ptr(aux), packed.data_ptr(),
-                  _ptr(None if bias is None else _c(bias.detach())), _ptr(residual),
-                  out.data_ptr(), n, cin, hs, ws, cout, ksize, pad, in_op, _act(relu),
-                  _stream(x))
+        nbytes = _lib.load().rpst_conv2d_workspace_size(n, cin, hs, ws, cout, ksize,
+                                                        in_op) if fold else 0
+        if nbytes:
+            ws_t = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
+            _lib.call("rpst_conv2d_ws", x.data_ptr(), _ptr(aux), packed.data_ptr(),
+                      _ptr(None if bias is None else _c(bias.detach())), _ptr(residual),
+                      out.data_ptr(), n, cin, hs, ws, cout, ksize, pad, in_op, _act(relu),
+                      ws_t.data_ptr(), nbytes, _stream(x))
+        else:
+            _lib.call("rpst_conv2d", x.data_ptr(), _ptr(aux), packed.data_ptr(),
+                      _ptr(None if bias is None else _c(bias.detach())), _ptr(residual),
+                      out.data_ptr(), n, cin, hs, ws, cout, ksize, pad, in_op, _act(relu),
+                      _stream(x))
     return out
 
 

@@ -302,18 +302,26 @@ def test_conv2d_stats_equal_calc_mean_std(cuda, shape, conv_algo):
     assert rel_l2(std, s2) < 1e-6
 
 
-def test_conv2d_adain_input_op(cuda, conv_algo):
+@pytest.mark.parametrize("fold", [True, False])
+@pytest.mark.parametrize("pad,shape,cin,cout", [(0, (2, 24, 40), 32, 16),
+                                                (0, (3, 37, 70), 64, 48),
+                                                (1, (2, 37, 70), 40, 32)])
+def test_conv2d_adain_input_op(cuda, conv_algo, fold, pad, shape, cin, cout):
+    """AdaIN -> conv: fold=True runs the F(4x4) conv with the affine folded into per-image
+    weights and a border-class bias (rpst_conv2d_ws), fold=False the in-loader affine."""
     from rpst import ops
-    c = gen(60, (2, 32, 24, 40), 2.0, 0.5).clamp_min(0)
-    s = gen(61, (2, 32, 24, 40), 1.0, 1.0).clamp_min(0)
-    wt = gen(62, (16, 32, 3, 3), 0.08)
-    b = gen(63, (16,), 0.05)
+    n, h, w = shape
+    c = gen(60, (n, cin, h, w), 2.0, 0.5).clamp_min(0)
+    s = gen(61, (n, cin, h, w), 1.0, 1.0).clamp_min(0)
+    wt = gen(62, (cout, cin, 3, 3), 0.08)
+    b = gen(63, (cout,), 0.05)
     mc, sc = R.calc_mean_std(c)
     ms, ss = R.calc_mean_std(s)
     aux = ops.adain_params(mc, sc, ms, ss).to(cuda)
     p = ops.pack_conv_weight(wt.to(cuda))
-    out = ops.conv2d(c.to(cuda), p, b.to(cuda), 16, 3, in_op=ops.IN_ADAIN, aux=aux, relu=True)
-    ref = _conv_ref(R.adain(c, s).double(), wt.double(), b.double(), 0, 0, True)
+    out = ops.conv2d(c.to(cuda), p, b.to(cuda), cout, 3, pad=pad, in_op=ops.IN_ADAIN, aux=aux,
+                     relu=True, fold=fold)
+    ref = _conv_ref(R.adain(c, s).double(), wt.double(), b.double(), pad, 0, True)
     assert rel_l2(out, ref) < 1e-5
 
 
