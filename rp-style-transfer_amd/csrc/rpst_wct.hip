@@ -8,6 +8,7 @@
 //   Sc = (Cc+1e-4 I)^(1/2), Ic = (Cc+1e-4 I)^(-1/2)                       wct_rp.py:104-105
 //   Mid = (Sc Cs Sc + 1e-4 I)^(1/2)                                         wct_rp.py:107
 //   T = Ic Mid Ic ; out = T (cF - mu_c) + mu_s  -> fp32                     wct_rp.py:109-113
+//   (the last product on the fp32 MFMA for fp32 features, T rounded once; see below)
 // Matrix square roots: coupled Newton-Schulz on A/||A||_F (GEMM-only):
 //   T_k = (3I - Z_k Y_k)/2, Y_{k+1} = Y_k T_k, Z_{k+1} = T_k Z_k  ->  Y = (A/s)^(1/2),
 //   Z = (A/s)^(-1/2). The reference's SVD truncation (singular values < 1e-5) can never
@@ -241,6 +242,133 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
       }
     }
   }
+}
+
+// ---- WCT colour transform in fp32: out = T (cF - mu_c) + mu_s (wct_rp.py:109-113) ----
+// T is computed in fp64 and rounded once; the product is a K = C GEMM over the fp32
+// features, so it runs on the fp32 MFMA (2x the fp64 rate). Centering in fp32 and fp32
+// accumulation over C = 256 terms: ~1.5e-7 rel-L2 vs the fp64 product on encoder features
+// with |T| up to 100 (the fp32 output itself rounds at 6e-8).
+__global__ __launch_bounds__(256) void wct_f32_prep_kernel(const double* __restrict__ T,
+                                                           const double* __restrict__ mu,
+                                                           float* __restrict__ Tf,
+                                                           float* __restrict__ muf, int64_t nT,
+                                                           int64_t nmu) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < nT) Tf[i] = (float)T[i];
+  if (i < nmu) muf[i] = (float)mu[i];
+}
+
+// Block tile 128 (m = output channel) x 128 (n = pixel), K = C in steps of 32, 4 waves of
+// 64 x 64 on v_mfma_f32_32x32x2f32; register-prefetched staging of the next K step.
+// A = T [n][C][C] (k contiguous), B = cF [n][C][HW] (pixels contiguous) centred by mu_c[k]
+// while staged, epilogue adds mu_s[m]. VEC: 16-B loads (HW % 4 == 0, C % 4 == 0).
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void wct_transform_f32_kernel(
+    const float* __restrict__ Tf, const float* __restrict__ X, const float* __restrict__ muc,
+    const float* __restrict__ mus, float* __restrict__ out, int C, int HW) {
+  constexpr int BK = 32, LD = 128 + 4;
+  __shared__ float As[BK * LD];
+  __shared__ float Bs[BK * LD];
+  const int b = blockIdx.z;
+  const int m0 = blockIdx.y * 128, n0 = blockIdx.x * 128;
+  const float* A = Tf + (int64_t)b * C * C;
+  const float* B = X + (int64_t)b * C * HW;
+  const float* mc = muc + (int64_t)b * C;
+  const float* ms = mus + (int64_t)b * C;
+  float* O = out + (int64_t)b * C * HW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, j = lane & 31;
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
+
+  // A staging: thread -> (row ar + 32p, k-run ak..ak+3); B: (k-row bk + 8p, n-run bn..bn+3)
+  const int ar = tid >> 3, ak = (tid & 7) * 4;
+  const int bk = tid >> 5, bn = (tid & 31) * 4;
+  float ra[16], rb[16];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int m = m0 + ar + 32 * p, k = k0 + ak;
+      if (VEC) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < C && k < C) v = *reinterpret_cast<const float4*>(A + (int64_t)m * C + k);
+        ra[4 * p] = v.x; ra[4 * p + 1] = v.y; ra[4 * p + 2] = v.z; ra[4 * p + 3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ra[4 * p + e] = (m < C && k + e < C) ? A[(int64_t)m * C + k + e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int k = k0 + bk + 8 * p, n = n0 + bn;
+      const float mu = k < C ? mc[k] : 0.f;
+      if (VEC) {
+        float4 v = make_float4(mu, mu, mu, mu);
+        if (k < C && n < HW) v = *reinterpret_cast<const float4*>(B + (int64_t)k * HW + n);
+        rb[4 * p] = v.x - mu; rb[4 * p + 1] = v.y - mu; rb[4 * p + 2] = v.z - mu; rb[4 * p + 3] = v.w - mu;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          rb[4 * p + e] = (k < C && n + e < HW) ? B[(int64_t)k * HW + n + e] - mu : 0.f;
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) As[(ak + e) * LD + ar + 32 * p] = ra[4 * p + e];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      *reinterpret_cast<float4*>(Bs + (bk + 8 * p) * LD + bn) =
+          make_float4(rb[4 * p], rb[4 * p + 1], rb[4 * p + 2], rb[4 * p + 3]);
+  };
+
+  const int ktiles = (C + BK - 1) / BK;
+  load(0);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    store();
+    __syncthreads();
+    if (kt + 1 < ktiles) load((kt + 1) * BK);
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      float av[2], bv[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) av[mt] = As[(2 * kk + h) * LD + wm * 64 + mt * 32 + j];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) bv[nt] = Bs[(2 * kk + h) * LD + wn * 64 + nt * 32 + j];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mt], bv[nt], acc[mt][nt], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // D: col n = lane & 31, row m = (r & 3) + 8 (r >> 2) + 4 h
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (m >= C) continue;
+      const float bias = ms[m];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int n = n0 + wn * 64 + nt * 32 + j;
+        if (n < HW) O[(int64_t)m * HW + n] = acc[mt][nt][r] + bias;
+      }
+    }
 }
 
 // Row means in fp64 of `rows` rows of length L (one workgroup per row).
@@ -512,7 +640,26 @@ static int wct_run(const void* cF, const void* sF, void* out, int n, int C, int6
   small_gemm(tmp, Ic, Tm, C, n, 1.0, 0.0, nullptr, st);
   if (int e = launch_status("wct matrix functions")) return e;
 
-  // 6. out = T (cF - mu_c) + mu_s
+  // 6. out = T (cF - mu_c) + mu_s; fp32 features -> fp32 MFMA (RPST_WCT_T_F64=1: fp64)
+  if (SRC == SRC_F32C && OUTM == OUT_F32_BIAS && !env_int("RPST_WCT_T_F64", 0)) {
+    float* Tf = reinterpret_cast<float*>(M0);  // M0 / Mid are free after step 5
+    float* muf = reinterpret_cast<float*>(Mid);
+    const int64_t nT = (int64_t)n * C * C, nmu = (int64_t)2 * n * C;  // mu_c, mu_s adjacent
+    wct_f32_prep_kernel<<<(unsigned)((std::max(nT, nmu) + 255) / 256), 256, 0, st>>>(Tm, mu_c, Tf, muf, nT, nmu);
+    if (int e = launch_status("wct_f32_prep_kernel")) return e;
+    dim3 grid((unsigned)((HW + 127) / 128), (C + 127) / 128, n);
+    const bool vec = (HW % 4 == 0) && (C % 4 == 0) &&
+                     (reinterpret_cast<uintptr_t>(cF) & 15) == 0;
+    if (vec)
+      wct_transform_f32_kernel<true><<<grid, 256, 0, st>>>(
+          Tf, static_cast<const float*>(cF), muf, muf + (size_t)n * C, static_cast<float*>(out),
+          C, (int)HW);
+    else
+      wct_transform_f32_kernel<false><<<grid, 256, 0, st>>>(
+          Tf, static_cast<const float*>(cF), muf, muf + (size_t)n * C, static_cast<float*>(out),
+          C, (int)HW);
+    return launch_status("wct_transform_f32_kernel");
+  }
   G64Args g{};
   g.A = Tm;
   g.B = cF;

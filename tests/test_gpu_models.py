@@ -145,6 +145,23 @@ def test_wct_fuse_vs_oracle(cuda, shape):
     assert rel_l2(out, ref) < TOL_WCT, rel_l2(out, ref)
 
 
+@pytest.mark.parametrize("shape", [(2, 256, 64, 64), (1, 64, 33, 31)])
+def test_wct_fp32_transform_vs_fp64(cuda, shape, monkeypatch):
+    """The colour transform out = T (cF - mu_c) + mu_s runs on the fp32 MFMA (T rounded
+    once from fp64); RPST_WCT_T_F64=1 keeps it in fp64 like wct_rp.py:110-113. The two
+    differ by fp32 accumulation only: bound it at 1e-6 rel-L2 (~16x the output rounding),
+    and both against the fp64 oracle at TOL_WCT."""
+    from rpst import ops
+    c = gen(21, shape, 2.0, 0.3, relu=True).to(cuda)
+    s = gen(22, shape, 1.5, 0.5, relu=True).to(cuda)
+    out32 = ops.wct_fuse(c, s)
+    monkeypatch.setenv("RPST_WCT_T_F64", "1")
+    out64 = ops.wct_fuse(c, s)
+    ref = R.wct_fuse(c.cpu(), s.cpu())
+    assert rel_l2(out32, out64) < 1e-6, rel_l2(out32, out64)
+    assert rel_l2(out32, ref) < TOL_WCT and rel_l2(out64, ref) < TOL_WCT
+
+
 def test_wct_rp_vs_oracle_hidden16(cuda):
     import network as net
     from rpst import synth
