@@ -42,6 +42,12 @@ struct G64Args {
   int ksplit;           // split-K factor (OUT_PARTIAL)
   int sym;              // only upper-triangular tiles (blockIdx.x enumerates them)
   int tiles_n;
+  // dual launch: batch entries z >= dual run C2 = A2 B2 (same shape / strides; ksplit 1),
+  // so two independent products share one launch (0 = off)
+  const void* A2;
+  const void* B2;
+  void* C2;
+  int dual;
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -115,7 +121,17 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
     tj = blockIdx.x;
   }
   const int z = blockIdx.z;
-  const int b = z / g.ksplit, split = z - b * g.ksplit;
+  int b = z / g.ksplit;
+  const int split = z - b * g.ksplit;
+  const void* gA = g.A;
+  const void* gB = g.B;
+  void* gC = g.C;
+  if (g.dual && b >= g.dual) {
+    b -= g.dual;
+    gA = g.A2;
+    gB = g.B2;
+    gC = g.C2;
+  }
   const int m0 = ti * BT, n0 = tj * BT;
   // split-K ranges are whole BK tiles
   const int kper = ((g.K + g.ksplit - 1) / g.ksplit + BK - 1) / BK * BK;
@@ -123,8 +139,8 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
   const int kend = min(g.K, kbeg + kper);
 
   constexpr unsigned ESA = SRCA == SRC_F32C ? 4u : 8u, ESB = SRCB == SRC_F32C ? 4u : 8u;
-  const char* Ab = static_cast<const char*>(g.A) + (int64_t)b * g.sA * ESA;
-  const char* Bb = static_cast<const char*>(g.B) + (int64_t)b * g.sB * ESB;
+  const char* Ab = static_cast<const char*>(gA) + (int64_t)b * g.sA * ESA;
+  const char* Bb = static_cast<const char*>(gB) + (int64_t)b * g.sB * ESB;
   const __amdgpu_buffer_rsrc_t ra = rsrc(Ab, (unsigned)g.M * g.lda * ESA);
   const __amdgpu_buffer_rsrc_t rb =
       rsrc(Bb, BLAY == B_NK ? (unsigned)g.N * g.ldb * ESB : (unsigned)g.K * g.ldb * ESB);
@@ -230,14 +246,14 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
         if (n >= g.N) continue;
         const double v = acc[i][jn][r];
         if (OUT == OUT_PARTIAL) {
-          static_cast<double*>(g.C)[(int64_t)z * g.sC + (int64_t)m * g.ldc + n] = v;
+          static_cast<double*>(gC)[(int64_t)z * g.sC + (int64_t)m * g.ldc + n] = v;
         } else if (OUT == OUT_F64) {
-          static_cast<double*>(g.C)[b * g.sC + (int64_t)m * g.ldc + n] =
+          static_cast<double*>(gC)[b * g.sC + (int64_t)m * g.ldc + n] =
               alpha * v + (m == n ? g.beta_diag : 0.0);
         } else if (OUT == OUT_F32_BIAS) {
-          static_cast<float*>(g.C)[b * g.sC + (int64_t)m * g.ldc + n] = (float)(v + bias);
+          static_cast<float*>(gC)[b * g.sC + (int64_t)m * g.ldc + n] = (float)(v + bias);
         } else {
-          static_cast<double*>(g.C)[b * g.sC + (int64_t)m * g.ldc + n] = v + bias;
+          static_cast<double*>(gC)[b * g.sC + (int64_t)m * g.ldc + n] = v + bias;
         }
       }
     }
@@ -253,15 +269,21 @@ __global__ __launch_bounds__(256) void wct_f32_prep_kernel(const double* __restr
                                                            const double* __restrict__ mu,
                                                            float* __restrict__ Tf,
                                                            float* __restrict__ muf, int64_t nT,
-                                                           int64_t nmu) {
+                                                           int64_t nmu, int C) {
+  // Tf = T^T per image ([k][m], output channels contiguous) so both GEMM operands stage
+  // with 16-B loads and 16-B LDS stores
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < nT) Tf[i] = (float)T[i];
+  if (i < nT) {
+    const int64_t cc = (int64_t)C * C, b = i / cc, r = i - b * cc;
+    const int m = (int)(r / C), k = (int)(r - (int64_t)m * C);
+    Tf[b * cc + (int64_t)k * C + m] = (float)T[i];
+  }
   if (i < nmu) muf[i] = (float)mu[i];
 }
 
 // Block tile 128 (m = output channel) x 128 (n = pixel), K = C in steps of 32, 4 waves of
 // 64 x 64 on v_mfma_f32_32x32x2f32; register-prefetched staging of the next K step.
-// A = T [n][C][C] (k contiguous), B = cF [n][C][HW] (pixels contiguous) centred by mu_c[k]
+// A = T^T [n][C(k)][C(m)] (m contiguous), B = cF [n][C][HW] (pixels contiguous) centred by mu_c[k]
 // while staged, epilogue adds mu_s[m]. VEC: 16-B loads (HW % 4 == 0, C % 4 == 0).
 template <bool VEC>
 __global__ __launch_bounds__(256, 2) void wct_transform_f32_kernel(
@@ -290,21 +312,20 @@ __global__ __launch_bounds__(256, 2) void wct_transform_f32_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
 
-  // A staging: thread -> (row ar + 32p, k-run ak..ak+3); B: (k-row bk + 8p, n-run bn..bn+3)
-  const int ar = tid >> 3, ak = (tid & 7) * 4;
+  // staging of both operands: thread -> (k-row bk + 8p, run bn..bn+3 of m or n)
   const int bk = tid >> 5, bn = (tid & 31) * 4;
   float ra[16], rb[16];
   auto load = [&](int k0) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const int m = m0 + ar + 32 * p, k = k0 + ak;
+      const int k = k0 + bk + 8 * p, m = m0 + bn;
       if (VEC) {
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (m < C && k < C) v = *reinterpret_cast<const float4*>(A + (int64_t)m * C + k);
+        if (k < C && m < C) v = *reinterpret_cast<const float4*>(A + (int64_t)k * C + m);
         ra[4 * p] = v.x; ra[4 * p + 1] = v.y; ra[4 * p + 2] = v.z; ra[4 * p + 3] = v.w;
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ra[4 * p + e] = (m < C && k + e < C) ? A[(int64_t)m * C + k + e] : 0.f;
+        for (int e = 0; e < 4; ++e) ra[4 * p + e] = (k < C && m + e < C) ? A[(int64_t)k * C + m + e] : 0.f;
       }
     }
 #pragma unroll
@@ -325,8 +346,8 @@ __global__ __launch_bounds__(256, 2) void wct_transform_f32_kernel(
   auto store = [&]() {
 #pragma unroll
     for (int p = 0; p < 4; ++p)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) As[(ak + e) * LD + ar + 32 * p] = ra[4 * p + e];
+      *reinterpret_cast<float4*>(As + (bk + 8 * p) * LD + bn) =
+          make_float4(ra[4 * p], ra[4 * p + 1], ra[4 * p + 2], ra[4 * p + 3]);
 #pragma unroll
     for (int p = 0; p < 4; ++p)
       *reinterpret_cast<float4*>(Bs + (bk + 8 * p) * LD + bn) =
@@ -473,6 +494,7 @@ static void gemm64(const G64Args& g, dim3 grid, hipStream_t st) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   bool vec = al(g.A) && al(g.B) && g.lda % va == 0 && g.ldb % vb == 0 && g.K % va == 0 &&
              g.sA % va == 0 && g.sB % vb == 0;
+  if (g.dual) vec = vec && al(g.A2) && al(g.B2);
   if (BLAY == B_NK) vec = vec && g.K % vb == 0;
   else vec = vec && g.N % vb == 0;
   if (vec)
@@ -481,13 +503,29 @@ static void gemm64(const G64Args& g, dim3 grid, hipStream_t st) {
     gemm_f64_kernel<BT, SRCA, SRCB, BLAY, OUT, false><<<grid, 256, 0, st>>>(g);
 }
 
+static int env_int(const char* name, int dflt);
+
 // C[b] = alpha*avec[b]*A[b]B[b] + beta_diag*I for batched n x n fp64 matrices.
 static void small_gemm(const double* A, const double* B, double* C, int n, int batch,
-                       double alpha, double beta_diag, const double* avec, hipStream_t st) {
+                       double alpha, double beta_diag, const double* avec, hipStream_t st,
+                       const double* A2 = nullptr, const double* B2 = nullptr,
+                       double* C2 = nullptr) {
+  if (A2 && 2 * batch > 65535) {  // grid.z limit: two launches
+    small_gemm(A, B, C, n, batch, alpha, beta_diag, avec, st);
+    small_gemm(A2, B2, C2, n, batch, alpha, beta_diag, avec, st);
+    return;
+  }
   G64Args g{};
   g.A = A;
   g.B = B;
   g.C = C;
+  if (A2) {  // second product C2 = A2 B2 in the same launch
+    g.A2 = A2;
+    g.B2 = B2;
+    g.C2 = C2;
+    g.dual = batch;
+  }
+  const int zb = A2 ? 2 * batch : batch;
   g.avec = avec;
   g.alpha = alpha;
   g.beta_diag = beta_diag;
@@ -495,8 +533,16 @@ static void small_gemm(const double* A, const double* B, double* C, int n, int b
   g.lda = g.ldb = g.ldc = n;
   g.sA = g.sB = g.sC = (int64_t)n * n;
   g.ksplit = 1;
-  const int t = (n + 63) / 64;
-  gemm64<64, SRC_F64, SRC_F64, B_KN, OUT_F64>(g, dim3(t, t, batch), st);
+  // 32x32 tiles: at n = 256, batch 16 that is 1024 workgroups instead of 256 (one per CU
+  // would leave each CU a single latency-bound 64x64 tile); RPST_WCT_NS_BT=64 restores
+  const int bt = env_int("RPST_WCT_NS_BT", 32);
+  if (bt == 32) {
+    const int t = (n + 31) / 32;
+    gemm64<32, SRC_F64, SRC_F64, B_KN, OUT_F64>(g, dim3(t, t, zb), st);
+  } else {
+    const int t = (n + 63) / 64;
+    gemm64<64, SRC_F64, SRC_F64, B_KN, OUT_F64>(g, dim3(t, t, zb), st);
+  }
 }
 
 constexpr int kNSIters = 40;
@@ -514,8 +560,7 @@ static void ns_power(const double* A, double add, double* sqrt_out, double* isqr
   ns_init_kernel<<<batch, 256, 0, st>>>(A, Y, Z, svec, n, add);
   for (int it = 0; it < kNSIters; ++it) {
     small_gemm(Z, Y, T, n, batch, -0.5, 1.5, nullptr, st);  // T = (3I - ZY)/2
-    small_gemm(Y, T, Y2, n, batch, 1.0, 0.0, nullptr, st);  // Y <- Y T
-    small_gemm(T, Z, Z2, n, batch, 1.0, 0.0, nullptr, st);  // Z <- T Z
+    small_gemm(Y, T, Y2, n, batch, 1.0, 0.0, nullptr, st, T, Z, Z2);  // Y <- Y T, Z <- T Z
     double* t = Y;
     Y = Y2;
     Y2 = t;
@@ -645,7 +690,7 @@ static int wct_run(const void* cF, const void* sF, void* out, int n, int C, int6
     float* Tf = reinterpret_cast<float*>(M0);  // M0 / Mid are free after step 5
     float* muf = reinterpret_cast<float*>(Mid);
     const int64_t nT = (int64_t)n * C * C, nmu = (int64_t)2 * n * C;  // mu_c, mu_s adjacent
-    wct_f32_prep_kernel<<<(unsigned)((std::max(nT, nmu) + 255) / 256), 256, 0, st>>>(Tm, mu_c, Tf, muf, nT, nmu);
+    wct_f32_prep_kernel<<<(unsigned)((std::max(nT, nmu) + 255) / 256), 256, 0, st>>>(Tm, mu_c, Tf, muf, nT, nmu, C);
     if (int e = launch_status("wct_f32_prep_kernel")) return e;
     dim3 grid((unsigned)((HW + 127) / 128), (C + 127) / 128, n);
     const bool vec = (HW % 4 == 0) && (C % 4 == 0) &&
