@@ -581,12 +581,14 @@ static int env_int(const char* name, int dflt) {
 }
 
 static int pick_ksplit(int batch, int tiles, int64_t K) {
-  // aim for ~2048 workgroups, each with >= 4096 K values
-  const int64_t target = env_int("RPST_WCT_BLOCKS", 4096);
+  // aim for ~4096 workgroups per covariance launch, each with >= kmin K values
+  // (profiles/r01_wct_blocks.log: 8192 -> 27.6 ms vs 28.9 at 4096)
+  const int64_t target = env_int("RPST_WCT_BLOCKS", 8192);
+  const int64_t kmin = env_int("RPST_WCT_KMIN", 4096);
   int s = (int)((target + (int64_t)batch * tiles - 1) / ((int64_t)batch * tiles));
-  const int64_t maxs = K / 4096 > 1 ? K / 4096 : 1;
+  const int64_t maxs = K / kmin > 1 ? K / kmin : 1;
   if (s > maxs) s = (int)maxs;
-  return s < 1 ? 1 : (s > 64 ? 64 : s);
+  return s < 1 ? 1 : (s > 128 ? 128 : s);
 }
 
 struct WctLayout {
