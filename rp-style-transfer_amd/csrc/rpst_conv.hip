@@ -376,6 +376,83 @@ static int pad_cout(int Cout) {
 
 static int ck_of(int ksize) { return ksize == 3 ? ConvK<3>::CK : ConvK<1>::CK; }
 
+// ---- narrow 3x3 layers on the VALU ------------------------------------------------------
+// Cin * Cout <= 64 (the RP stacks' 3->16 input and 16->3 output convs, rp.py encoder /
+// decoder ends): an MFMA tile pads such a layer to 32 output channels (16->3: 10x the
+// work) or 8 input channels, so these run as plain FMAs instead. Block = 8 rows x 64
+// columns, 256 threads (column, row pair); per input channel the (8+2) x (64+2) patch is
+// staged in LDS with the padding resolved, weights [ci][tap][co] sit in LDS for the
+// whole block. Same epilogue as the direct kernel: bias, activation, residual.
+constexpr int kNrTH = 8, kNrTW = 64, kNrPW = kNrTW + 2, kNrPS = (kNrTH + 2) * kNrPW;
+
+static bool narrow_shape(int Cin, int Cout) {
+  return (Cout <= 4 && Cin <= 16) || (Cout <= 16 && Cin <= 4);
+}
+
+template <int CO>
+__global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
+  constexpr int CK = ConvK<3>::CK;
+  __shared__ float patch[kNrPS];
+  __shared__ float wl[64 * 9];  // Cin * 9 * CO <= 576
+  const int x0 = blockIdx.x * kNrTW, y0 = blockIdx.y * kNrTH, n = blockIdx.z;
+  const int tid = threadIdx.x, col = tid & 63, rg = tid >> 6;  // output rows 2 rg, 2 rg + 1
+  // direct-packed weights [ci / CK][tap][ci % CK][Cout_pad] (zero beyond Cout)
+  for (int i = tid; i < a.Cin * 9 * CO; i += 256) {
+    const int co = i % CO, t = (i / CO) % 9, ci = i / (9 * CO);
+    wl[i] = a.wpk[((int64_t)(ci / CK) * 9 + t) * CK * a.Cout_pad + (ci % CK) * a.Cout_pad + co];
+  }
+  float acc[2][CO];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int co = 0; co < CO; ++co) acc[r][co] = 0.f;
+  const int64_t plane = (int64_t)a.H * a.W;
+  const float* in = a.in + (int64_t)n * a.Cin * plane;
+  for (int ci = 0; ci < a.Cin; ++ci) {
+    __syncthreads();  // the previous channel's patch is consumed (first pass: weights)
+    for (int i = tid; i < kNrPS; i += 256) {
+      const int r = i / kNrPW, c = i - r * kNrPW;
+      int y = y0 - 1 + r, x = x0 - 1 + c;
+      const bool oky = resolve(y, a.H, a.pad, true), okx = resolve(x, a.W, a.pad, true);
+      patch[i] = oky && okx ? in[ci * plane + (int64_t)y * a.W + x] : 0.f;
+    }
+    __syncthreads();
+    float win[4][3];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) win[r][c] = patch[(2 * rg + r) * kNrPW + col + c];
+    const float* w = wl + ci * 9 * CO;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int co = 0; co < CO; ++co) {
+        const float wv = w[t * CO + co];
+        acc[0][co] = fmaf(win[t / 3][t % 3], wv, acc[0][co]);
+        acc[1][co] = fmaf(win[t / 3 + 1][t % 3], wv, acc[1][co]);
+      }
+  }
+  const int x = x0 + col;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int y = y0 + 2 * rg + r;
+    if (y >= a.H || x >= a.W) continue;
+#pragma unroll
+    for (int co = 0; co < CO; ++co) {
+      if (co >= a.Cout) break;
+      const int64_t o = ((int64_t)n * a.Cout + co) * plane + (int64_t)y * a.W + x;
+      float v = activate(acc[r][co] + (a.bias ? a.bias[co] : 0.f), a.relu);
+      if (a.res) v += a.res[o];
+      a.out[o] = v;
+    }
+  }
+}
+
+static bool narrow_enabled() {
+  const char* e = getenv("RPST_CONV_NARROW");  // A/B switch
+  return !(e && *e && atoi(e) == 0);
+}
+
 // Tile variants per BM. RPST_CONV_VARIANT (tools/bench_conv.py) forces one for tuning;
 // otherwise pick_variant() chooses from the measured table (profiles/r01_bench_conv.log):
 //   BM=128: 3x3 -> v1 (128 co x 8x32 px, 8 accumulators/wave, 134-143 TF/s);
@@ -489,6 +566,8 @@ static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
   // 3-channel input layers (3->16, VGG 3->64) and the remaining 16-wide outputs run
   // faster direct
   if (Cin < 16) return RPST_CONV_DIRECT;
+  if (in_op == RPST_IN_NONE && narrow_shape(Cin, Cout) && narrow_enabled())
+    return RPST_CONV_DIRECT;  // 16->3: conv3x3_narrow_kernel
   if (w4 && !t_conv_precise) return RPST_CONV_WINOGRAD4;
   if (w4) return RPST_CONV_WINOGRAD;  // precise mode, same shapes as F(4x4)
   return Cout >= 32 ? RPST_CONV_WINOGRAD : RPST_CONV_DIRECT;
@@ -713,6 +792,16 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * N * a.co_tiles;
   RPST_REQUIRE(blocks <= 0x7fffffffLL, "conv2d: grid too large");
   if (args_out) *args_out = a;
+  if (ksize == 3 && in_op == RPST_IN_NONE && !stat_part && narrow_shape(Cin, Cout) &&
+      narrow_enabled()) {
+    dim3 grid((unsigned)((a.W + kNrTW - 1) / kNrTW), (unsigned)((a.H + kNrTH - 1) / kNrTH), N);
+    RPST_REQUIRE(N <= 65535 && grid.y <= 65535, "conv2d: grid too large");
+    if (Cout <= 4)
+      conv3x3_narrow_kernel<4><<<grid, 256, 0, st>>>(a);
+    else
+      conv3x3_narrow_kernel<16><<<grid, 256, 0, st>>>(a);
+    return launch_status("conv3x3_narrow_kernel");
+  }
   if (ksize == 1) {
     RPST_REQUIRE(in_op == RPST_IN_NONE, "conv2d: 1x1 conv supports in_op NONE only");
     launch_conv<1, RPST_IN_NONE>(a, cfg.BM, variant, st);

@@ -138,6 +138,10 @@ CONV_CASES = [
     (2, 16, 9, 35, 64, 3, 1, 2, True),      # upsample of an odd source
     (2, 64, 33, 130, 96, 3, 0, 0, True),    # F(4x4) interior (16-B DMA) block + edges, ragged H
     (1, 32, 20, 200, 64, 3, 1, 0, False),   # reflect: two interior blocks, partial last block
+    (2, 3, 70, 130, 16, 3, 0, 0, True),     # narrow VALU kernel: RP encoder first, ragged blocks
+    (2, 16, 17, 70, 3, 3, 1, 0, False),     # narrow: 16->3 reflect, no relu
+    (1, 4, 9, 66, 16, 3, 1, 0, True),       # narrow: Cin 4 -> 16
+    (1, 16, 2, 2, 4, 3, 1, 0, False),       # narrow: tiny reflect
 ]
 
 

@@ -12,7 +12,7 @@ LAYERS = ["3->16 N64", "16->32 N64", "32->64 N64", "64->128 N64", "128->256 N64"
 
 
 def main(path):
-    rows = [r for r in csv.DictReader(open(path)) if "mfma_kernel" in r["Kernel_Name"]
+    rows = [r for r in csv.DictReader(open(path)) if ("mfma_kernel" in r["Kernel_Name"] or "narrow_kernel" in r["Kernel_Name"])
             and "wgrad" not in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     n = len(LAYERS)
