@@ -379,31 +379,31 @@ static int ck_of(int ksize) { return ksize == 3 ? ConvK<3>::CK : ConvK<1>::CK; }
 // ---- narrow 3x3 layers on the VALU ------------------------------------------------------
 // Cin * Cout <= 64 (the RP stacks' 3->16 input and 16->3 output convs, rp.py encoder /
 // decoder ends): an MFMA tile pads such a layer to 32 output channels (16->3: 10x the
-// work) or 8 input channels, so these run as plain FMAs instead. Block = 8 rows x 64
-// columns, 256 threads (column, row pair); per input channel the (8+2) x (64+2) patch is
+// work) or 8 input channels, so these run as plain FMAs instead. Block = 4 RPT rows x 64
+// columns, 256 threads (column, RPT rows); per input channel the (4 RPT+2) x 66 patch is
 // staged in LDS with the padding resolved, weights [ci][tap][co] sit in LDS for the
 // whole block. Same epilogue as the direct kernel: bias, activation, residual.
-constexpr int kNrTH = 8, kNrTW = 64, kNrPW = kNrTW + 2, kNrPS = (kNrTH + 2) * kNrPW;
+constexpr int kNrTW = 64, kNrPW = kNrTW + 2;
 
 static bool narrow_shape(int Cin, int Cout) {
   return (Cout <= 4 && Cin <= 16) || (Cout <= 16 && Cin <= 4);
 }
 
-template <int CO>
+template <int CO, int RPT>  // RPT output rows per thread: block = 4 RPT rows x 64 columns
 __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
-  constexpr int CK = ConvK<3>::CK;
+  constexpr int CK = ConvK<3>::CK, kNrTH = 4 * RPT, kNrPS = (kNrTH + 2) * kNrPW;
   __shared__ float patch[kNrPS];
   __shared__ float wl[64 * 9];  // Cin * 9 * CO <= 576
   const int x0 = blockIdx.x * kNrTW, y0 = blockIdx.y * kNrTH, n = blockIdx.z;
-  const int tid = threadIdx.x, col = tid & 63, rg = tid >> 6;  // output rows 2 rg, 2 rg + 1
+  const int tid = threadIdx.x, col = tid & 63, rg = tid >> 6;  // output rows RPT rg ..
   // direct-packed weights [ci / CK][tap][ci % CK][Cout_pad] (zero beyond Cout)
   for (int i = tid; i < a.Cin * 9 * CO; i += 256) {
     const int co = i % CO, t = (i / CO) % 9, ci = i / (9 * CO);
     wl[i] = a.wpk[((int64_t)(ci / CK) * 9 + t) * CK * a.Cout_pad + (ci % CK) * a.Cout_pad + co];
   }
-  float acc[2][CO];
+  float acc[RPT][CO];
 #pragma unroll
-  for (int r = 0; r < 2; ++r)
+  for (int r = 0; r < RPT; ++r)
 #pragma unroll
     for (int co = 0; co < CO; ++co) acc[r][co] = 0.f;
   const int64_t plane = (int64_t)a.H * a.W;
@@ -417,25 +417,25 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
       patch[i] = oky && okx ? in[ci * plane + (int64_t)y * a.W + x] : 0.f;
     }
     __syncthreads();
-    float win[4][3];
+    float win[RPT + 2][3];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < RPT + 2; ++r)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) win[r][c] = patch[(2 * rg + r) * kNrPW + col + c];
+      for (int c = 0; c < 3; ++c) win[r][c] = patch[(RPT * rg + r) * kNrPW + col + c];
     const float* w = wl + ci * 9 * CO;
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
       for (int co = 0; co < CO; ++co) {
         const float wv = w[t * CO + co];
-        acc[0][co] = fmaf(win[t / 3][t % 3], wv, acc[0][co]);
-        acc[1][co] = fmaf(win[t / 3 + 1][t % 3], wv, acc[1][co]);
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) acc[r][co] = fmaf(win[t / 3 + r][t % 3], wv, acc[r][co]);
       }
   }
   const int x = x0 + col;
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int y = y0 + 2 * rg + r;
+  for (int r = 0; r < RPT; ++r) {
+    const int y = y0 + RPT * rg + r;
     if (y >= a.H || x >= a.W) continue;
 #pragma unroll
     for (int co = 0; co < CO; ++co) {
@@ -794,12 +794,19 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   if (args_out) *args_out = a;
   if (ksize == 3 && in_op == RPST_IN_NONE && !stat_part && narrow_shape(Cin, Cout) &&
       narrow_enabled()) {
-    dim3 grid((unsigned)((a.W + kNrTW - 1) / kNrTW), (unsigned)((a.H + kNrTH - 1) / kNrTH), N);
+    // rows per thread: 4 for Cout <= 4 (16->3: 0.307 vs 0.348 ms), 2 for Cout <= 16
+    // (3->16 at 4 rows spills: 1.47 vs 0.51 ms); RPST_CONV_NARROW_RPT=2|4 overrides
+    const char* e = getenv("RPST_CONV_NARROW_RPT");
+    const int rpt = (e && *e) ? (atoi(e) == 4 ? 4 : 2) : (Cout <= 4 ? 4 : 2);
+    dim3 grid((unsigned)((a.W + kNrTW - 1) / kNrTW), (unsigned)((a.H + 4 * rpt - 1) / (4 * rpt)), N);
     RPST_REQUIRE(N <= 65535 && grid.y <= 65535, "conv2d: grid too large");
-    if (Cout <= 4)
-      conv3x3_narrow_kernel<4><<<grid, 256, 0, st>>>(a);
-    else
-      conv3x3_narrow_kernel<16><<<grid, 256, 0, st>>>(a);
+    if (Cout <= 4) {
+      if (rpt == 4) conv3x3_narrow_kernel<4, 4><<<grid, 256, 0, st>>>(a);
+      else conv3x3_narrow_kernel<4, 2><<<grid, 256, 0, st>>>(a);
+    } else {
+      if (rpt == 4) conv3x3_narrow_kernel<16, 4><<<grid, 256, 0, st>>>(a);
+      else conv3x3_narrow_kernel<16, 2><<<grid, 256, 0, st>>>(a);
+    }
     return launch_status("conv3x3_narrow_kernel");
   }
   if (ksize == 1) {
