@@ -794,18 +794,17 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   if (args_out) *args_out = a;
   if (ksize == 3 && in_op == RPST_IN_NONE && !stat_part && narrow_shape(Cin, Cout) &&
       narrow_enabled()) {
-    // rows per thread: 4 for Cout <= 4 (16->3: 0.307 vs 0.348 ms), 2 for Cout <= 16
-    // (3->16 at 4 rows spills: 1.47 vs 0.51 ms); RPST_CONV_NARROW_RPT=2|4 overrides
+    // rows per thread: 4 for Cout <= 4 (16->3: 0.307 vs 0.348 ms; RPST_CONV_NARROW_RPT=2
+    // overrides), 2 for Cout <= 16 (3->16 at 4 rows spills to scratch: 1.47 vs 0.51 ms)
     const char* e = getenv("RPST_CONV_NARROW_RPT");
-    const int rpt = (e && *e) ? (atoi(e) == 4 ? 4 : 2) : (Cout <= 4 ? 4 : 2);
+    const int rpt = Cout <= 4 && !(e && *e && atoi(e) == 2) ? 4 : 2;
     dim3 grid((unsigned)((a.W + kNrTW - 1) / kNrTW), (unsigned)((a.H + 4 * rpt - 1) / (4 * rpt)), N);
     RPST_REQUIRE(N <= 65535 && grid.y <= 65535, "conv2d: grid too large");
     if (Cout <= 4) {
       if (rpt == 4) conv3x3_narrow_kernel<4, 4><<<grid, 256, 0, st>>>(a);
       else conv3x3_narrow_kernel<4, 2><<<grid, 256, 0, st>>>(a);
     } else {
-      if (rpt == 4) conv3x3_narrow_kernel<16, 4><<<grid, 256, 0, st>>>(a);
-      else conv3x3_narrow_kernel<16, 2><<<grid, 256, 0, st>>>(a);
+      conv3x3_narrow_kernel<16, 2><<<grid, 256, 0, st>>>(a);
     }
     return launch_status("conv3x3_narrow_kernel");
   }
