@@ -5,17 +5,26 @@ hidden_dim=16), batch 32 per GPU, 512x512 fp32, synthetic U[0,1) images and
 He-uniform synthetic weights (no checkpoints exist offline). One "step" = one test()
 call over the whole per-GPU batch, inputs already resident in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--model adain|wct|sanet|multiscale|source]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model adain|wct|sanet|...]
+    python bench.py --config 4 [--gpus 8]     # BASELINE configs[4]: 1024^2, 128 images
+                                              # split over the GPUs, host gather timed
 
-N>1 runs one process per GPU under torch.distributed.run; each rank stylises its own
-batch (weak scaling: the batch is split per image, no collective touches the data; a
-barrier and a MAX over per-rank times are the only communication).
+--gpus N > 1 runs one process per GPU. Under torch.distributed.run (WORLD_SIZE set, the
+driver's launch) each process is one rank; started directly, bench.py launches
+torch.distributed.run itself as a CHILD process before anything touches the GPU and exits
+with its code. Each rank stylises its own images (per-image split, no collective touches
+the data); a barrier before and after the timed steps and a MAX over per-rank times are
+the only communication. Weak scaling by default (per-GPU batch fixed); --global-batch G
+splits G images over the ranks (strong scaling). --gather copies every step's output into
+one host buffer shared by all ranks (/dev/shm, each rank's slice page-locked) inside the
+timed region: the "results gathered on the host" of BASELINE configs[4].
 
 The JSON line also carries:
   roofline     the dominant kernel's algorithmic FLOP (or bytes) per launch divided by
                its mean launch time, measured with HIP events on the launch stream
-               during the timed steps, against the MI355X peak;
-  roofline_adain  the same for the AdaIN statistics+apply path (HBM-bound);
+               during the timed steps, against the MI355X peak; "traffic" is that
+               launch's HBM bytes from the committed per-dispatch PMC table;
+  roofline_adain  the same for the AdaIN statistics+apply pair (HBM-bound);
   roofline_adain_stats  calc_mean_std alone (the AdaIN statistics path: one read of the
                feature, 4 B per element) against the HBM peak;
   cpu_baseline the CPU oracle (PyTorch-CPU restatement of the reference) timed on this
@@ -27,19 +36,23 @@ import argparse
 import copy
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "rp-style-transfer_amd"))
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (matrix = vector rate), MI355X_MICROARCH.md
 PEAK_FP64_TFLOPS = 78.6    # MI355X dense FP64 matrix (vendor spec)
 PEAK_HBM_GBS = 8000.0      # HBM3E 8 TB/s
+
+# BASELINE.json configs[i] -> (model, image side, per-GPU batch or None, global batch, gather)
+CONFIGS = {1: ("adain", 512, 32, None, False), 2: ("wct", 512, 16, None, False),
+           3: ("sanet", 512, 32, None, False), 4: ("adain", 1024, None, 128, True)}
 
 
 def build_model(kind, dev):
@@ -78,23 +91,46 @@ ADAPTIVE_CONFIG = {"ada_module": "relu", "content_weight": 1.0, "style_weight": 
 
 
 WORKLOADS = {
-    "adain": "AdaINRPNet.test() rp_blocks=5 hidden_dim=16, 512x512 (BASELINE configs[1])",
-    "wct": "WCTRPNet.test() rp_blocks=5 hidden_dim=16, 512x512, fp64 WCT (BASELINE configs[2])",
-    "sanet": "SAModel.test() VGG relu1_1-5_1 + SANet 4_1/5_1 + decoder, 512x512 (BASELINE configs[3])",
-    "multiscale": "MultiScaleAdaINRPNet.test() constant stack hidden 32 x 5, 512x512 (SURVEY 8(f) rank 1)",
-    "source": "SourceNet.test() VGG relu4_1 AdaIN + decoder, 512x512 (SURVEY 8(f) rank 3)",
-    "adaptive": "AdaptiveSAModel.test() ada_module=relu (AEA clamp) VGG relu1_1-5_1 + decoder, "
-                "512x512 (SURVEY 8(f) rank 3)",
+    "adain": "AdaINRPNet.test() rp_blocks=5 hidden_dim=16 (BASELINE configs[1] at 512x512, "
+             "configs[4] at 1024x1024)",
+    "wct": "WCTRPNet.test() rp_blocks=5 hidden_dim=16, fp64 WCT (BASELINE configs[2])",
+    "sanet": "SAModel.test() VGG relu1_1-5_1 + SANet 4_1/5_1 + decoder (BASELINE configs[3])",
+    "multiscale": "MultiScaleAdaINRPNet.test() constant stack hidden 32 x 5 (SURVEY 8(f) rank 1)",
+    "source": "SourceNet.test() VGG relu4_1 AdaIN + decoder (SURVEY 8(f) rank 3)",
+    "adaptive": "AdaptiveSAModel.test() ada_module=relu (AEA clamp) VGG relu1_1-5_1 + decoder "
+                "(SURVEY 8(f) rank 3)",
     "train": "AdaINRPNet training iteration: forward() losses + total_loss.backward() + Adam "
-             "step, rp_blocks=5 hidden_dim=16, 512x512 (SURVEY 8(f) rank 2; gradients "
-             "all-reduced over ranks)",
+             "step, rp_blocks=5 hidden_dim=16 (SURVEY 8(f) rank 2; gradients all-reduced "
+             "over ranks)",
+    "selftest": "CPU stand-in per-image function (launcher / timing / gather test only)",
 }
 DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32, "multiscale": 32, "source": 32,
-                 "adaptive": 32, "train": 8}
+                 "adaptive": 32, "train": 8, "selftest": 4}
+# CPU-baseline sample per workload (BASELINE.md plan: B=2 at 512^2, B=1 for WCT)
+CPU_SAMPLE_BATCH = {"wct": 1, "train": 1}
 
 
-def cpu_baseline(kind, size, budget_s=12.0):
-    """Time the CPU oracle on a bounded sample: one content/style pair at size^2."""
+def cpu_info():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return model, os.cpu_count(), avail
+
+
+def cpu_baseline(kind, size, reps=3):
+    """Time the CPU oracle on a bounded sample: B=2 content/style pairs at size^2 (B=1 for
+    WCT and training), one warm-up then the median of `reps` runs."""
+    import torch
     from oracle import restate as R
     from rpst import synth
     import network as net
@@ -123,46 +159,46 @@ def cpu_baseline(kind, size, budget_s=12.0):
     synth.synth_module_(m, 0)
     # (.cpu(): SourceNet shares the module-level decoder, which build_model moved to the GPU)
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
-    c = torch.from_numpy(synth.image(11, (1, 3, size, size)))
-    s = torch.from_numpy(synth.image(12, (1, 3, size, size)))
+    b = CPU_SAMPLE_BATCH.get(kind, 2)
+    c = torch.from_numpy(synth.image(11, (b, 3, size, size)))
+    s = torch.from_numpy(synth.image(12, (b, 3, size, size)))
     threads = torch.get_num_threads()
     fn(c, s, sd)  # warm-up
-    reps, t0 = 0, time.perf_counter()
-    while reps < 8:
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
         fn(c, s, sd)
-        reps += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": reps / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle {kind} test() on {reps} x 1 pair at {size}x{size}, "
-                      f"{threads} threads, {dt:.1f}s"}
+        times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    model, host_cpus, avail = cpu_info()
+    return {"value": b / med, "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cpus": host_cpus, "cpus_available": avail,
+            "sample": f"oracle (PyTorch-CPU restatement) {kind} test() on B={b} at "
+                      f"{size}x{size}, median of {reps} after 1 warm-up ({med:.2f}s each), "
+                      f"{threads} torch threads"}
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic_final.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 
 
-def pmc_lookup(kernel_substr, grid=None):
-    """HBM bytes per launch from the committed rocprofv3 PMC table (tools/pmc_traffic.py);
-    None if the kernel/grid was not profiled."""
+def pmc_table():
     if not os.path.exists(PMC_TRAFFIC):
-        return None
-    table = json.load(open(PMC_TRAFFIC))
-    tot = 0.0
-    found = False
-    for k, v in table.items():
-        name, g = k.rsplit("|", 1)
-        if kernel_substr in name and (grid is None or int(g) == grid):
-            tot += v["traffic_bytes"]
-            found = True
-    return tot if found else None
+        return {}
+    return json.load(open(PMC_TRAFFIC))
+
+
+def pmc_lookup(section, key):
+    """HBM bytes per launch of one traced launch (tools/pmc_traffic.py attributes every PMC
+    dispatch to the bench launch that issued it); None if that launch was not profiled."""
+    rec = pmc_table().get(section, {}).get(key)
+    return None if rec is None else rec["traffic_bytes"]
 
 
 def roofline_from_trace(summary):
     from rpst import _lib
     best = None
     for name, a in summary.items():
-        if not name.startswith(("conv", "wino", "wgrad")):
+        if not name.startswith(("conv", "wino", "wgrad", "narrow")):
             continue
         if best is None or a["ms"] > best[1]["ms"]:
             best = (name, a)
@@ -178,18 +214,11 @@ def roofline_from_trace(summary):
     flop = a["flops"] * (0.25 if wino4 else (4.0 / 9.0 if wino else 1.0))
     achieved = flop / (avg_ms * 1e-3) / 1e12
     effective = a["flops"] / (avg_ms * 1e-3) / 1e12
-    # "conv3x3 128->256 512x512 N64 op0" -> launch geometry -> PMC record
-    k, chans, hw, nn, op = name.split()
-    cin, cout = (int(v) for v in chans.split("->"))
-    h, w = (int(v) for v in hw.split("x"))
-    n, in_op, ks = int(nn[1:]), int(op[2:]), int(k[-1])
-    hs, ws = ((h * 2, w * 2) if in_op == 1 else ((h // 2, w // 2) if in_op == 2 else (h, w)))
-    if name.startswith("wgrad"):  # weight gradient (training): not in the PMC table
-        kname, traffic = "conv_wgrad_kernel", None
-    else:
-        grid = _lib.load().rpst_conv2d_grid_threads(n, cin, hs, ws, cout, ks, in_op)
-        kname = ("wino4_mfma_kernel" if wino4 else "wino_mfma_kernel") if wino else "conv_mfma_kernel"
-        traffic = pmc_lookup(kname, grid)
+    kname = {"wino4": "wino4_mfma_kernel", "wino": "wino_mfma_kernel",
+             "wgrad": "conv_wgrad_kernel", "narrow": "conv3x3_narrow_kernel"}.get(
+        next((p for p in ("wino4", "wino", "wgrad", "narrow") if name.startswith(p)), ""),
+        "conv_mfma_kernel")
+    traffic = pmc_lookup("launches", name)
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
             "traffic": traffic, "kernel": f"{kname} [{name}]",
@@ -206,6 +235,7 @@ def measure_adain_standalone(dev, n, c, hw, reps=3):
     """The model path fuses AdaIN into the encoder epilogue / decoder loader, so the
     HBM-bound AdaIN kernel pair (the function-level API, base.py:410-418) is timed on its
     own here, on feature-shaped tensors of the benchmark (n, C, HW), after the timed loop."""
+    import torch
     from rpst import ops
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.rand((n, c, hw), device=dev, generator=g).view(n, c, hw, 1)
@@ -230,10 +260,12 @@ def stats_roofline(summary):
         if name.startswith("stats"):
             avg_ms = a["ms"] / a["launches"]
             gbs = a["bytes"] / (avg_ms * 1e-3) / 1e9
+            traffic = pmc_lookup("stats", name)
             return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
                     "kernel": f"plane_stats_kernel + stat merge [{name}]",
-                    "launch_ms": round(avg_ms, 4), "bytes_per_launch": a["bytes"]}
+                    "launch_ms": round(avg_ms, 4), "bytes_per_launch": a["bytes"],
+                    "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None}
     return None
 
 
@@ -242,9 +274,7 @@ def adain_roofline(summary):
         if name.startswith("adain"):
             avg_ms = a["ms"] / a["launches"]
             gbs = a["bytes"] / (avg_ms * 1e-3) / 1e9
-            st = pmc_lookup("plane_stats_kernel")
-            ap = pmc_lookup("plane_apply_kernel<true>")
-            traffic = (st + ap) if (st is not None and ap is not None) else None
+            traffic = pmc_lookup("adain", name)
             return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
                     "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
                     "kernel": f"plane_stats_kernel+plane_apply_kernel [{name}]",
@@ -253,33 +283,140 @@ def adain_roofline(summary):
     return None
 
 
+# ---- launcher -------------------------------------------------------------------------
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(nproc, argv):
+    """Run this script under torch.distributed.run with `nproc` ranks as a child process
+    (the parent never initialises the GPU, so no exec of a GPU process is involved)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+class HostGather:
+    """One host buffer holding the whole output batch, shared by every rank of the node
+    (/dev/shm file mapped by each process); rank r writes images [start, end) of it. Each
+    rank page-locks its own slice (hipHostRegister) so the D2H copy is a direct DMA."""
+
+    def __init__(self, tag, shape, start, end, rank, cuda):
+        import torch
+        self.path = f"/dev/shm/rpst_bench_gather_{tag}"
+        numel = 1
+        for s in shape:
+            numel *= s
+        self.full = torch.from_file(self.path, shared=True, size=numel,
+                                    dtype=torch.float32).view(shape)
+        self.slice = self.full[start:end]
+        self.pinned = False
+        self.rank = rank
+        if cuda and self.slice.numel():
+            cudart = torch.cuda.cudart()
+            rc = cudart.cudaHostRegister(self.slice.data_ptr(),
+                                         self.slice.numel() * 4, 0)
+            self.pinned = int(rc) == 0
+        self.cudart = torch.cuda.cudart() if self.pinned else None
+
+    def put(self, out):
+        self.slice.copy_(out, non_blocking=self.pinned)
+
+    def close(self):
+        if self.pinned:
+            self.cudart.cudaHostUnregister(self.slice.data_ptr())
+        self.slice = self.full = None
+        if self.rank == 0:
+            try:
+                os.unlink(self.path)
+            except OSError:
+                pass
+
+
+def selftest_model():
+    """CPU stand-in for the launcher test: an independent per-image function."""
+    import torch
+
+    class _M:
+        def test(self, c, s):
+            return c * 0.5 + s.mean(dim=(1, 2, 3), keepdim=True)
+    return _M()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", choices=list(WORKLOADS), default="adain")
-    ap.add_argument("--batch", type=int, default=None, help="images per GPU")
-    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--config", type=int, choices=sorted(CONFIGS), default=None,
+                    help="BASELINE.json configs[i] (sets model, size, batch, gather)")
+    ap.add_argument("--model", choices=list(WORKLOADS), default=None)
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="images split over all GPUs (strong scaling)")
+    ap.add_argument("--size", type=int, default=None)
+    ap.add_argument("--gather", action="store_true",
+                    help="copy each step's output into a shared host buffer (timed)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layer-order", default=None,
+                    help="write the traced launch names of one step (tools/pmc_traffic.py)")
     args = ap.parse_args()
 
+    model_kind, size, batch, gbatch, gather = CONFIGS[args.config or 1]
+    if args.config is None:
+        model_kind, size, batch, gbatch, gather = "adain", 512, None, None, False
+    model_kind = args.model or model_kind
+    size = args.size or size
+    gbatch = args.global_batch if args.global_batch is not None else gbatch
+    batch = args.batch or batch or DEFAULT_BATCH[model_kind]
+    gather = gather or args.gather
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    import torch.distributed as dist
     from rpst import ops, synth
+    from rpst.shard import partition
 
-    B = args.batch or DEFAULT_BATCH[args.model]
-    model = build_model(args.model, dev)
-    shape = (B, 3, args.size, args.size)
-    content = torch.from_numpy(synth.image(1000 + rank, shape)).to(dev)
-    style = torch.from_numpy(synth.image(2000 + rank, shape)).to(dev)
+    cuda = model_kind != "selftest"
+    if world > 1:
+        dist.init_process_group("nccl" if cuda else "gloo")
+    if cuda:
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
 
-    if args.model == "train":
+    if gbatch is not None:
+        start, end = partition(gbatch, world, rank)
+        B, scaling, total = end - start, "strong", gbatch
+    else:
+        start, end = rank * batch, (rank + 1) * batch
+        B, scaling, total = batch, "weak", batch * world
+    if B < 1:
+        raise SystemExit(f"bench.py: rank {rank} has no images (global batch {gbatch})")
+    model = selftest_model() if not cuda else build_model(model_kind, dev)
+    shape = (B, 3, size, size)
+    # image i of the global batch is the same tensor whatever the rank count
+    content = torch.from_numpy(synth.image_range(1000, (total, 3, size, size), start, end)).to(dev)
+    style = torch.from_numpy(synth.image_range(2000, (total, 3, size, size), start, end)).to(dev)
+
+    if model_kind == "train":
         from rpst.shard import GradientAllReduce
         params = [p for p in model.parameters() if p.requires_grad]
         optimizer = torch.optim.Adam(params, lr=1e-4)
@@ -287,66 +424,111 @@ def main():
 
         def step():
             optimizer.zero_grad()
-            _, total = model(content, style)
-            total.backward()
+            _, tot = model(content, style)
+            tot.backward()
             if reduce_grads is not None:
                 reduce_grads()
             optimizer.step()
-            return total
+            return tot
     else:
         def step():
             return model.test(content, style)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+    host = None
+    if gather:
+        tag = f"{os.environ.get('MASTER_PORT', 'solo')}_{os.getppid() if world > 1 else os.getpid()}"
+        host = HostGather(tag, (total, 3, size, size), start, end, rank, cuda)
 
-    ops.TRACE = ops.Trace()
+    for _ in range(args.warmup):
+        out = step()
+        if host is not None:
+            host.put(out)
+    sync()
+
+    ops.TRACE = ops.Trace() if cuda else None
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = step()
-    torch.cuda.synchronize()
+        if host is not None:
+            host.put(out)
+    sync()
+    dt_rank = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    summary = ops.TRACE.summary()
+    summary = ops.TRACE.summary() if cuda else {}
+    order = None
+    if cuda:
+        names = [r[0] for r in ops.TRACE.records]
+        order = {"steps": args.steps, "warmup": args.warmup,
+                 "per_step": names[:len(names) // max(args.steps, 1)]}
     ops.TRACE = None
-    assert torch.isfinite(out).all() and (args.model == "train" or out.shape == shape)
+    assert torch.isfinite(out).all() and (model_kind == "train" or out.shape == shape)
 
+    per_rank = [dt_rank]
     if world > 1:
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    value = world * B * args.steps / dt
+        rt = torch.zeros(world, device=dev, dtype=torch.float64)
+        rt[rank] = dt_rank
+        dist.all_reduce(rt, op=dist.ReduceOp.SUM)
+        per_rank = [float(v) for v in rt.cpu()]
+    value = total * args.steps / dt
+    gathered_ok = None
+    if host is not None:
+        if world > 1:
+            dist.barrier()  # every rank's slice is in the shared buffer
+        gathered_ok = bool(torch.isfinite(host.full).all()) if rank == 0 else None
+        if not cuda and rank == 0:  # selftest: the gathered batch equals the unsplit result
+            full = (torch.from_numpy(synth.image(1000, (total, 3, size, size))),
+                    torch.from_numpy(synth.image(2000, (total, 3, size, size))))
+            gathered_ok = gathered_ok and torch.equal(host.full, model.test(*full))
 
     if rank == 0:
         rec = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32" if args.model != "wct"
-            else "fp32 conv / f64 WCT", "data": "synthetic U[0,1) images, synthetic He-uniform weights",
-            "config": {"workload": WORKLOADS[args.model], "per_gpu_batch": B,
-                       "global_batch": B * world, "image": f"{args.size}x{args.size}",
+            "scaling": scaling, "vs_baseline": None,
+            "dtype": "fp32 conv / f64 WCT" if model_kind == "wct" else "fp32",
+            "data": "synthetic U[0,1) images, synthetic He-uniform weights",
+            "config": {"workload": WORKLOADS[model_kind], "per_gpu_batch": B,
+                       "global_batch": total, "image": f"{size}x{size}",
+                       "baseline_config": args.config,
                        "parallelism": (f"data parallel over {world} GPU(s), one gradient "
-                                       "all-reduce per step") if args.model == "train" else
-                       f"per-image batch split over {world} GPU(s), no collectives"},
-            "roofline": roofline_from_trace(summary),
+                                       "all-reduce per step") if model_kind == "train" else
+                       f"per-image batch split over {world} GPU(s), no collectives",
+                       "host_gather": bool(host is not None)},
+            "per_rank_s": [round(v, 4) for v in per_rank],
         }
-        adain_summary = measure_adain_standalone(dev, B, 256, args.size * args.size)
-        rec["roofline_adain"] = adain_roofline(
-            summary if any(k.startswith("adain") for k in summary) else adain_summary)
-        rec["roofline_adain_stats"] = stats_roofline(adain_summary)
-        if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(args.model, args.size)
-        else:
-            rec["cpu_baseline"] = None
-        kernels = sorted(summary.items(), key=lambda kv: -kv[1]["ms"])[:12]
-        rec["kernel_ms_per_step"] = {k: round(v["ms"] / args.steps, 3) for k, v in kernels}
+        if host is not None:
+            rec["host_gather"] = {"pinned": host.pinned, "bytes_per_step": total * 3 * size * size * 4,
+                                  "all_finite": gathered_ok}
+        if cuda:
+            rec["roofline"] = roofline_from_trace(summary)
+            adain_summary = measure_adain_standalone(dev, min(B, 32), 256, min(size, 512) ** 2)
+            rec["roofline_adain"] = adain_roofline(
+                summary if any(k.startswith("adain") for k in summary) else adain_summary)
+            rec["roofline_adain_stats"] = stats_roofline(adain_summary)
+            if args.layer_order:
+                order["adain_name"] = next((k for k in adain_summary if k.startswith("adain")), None)
+                order["stats_name"] = next((k for k in adain_summary if k.startswith("stats")), None)
+                json.dump(order, open(args.layer_order, "w"), indent=1)
+            if world == 1 and not args.no_cpu_baseline:
+                rec["cpu_baseline"] = cpu_baseline(model_kind, min(size, 512))
+            else:
+                rec["cpu_baseline"] = None
+            kernels = sorted(summary.items(), key=lambda kv: -kv[1]["ms"])[:12]
+            rec["kernel_ms_per_step"] = {k: round(v["ms"] / args.steps, 3) for k, v in kernels}
         print(json.dumps(rec), flush=True)
+    if host is not None:
+        if world > 1:
+            dist.barrier()
+        host.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -143,15 +143,20 @@ int rpst_conv2d_skip_adain(const float* stylized, const float* content, const fl
 int64_t rpst_conv2d_grid_threads(int N, int Cin, int Hs, int Ws, int Cout, int ksize,
                                  int in_op);
 
-/* Algorithm rpst_conv2d uses for this layer — host-only: RPST_CONV_DIRECT (implicit GEMM:
- * every 1x1 layer and 3x3 layers with < 16 input channels), RPST_CONV_WINOGRAD4 (F(4x4,3x3)
- * in fp32: 3x3 layers with >= 16 input channels whose loader operator is NONE / ADAIN /
- * UPSAMPLE2) or RPST_CONV_WINOGRAD (F(2x2,3x3) in fp32: the other 3x3 layers with >= 16
- * input and >= 32 output channels). The environment variable
- * RPST_CONV_ALGO=direct|winograd|winograd4 overrides. */
+/* Algorithm rpst_conv2d uses for this layer — host-only: RPST_CONV_NARROW (VALU kernel for
+ * 3x3 layers with loader NONE and Cout <= 4, Cin <= 16 or Cout <= 16, Cin <= 4: the RP
+ * stacks' 3->16 / 16->3 convs; batches above 65535 images and the statistics entry point
+ * take the direct path instead), RPST_CONV_DIRECT (implicit GEMM: every 1x1 layer and the
+ * other 3x3 layers with < 16 input channels), RPST_CONV_WINOGRAD4 (F(4x4,3x3) in fp32: 3x3
+ * layers with >= 16 input channels whose loader operator is NONE / ADAIN / UPSAMPLE2) or
+ * RPST_CONV_WINOGRAD (F(2x2,3x3) in fp32: the other 3x3 layers with >= 16 input and >= 32
+ * output channels). The environment variable RPST_CONV_ALGO=direct|winograd|winograd4
+ * overrides ("direct" keeps the narrow kernel for narrow shapes; RPST_CONV_NARROW=0 turns
+ * it off). */
 #define RPST_CONV_DIRECT 0
 #define RPST_CONV_WINOGRAD 1
 #define RPST_CONV_WINOGRAD4 2
+#define RPST_CONV_NARROW 3
 int rpst_conv2d_algorithm(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op);
 
 /* Precise mode for the CALLING THREAD (host-only): while on, the default choice never picks

@@ -377,23 +377,28 @@ static int pad_cout(int Cout) {
 static int ck_of(int ksize) { return ksize == 3 ? ConvK<3>::CK : ConvK<1>::CK; }
 
 // ---- narrow 3x3 layers on the VALU ------------------------------------------------------
-// Cin * Cout <= 64 (the RP stacks' 3->16 input and 16->3 output convs, rp.py encoder /
-// decoder ends): an MFMA tile pads such a layer to 32 output channels (16->3: 10x the
-// work) or 8 input channels, so these run as plain FMAs instead. Block = 4 RPT rows x 64
+// Cout <= 4 with Cin <= 16, or Cout <= 16 with Cin <= 4 (narrow_shape; the RP stacks'
+// 3->16 input and 16->3 output convs, base.py:363-396 encoder / decoder ends): an MFMA tile
+// pads such a layer to 32 output channels (16->3: 10x the work) or 8 input channels, so
+// these run as plain FMAs instead (algorithm RPST_CONV_NARROW). Block = 4 RPT rows x 64
 // columns, 256 threads (column, RPT rows); per input channel the (4 RPT+2) x 66 patch is
 // staged in LDS with the padding resolved, weights [ci][tap][co] sit in LDS for the
-// whole block. Same epilogue as the direct kernel: bias, activation, residual.
+// whole block. Same epilogue as the direct kernel: bias, activation, residual. Images go
+// on grid.z: batches above 65535 images (or 65535 row tiles) take the MFMA direct path.
 constexpr int kNrTW = 64, kNrPW = kNrTW + 2;
+constexpr int kNrMaxCin = 16, kNrMaxCo = 16, kNrWl = 64 * 9;  // weight floats in LDS
 
 static bool narrow_shape(int Cin, int Cout) {
-  return (Cout <= 4 && Cin <= 16) || (Cout <= 16 && Cin <= 4);
+  return (Cout <= 4 && Cin <= kNrMaxCin) || (Cout <= kNrMaxCo && Cin <= 4);
 }
+// the largest Cin * CO an instantiation can meet must fit the LDS weight array
+static_assert(kNrMaxCin * 9 * 4 <= kNrWl && 4 * 9 * kNrMaxCo <= kNrWl, "narrow weights fit LDS");
 
 template <int CO, int RPT>  // RPT output rows per thread: block = 4 RPT rows x 64 columns
 __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
   constexpr int CK = ConvK<3>::CK, kNrTH = 4 * RPT, kNrPS = (kNrTH + 2) * kNrPW;
   __shared__ float patch[kNrPS];
-  __shared__ float wl[64 * 9];  // Cin * 9 * CO <= 576
+  __shared__ float wl[kNrWl];  // Cin * 9 * CO <= 576 (narrow_shape)
   const int x0 = blockIdx.x * kNrTW, y0 = blockIdx.y * kNrTH, n = blockIdx.z;
   const int tid = threadIdx.x, col = tid & 63, rg = tid >> 6;  // output rows RPT rg ..
   // direct-packed weights [ci / CK][tap][ci % CK][Cout_pad] (zero beyond Cout)
@@ -555,19 +560,19 @@ static thread_local int t_conv_precise = 0;
 static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
   if (ksize != 3) return RPST_CONV_DIRECT;
   const bool w4 = wino4_supports(in_op) && wino4_fits(1, Cin, Hs, Ws, in_op);
+  const bool nr = in_op == RPST_IN_NONE && narrow_shape(Cin, Cout) && narrow_enabled();
   const char* e = getenv("RPST_CONV_ALGO");
   if (e && *e) {
-    if (e[0] == 'd') return RPST_CONV_DIRECT;
+    if (e[0] == 'd') return nr ? RPST_CONV_NARROW : RPST_CONV_DIRECT;
     if (!strcmp(e, "winograd")) return RPST_CONV_WINOGRAD;
     if (!strcmp(e, "winograd4")) return w4 ? RPST_CONV_WINOGRAD4 : RPST_CONV_WINOGRAD;
   }
   // measured (profiles/r01_bench_conv_wino4.log): F(4x4) wins every layer with >= 16 input
-  // channels it supports, the 16-wide 32->16 / 16->3 decoder layers included; the
-  // 3-channel input layers (3->16, VGG 3->64) and the remaining 16-wide outputs run
-  // faster direct
+  // channels it supports, the 16-wide 32->16 decoder layer included; the narrow 3->16 /
+  // 16->3 layers run on the VALU kernel (0.51 / 0.30 ms vs 0.57 / 0.64 on MFMA tiles) and
+  // the other 3-channel input layers (VGG 3->64) faster direct
+  if (nr) return RPST_CONV_NARROW;
   if (Cin < 16) return RPST_CONV_DIRECT;
-  if (in_op == RPST_IN_NONE && narrow_shape(Cin, Cout) && narrow_enabled())
-    return RPST_CONV_DIRECT;  // 16->3: conv3x3_narrow_kernel
   if (w4 && !t_conv_precise) return RPST_CONV_WINOGRAD4;
   if (w4) return RPST_CONV_WINOGRAD;  // precise mode, same shapes as F(4x4)
   return Cout >= 32 ? RPST_CONV_WINOGRAD : RPST_CONV_DIRECT;
@@ -593,11 +598,36 @@ struct ConvGeom {
   int nth, stat_P, stat_nt, stat_wn, stat_tw, tiles_x;
 };
 
-static ConvGeom conv_geom(int N, int Cin, int Hs, int Ws, int Cout, int ksize, int in_op) {
+// rows per thread of the narrow kernel: 4 for Cout <= 4 (16->3: 0.307 vs 0.348 ms;
+// RPST_CONV_NARROW_RPT=2 overrides), 2 for Cout <= 16 (3->16 at 4 rows spills to scratch:
+// 1.47 vs 0.51 ms)
+static int narrow_rpt(int Cout) {
+  const char* e = getenv("RPST_CONV_NARROW_RPT");
+  return Cout <= 4 && !(e && *e && atoi(e) == 2) ? 4 : 2;
+}
+
+// the narrow kernel puts the images on grid.z and the row tiles on grid.y (<= 65535 each);
+// it has no statistics epilogue
+static bool narrow_launchable(int N, int H, int Cout, bool stats) {
+  return !stats && N <= 65535 && (H + 4 * narrow_rpt(Cout) - 1) / (4 * narrow_rpt(Cout)) <= 65535;
+}
+
+static ConvGeom conv_geom(int N, int Cin, int Hs, int Ws, int Cout, int ksize, int in_op,
+                          bool stats = false) {
   int H, W;
   logical_hw(Hs, Ws, in_op, &H, &W);
   ConvGeom g{};
   g.algo = conv_algo(Cout, Cin, Hs, Ws, ksize, in_op);
+  if (g.algo == RPST_CONV_NARROW && !narrow_launchable(N, H, Cout, stats))
+    g.algo = RPST_CONV_DIRECT;
+  if (g.algo == RPST_CONV_NARROW) {
+    const int rows = 4 * narrow_rpt(Cout);
+    g.tiles_x = (W + kNrTW - 1) / kNrTW;
+    g.blocks = (int64_t)g.tiles_x * ((H + rows - 1) / rows) * N;
+    g.nth = 256;
+    g.stat_tw = kNrTW;
+    return g;
+  }
   g.tiles_x = (W + kTW - 1) / kTW;
   g.stat_tw = kTW;
   if (g.algo == RPST_CONV_WINOGRAD4) {
@@ -754,7 +784,13 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   // buffer offset
   RPST_REQUIRE(((int64_t)Cin + 16) * Hs * Ws * 4 < (1LL << 31),
                "conv2d: one image's input exceeds 2 GiB");
-  const int algo = conv_algo(Cout, Cin, Hs, Ws, ksize, in_op);
+  int algo = conv_algo(Cout, Cin, Hs, Ws, ksize, in_op);
+  if (algo == RPST_CONV_NARROW && !narrow_launchable(N, a.H, Cout, stat_part != nullptr))
+    algo = RPST_CONV_DIRECT;
+  // the residual epilogue (SANet out_conv, sanet.py:97-98) exists on the direct and narrow
+  // kernels only
+  if (residual && (algo == RPST_CONV_WINOGRAD || algo == RPST_CONV_WINOGRAD4))
+    algo = RPST_CONV_DIRECT;
   if (algo == RPST_CONV_WINOGRAD4) {
     a.wpk = packed_weight + direct_packed_floats(Cout, Cin, ksize) + wino_packed_floats(Cout, Cin);
     a.stat_part = stat_part;
@@ -792,14 +828,10 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * N * a.co_tiles;
   RPST_REQUIRE(blocks <= 0x7fffffffLL, "conv2d: grid too large");
   if (args_out) *args_out = a;
-  if (ksize == 3 && in_op == RPST_IN_NONE && !stat_part && narrow_shape(Cin, Cout) &&
-      narrow_enabled()) {
-    // rows per thread: 4 for Cout <= 4 (16->3: 0.307 vs 0.348 ms; RPST_CONV_NARROW_RPT=2
-    // overrides), 2 for Cout <= 16 (3->16 at 4 rows spills to scratch: 1.47 vs 0.51 ms)
-    const char* e = getenv("RPST_CONV_NARROW_RPT");
-    const int rpt = Cout <= 4 && !(e && *e && atoi(e) == 2) ? 4 : 2;
+  if (algo == RPST_CONV_NARROW) {
+    const int rpt = narrow_rpt(Cout);
+    RPST_REQUIRE(Cin * 9 * (Cout <= 4 ? 4 : 16) <= kNrWl, "conv2d: narrow weights exceed LDS");
     dim3 grid((unsigned)((a.W + kNrTW - 1) / kNrTW), (unsigned)((a.H + 4 * rpt - 1) / (4 * rpt)), N);
-    RPST_REQUIRE(N <= 65535 && grid.y <= 65535, "conv2d: grid too large");
     if (Cout <= 4) {
       if (rpt == 4) conv3x3_narrow_kernel<4, 4><<<grid, 256, 0, st>>>(a);
       else conv3x3_narrow_kernel<4, 2><<<grid, 256, 0, st>>>(a);
@@ -881,7 +913,7 @@ extern "C" int rpst_conv2d_skip_adain(const float* stylized, const float* conten
 extern "C" size_t rpst_conv2d_stats_workspace_size(int N, int Cin, int Hs, int Ws, int Cout,
                                                    int ksize, int in_op) {
   if (N <= 0 || Cin <= 0 || Hs <= 0 || Ws <= 0 || Cout <= 0 || (ksize != 1 && ksize != 3)) return 0;
-  const ConvGeom g = conv_geom(N, Cin, Hs, Ws, Cout, ksize, in_op);
+  const ConvGeom g = conv_geom(N, Cin, Hs, Ws, Cout, ksize, in_op, true);
   const size_t stats = ((size_t)N * Cout * g.stat_P * sizeof(float2) + 255) / 256 * 256;
   return stats + fold_bytes(N, Cin, Hs, Ws, Cout, ksize, in_op);
 }
@@ -901,7 +933,7 @@ extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
   hipStream_t st = as_stream(stream);
   ConvArgs a{};
   int P = 0;
-  const ConvGeom g = conv_geom(N, Cin, Hs, Ws, Cout, ksize, in_op);
+  const ConvGeom g = conv_geom(N, Cin, Hs, Ws, Cout, ksize, in_op, true);
   const int planes = N * Cout;
   if (g.algo == RPST_CONV_DIRECT && g.stat_nt < 4) {  // tile without the fused statistics epilogue
     if (int e = conv_common(input, aux, nullptr, packed_weight, bias, residual, out, N, Cin, Hs,

@@ -170,13 +170,14 @@ def conv_out_hw(h: int, w: int, in_op: int) -> Tuple[int, int]:
     return h, w
 
 
-_ALGO_TAG = {0: "conv", 1: "wino", 2: "wino4"}
+_ALGO_TAG = {0: "conv", 1: "wino", 2: "wino4", 3: "narrow"}
 
 
 def _conv_name(ksize, cin, cout, hs, ws, n, in_op):
-    """Trace key of a conv launch: 'wino3x3' / 'wino43x3' when the library runs it as
-    Winograd F(2x2,3x3) / F(4x4,3x3) (the recorded FLOPs stay the direct-convolution
-    count). hs, ws: the SOURCE size; the key carries the output size."""
+    """Trace key of a conv launch: 'wino3x3' / 'wino43x3' / 'narrow3x3' when the library
+    runs it as Winograd F(2x2,3x3) / F(4x4,3x3) / the VALU narrow kernel (the recorded
+    FLOPs stay the direct-convolution count). hs, ws: the SOURCE size; the key carries the
+    output size."""
     algo = "conv"
     if TRACE is not None:
         algo = _ALGO_TAG[_lib.load().rpst_conv2d_algorithm(cout, cin, hs, ws, ksize, in_op)]

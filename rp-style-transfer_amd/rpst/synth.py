@@ -28,11 +28,11 @@ def _key_seed(seed: int, key: str) -> np.uint64:
     return np.uint64(int.from_bytes(h[:8], "little"))
 
 
-def uniform01(seed: int, key: str, n: int) -> np.ndarray:
-    """n float64 values in [0,1) from splitmix64 over counter 1..n."""
+def uniform01(seed: int, key: str, n: int, offset: int = 0) -> np.ndarray:
+    """n float64 values in [0,1) from splitmix64 over counter offset+1..offset+n."""
     base = _key_seed(seed, key)
     with np.errstate(over="ignore"):
-        z = base + (np.arange(1, n + 1, dtype=np.uint64) * _GOLDEN)
+        z = base + (np.arange(offset + 1, offset + n + 1, dtype=np.uint64) * _GOLDEN)
         z = (z ^ (z >> np.uint64(30))) * _M1
         z = (z ^ (z >> np.uint64(27))) * _M2
         z = z ^ (z >> np.uint64(31))
@@ -69,6 +69,14 @@ def synth_module_(module, seed: int) -> None:
 def image(seed: int, shape: Tuple[int, ...]) -> np.ndarray:
     """Synthetic image batch in [0,1), float32, NCHW."""
     return uniform01(seed, "image", int(np.prod(shape))).astype(np.float32).reshape(shape)
+
+
+def image_range(seed: int, shape: Tuple[int, ...], start: int, end: int) -> np.ndarray:
+    """Images [start, end) of image(seed, shape) without generating the others (the
+    counter of element i is i + 1, so a batch slice is a counter range)."""
+    per = int(np.prod(shape[1:]))
+    return uniform01(seed, "image", (end - start) * per, offset=start * per).astype(
+        np.float32).reshape((end - start,) + tuple(shape[1:]))
 
 
 def checksum(arrs: Dict[str, np.ndarray]) -> Tuple[float, float]:

@@ -86,19 +86,30 @@ def test_cpu_tensors_raise_no_fallback():
 
 
 def test_conv_algorithm_choice_is_host_only(monkeypatch):
-    """rpst_conv2d_algorithm: direct below 16 input channels, else F(4x4) for the NONE /
-    ADAIN / UPSAMPLE2 loaders, F(2x2) for the other 3x3 layers with Cout >= 32, direct
-    otherwise;
-    precise mode (training) and RPST_CONV_ALGO override."""
+    """rpst_conv2d_algorithm: the VALU narrow kernel for the 3->16 / 16->3 shapes, direct
+    for the other layers below 16 input channels, else F(4x4) for the NONE / ADAIN /
+    UPSAMPLE2 loaders, F(2x2) for the other 3x3 layers with Cout >= 32, direct otherwise;
+    precise mode (training), RPST_CONV_ALGO and RPST_CONV_NARROW override."""
     monkeypatch.delenv("RPST_CONV_ALGO", raising=False)
+    monkeypatch.delenv("RPST_CONV_NARROW", raising=False)
     lib = _lib.load()
-    D, W2, W4 = 0, 1, 2
+    D, W2, W4, NR = 0, 1, 2, 3
     assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == W4
     assert lib.rpst_conv2d_algorithm(128, 256, 512, 512, 3, 4) == W4   # AdaIN-in-loader
     assert lib.rpst_conv2d_algorithm(256, 256, 32, 32, 3, 2) == W4     # upsample
     assert lib.rpst_conv2d_algorithm(128, 64, 64, 64, 3, 1) == W2      # max-pool loader
     assert lib.rpst_conv2d_algorithm(64, 3, 512, 512, 3, 0) == D        # 3-channel input
+    assert lib.rpst_conv2d_algorithm(16, 3, 512, 512, 3, 0) == NR      # RP 3->16
+    assert lib.rpst_conv2d_algorithm(3, 16, 512, 512, 3, 0) == NR      # RP 16->3
+    assert lib.rpst_conv2d_algorithm(8, 8, 512, 512, 3, 0) == D        # not narrow_shape
+    assert lib.rpst_conv2d_algorithm(3, 16, 512, 512, 3, 1) == D       # loader op: MFMA path
+    # narrow grid threads: 64 columns x 16 rows (Cout <= 4: 4 rows per thread) per block
+    assert lib.rpst_conv2d_grid_threads(2, 16, 512, 512, 3, 3, 0) == 2 * 8 * 32 * 256
+    assert lib.rpst_conv2d_grid_threads(2, 3, 512, 512, 16, 3, 0) == 2 * 8 * 64 * 256
+    monkeypatch.setenv("RPST_CONV_NARROW", "0")
+    assert lib.rpst_conv2d_algorithm(3, 16, 512, 512, 3, 0) == W4
     assert lib.rpst_conv2d_algorithm(16, 3, 512, 512, 3, 0) == D
+    monkeypatch.delenv("RPST_CONV_NARROW")
     assert lib.rpst_conv2d_algorithm(16, 32, 512, 512, 3, 0) == W4
     assert lib.rpst_conv2d_algorithm(512, 512, 64, 64, 1, 0) == D
     old = lib.rpst_conv2d_set_precise(1)
@@ -109,3 +120,4 @@ def test_conv_algorithm_choice_is_host_only(monkeypatch):
     assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == W4
     monkeypatch.setenv("RPST_CONV_ALGO", "direct")
     assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == D
+    assert lib.rpst_conv2d_algorithm(3, 16, 512, 512, 3, 0) == NR

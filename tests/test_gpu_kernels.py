@@ -182,6 +182,52 @@ def test_conv2d_residual(cuda):
     assert rel_l2(out, ref) < 1e-5
 
 
+def test_conv2d_residual_3x3_every_algorithm(cuda, conv_algo):
+    """A 3x3 conv with a residual runs on a kernel with the residual epilogue whatever
+    algorithm the layer would otherwise take (the Winograd kernels have none)."""
+    from rpst import ops
+    x = gen(24, (2, 32, 20, 72))
+    w = gen(25, (64, 32, 3, 3), 0.05)
+    b = gen(26, (64,), 0.05)
+    r = gen(27, (2, 64, 20, 72))
+    ref = _conv_ref(x.double(), w.double(), b.double(), 1, 0, True, res=r.double())
+    out = ops.conv2d(x.to(cuda), ops.pack_conv_weight(w.to(cuda)), b.to(cuda), 64, 3, pad=1,
+                     relu=True, residual=r.to(cuda))
+    assert rel_l2(out, ref) < 1e-5
+
+
+NARROW_CASES = [  # (N, Cin, Hs, Ws, Cout, pad, relu, residual)
+    (2, 16, 17, 70, 3, 1, False, False),   # RP 16->3 shape, reflect
+    (1, 16, 33, 64, 3, 0, True, True),     # 16->3 with the residual epilogue
+    (2, 3, 21, 130, 16, 0, True, True),    # 3->16 with the residual epilogue
+    (1, 4, 9, 66, 4, 1, True, False),      # Cout <= 4 instantiation, Cin 4
+]
+
+
+@pytest.mark.parametrize("rpt", ["2", "4"])
+@pytest.mark.parametrize("narrow", ["0", "1"])
+@pytest.mark.parametrize("case", NARROW_CASES)
+def test_conv2d_narrow_variants(cuda, case, rpt, narrow, monkeypatch):
+    """conv3x3_narrow_kernel<4, 4> / <4, 2> (RPST_CONV_NARROW_RPT) and <16, 2>, with and
+    without a residual, and the RPST_CONV_NARROW=0 A/B switch (MFMA paths)."""
+    from rpst import _lib, ops
+    monkeypatch.delenv("RPST_CONV_ALGO", raising=False)
+    monkeypatch.setenv("RPST_CONV_NARROW_RPT", rpt)
+    monkeypatch.setenv("RPST_CONV_NARROW", narrow)
+    n, cin, hs, ws, cout, pad, relu, with_res = case
+    algo = _lib.load().rpst_conv2d_algorithm(cout, cin, hs, ws, 3, 0)
+    assert (algo == 3) == (narrow == "1")
+    x = gen(50, (n, cin, hs, ws), 1.0, 0.2)
+    w = gen(51, (cout, cin, 3, 3), (2.0 / (cin * 9)) ** 0.5)
+    b = gen(52, (cout,), 0.05)
+    r = gen(53, (n, cout, hs, ws)) if with_res else None
+    ref = _conv_ref(x.double(), w.double(), b.double(), pad, 0, relu,
+                    res=None if r is None else r.double())
+    out = ops.conv2d(x.to(cuda), ops.pack_conv_weight(w.to(cuda)), b.to(cuda), cout, 3, pad=pad,
+                     relu=relu, residual=None if r is None else r.to(cuda))
+    assert rel_l2(out, ref) < 1e-5, rel_l2(out, ref)
+
+
 def test_conv2d_deterministic(cuda, conv_algo):
     from rpst import ops
     x = gen(30, (2, 128, 32, 64)).to(cuda)
