@@ -279,26 +279,54 @@ int rpst_sq_diff_sum(const float* a, const float* b, int64_t n, double scale, fl
 
 /* ---- a7: matrix_sqrt / matrix_inv_sqrt  network/wct_rp.py:7-40 ----------------------
  * out[b] = (A[b] + 1e-4 I)^(+1/2) (inverse = 0) or ^(-1/2) (inverse = 1) for symmetric PSD
- * fp64 n x n matrices, batch of `batch`. Coupled Newton-Schulz (fixed 40 steps); equal to
- * the reference's SVD form because its truncation (< 1e-5) cannot trigger after +1e-4.
+ * fp64 n x n matrices, batch of `batch`. Coupled Newton-Schulz, per matrix until
+ * ||I - Z Y||_F < 1e-10 (at most 64 steps); equal to the reference's SVD form because its
+ * truncation (< 1e-5) cannot trigger after +1e-4 on a PSD matrix. residual (batch doubles,
+ * may be NULL) receives each matrix's last residual: a value >= 1e-10 means the input was
+ * not symmetric PSD (the reference's SVD would return V |S|^p V^T there; callers reject it).
  * Workspace: rpst_matrix_power_workspace_size(n, batch). */
 size_t rpst_matrix_power_workspace_size(int n, int batch);
 int rpst_matrix_power_psd_f64(const double* A, double* out, int n, int batch, int inverse,
-                              void* workspace, size_t workspace_bytes, rpst_stream_t stream);
+                              double* residual, void* workspace, size_t workspace_bytes,
+                              rpst_stream_t stream);
 
 /* ---- a8: WCTRPNet.whiten_and_color(cF, sF, 'closed-form')  network/wct_rp.py:82-114 ---
  * cF, sF, out: (C, HW) fp64. out = T (cF - mu_c) + mu_s with the closed-form T.
+ * residual (2 doubles or NULL): Newton-Schulz residuals of Cc + 1e-4 I and of Mid's argument.
  * Workspace: rpst_wct_workspace_size(1, C, HW). */
 size_t rpst_wct_workspace_size(int n, int C, int64_t HW);
 int rpst_whiten_and_color_f64(const double* cF, const double* sF, double* out, int C,
-                              int64_t HW, void* workspace, size_t workspace_bytes,
-                              rpst_stream_t stream);
+                              int64_t HW, double* residual, void* workspace,
+                              size_t workspace_bytes, rpst_stream_t stream);
 
 /* ---- a9: WCTRPNet.fuse(content_feats, style_feats)  network/wct_rp.py:157-166 --------
  * content, style, out: (n, C, HW) fp32. Per image: widen to fp64, whiten_and_color, round
- * to fp32 — all n images in one set of launches. Workspace: rpst_wct_workspace_size(n,C,HW). */
+ * to fp32 — all n images in one set of launches. residual: 2n doubles or NULL (as a8, per
+ * image). Workspace: rpst_wct_workspace_size(n, C, HW). */
 int rpst_wct_fuse(const float* content, const float* style, float* out, int n, int C,
-                  int64_t HW, void* workspace, size_t workspace_bytes, rpst_stream_t stream);
+                  int64_t HW, double* residual, void* workspace, size_t workspace_bytes,
+                  rpst_stream_t stream);
+
+/* ---- a9 split for the fused WCTRPNet.test: the closed-form matrices without the product
+ * T: (n, C, C) fp64 and offset c = mu_s - T mu_c: (n, C) fp64, so that the fused feature
+ * T (cF - mu_c) + mu_s = T cF + c (wct_rp.py:109-113) is formed inside the decoder's first
+ * conv (rpst_conv2d_mix) instead of being written. means: optional fp32 row means (2n x C,
+ * content rows then style rows, e.g. the encoder's statistics epilogue); NULL computes them.
+ * Workspace: rpst_wct_workspace_size(n, C, HW). */
+int rpst_wct_params(const float* content, const float* style, const float* means, double* T,
+                    double* offset, int n, int C, int64_t HW, double* residual, void* workspace,
+                    size_t workspace_bytes, rpst_stream_t stream);
+
+/* out = act(conv(pad(T_n x + c_n)) + bias) per image n: the WCT colour transform fused into
+ * the consumer conv. F(4x4) layers fold T_n into per-image weights W T_n (fp64, rounded
+ * once) and c_n into per-(n, co) border-class biases; other layers materialise T x + c.
+ * x: (N, Cin, H, W) fp32; T: (N, Cin, Cin) fp64; offset: (N, Cin) fp64.
+ * Workspace: rpst_conv2d_mix_workspace_size(N, Cin, H, W, Cout, ksize). */
+size_t rpst_conv2d_mix_workspace_size(int N, int Cin, int H, int W, int Cout, int ksize);
+int rpst_conv2d_mix(const float* input, const double* T, const double* offset,
+                    const float* packed_weight, const float* bias, float* out, int N, int Cin,
+                    int H, int W, int Cout, int ksize, int pad_mode, int relu, void* workspace,
+                    size_t workspace_bytes, rpst_stream_t stream);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -62,6 +62,13 @@ __device__ __forceinline__ int reflect1(int i, int n) {
   return i < 0 ? 0 : (i >= n ? n - 1 : i);
 }
 
+// ---- WCT colour transform (rpst_wct.hip), used by rpst_conv2d_mix's fallback ----------
+// z[b] = T[b] x[b] + c[b] for fp32 x (n, C, HW), fp64 T (n, C, C) and c (n, C); scratch:
+// wct_apply_scratch_floats(n, C) floats
+size_t wct_apply_scratch_floats(int n, int C);
+int wct_apply_f32(const double* T, const double* c, const float* x, float* z, int n, int C,
+                  int64_t HW, float* scratch, hipStream_t st);
+
 }  // namespace rpst
 
 #define RPST_REQUIRE(cond, ...)          \

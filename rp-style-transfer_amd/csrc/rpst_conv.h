@@ -244,5 +244,9 @@ int wino4_launch(ConvArgs& a, int in_op, hipStream_t st);
 size_t wino4_fold_floats(int N, int Cin, int Cout);
 int wino4_fold(ConvArgs& a, const float* direct_packed, int direct_cout_pad, float* ws,
                hipStream_t st);
+size_t wino4_mix_floats(int N, int Cin, int Cout);
+int wino4_mix(ConvArgs& a, const double* T, const double* cvec, const float* direct_packed,
+              int direct_cout_pad, float* ws, hipStream_t st);
+
 
 }  // namespace rpst

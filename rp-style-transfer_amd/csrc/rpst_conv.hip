@@ -899,6 +899,63 @@ extern "C" int rpst_conv2d_ws(const float* input, const float* aux, const float*
                      as_stream(stream), need ? static_cast<float*>(workspace) : nullptr);
 }
 
+// conv(pad(T_n x + c_n)): F(4x4) layers fold T_n / c_n into per-image weights and border
+// biases (wino4_mix); other layers materialise z = T x + c (fp32 MFMA GEMM) and convolve it
+static bool mix_folds(int Cin, int H, int W, int Cout, int ksize) {
+  return ksize == 3 && H >= 2 && W >= 2 &&
+         conv_algo(Cout, Cin, H, W, ksize, RPST_IN_NONE) == RPST_CONV_WINOGRAD4;
+}
+
+extern "C" size_t rpst_conv2d_mix_workspace_size(int N, int Cin, int H, int W, int Cout,
+                                                 int ksize) {
+  if (N <= 0 || Cin <= 0 || H <= 0 || W <= 0 || Cout <= 0 || (ksize != 1 && ksize != 3)) return 0;
+  if (mix_folds(Cin, H, W, Cout, ksize)) return (wino4_mix_floats(N, Cin, Cout) + 64) * sizeof(float);
+  return ((size_t)N * Cin * H * W + wct_apply_scratch_floats(N, Cin) + 64) * sizeof(float);
+}
+
+extern "C" int rpst_conv2d_mix(const float* input, const double* T, const double* offset,
+                               const float* packed_weight, const float* bias, float* out, int N,
+                               int Cin, int H, int W, int Cout, int ksize, int pad_mode,
+                               int relu, void* workspace, size_t workspace_bytes,
+                               rpst_stream_t stream) {
+  RPST_REQUIRE(input && T && offset && packed_weight && out, "conv2d_mix: null pointer");
+  RPST_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && H > 0 && W > 0, "conv2d_mix: bad shape");
+  const size_t need = rpst_conv2d_mix_workspace_size(N, Cin, H, W, Cout, ksize);
+  if (!workspace || workspace_bytes < need) {
+    set_error("conv2d_mix: workspace %zu < %zu bytes", workspace_bytes, need);
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  float* ws = static_cast<float*>(workspace);
+  if (!mix_folds(Cin, H, W, Cout, ksize)) {
+    float* z = ws;
+    if (int e = wct_apply_f32(T, offset, input, z, N, Cin, (int64_t)H * W,
+                              z + (size_t)N * Cin * H * W, st))
+      return e;
+    return conv_common(z, nullptr, nullptr, packed_weight, bias, nullptr, out, N, Cin, H, W, Cout,
+                       ksize, pad_mode, RPST_IN_NONE, relu, nullptr, nullptr, nullptr, st);
+  }
+  // the F(4x4) launch of conv_common with the folded weights: set up the arguments the way
+  // conv_common does for a NONE loader, then fold and launch
+  RPST_REQUIRE(pad_mode == RPST_PAD_ZERO || pad_mode == RPST_PAD_REFLECT, "conv2d_mix: bad pad");
+  RPST_REQUIRE(relu >= RPST_ACT_NONE && relu <= RPST_ACT_LRELU, "conv2d_mix: bad activation");
+  RPST_REQUIRE(((int64_t)Cin + 16) * H * W * 4 < (1LL << 31), "conv2d_mix: image too large");
+  ConvArgs a{};
+  a.in = input;
+  a.wpk = packed_weight + direct_packed_floats(Cout, Cin, ksize) + wino_packed_floats(Cout, Cin);
+  a.bias = bias;
+  a.out = out;
+  a.N = N;
+  a.Cin = Cin;
+  a.Hs = a.H = H;
+  a.Ws = a.W = W;
+  a.Cout = Cout;
+  a.pad = pad_mode;
+  a.relu = relu;
+  if (int e = wino4_mix(a, T, offset, packed_weight, pad_cout(Cout), ws, st)) return e;
+  return wino4_launch(a, RPST_IN_NONE, st);
+}
+
 extern "C" int rpst_conv2d_skip_adain(const float* stylized, const float* content,
                                       const float* params, const float* packed_weight,
                                       const float* bias, float* out, int N, int Cin, int H, int W,

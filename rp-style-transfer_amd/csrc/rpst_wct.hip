@@ -14,6 +14,13 @@
 //   Z = (A/s)^(-1/2). The reference's SVD truncation (singular values < 1e-5) can never
 //   trigger because every input carries +1e-4 I on a PSD matrix, and V diag(e^p) V^T of
 //   an SVD equals the principal power, so the two agree to fp64 rounding (~1e-13).
+//   Convergence is checked per matrix: after each T_k a residual kernel computes
+//   r_k = ||I - Z_k Y_k||_F = 2 ||T_k - I||_F; once r_k < kNSTol the matrix takes that last
+//   update and every later iteration skips it (its blocks exit at once), so a batch costs
+//   the iterations of its slowest matrix (10-25 on encoder covariances) up to kNSMaxIters.
+//   The final residual of every matrix is written out; a matrix that has not converged
+//   (an input that is not symmetric positive semi-definite after the +1e-4 I shift, or
+//   beyond kNSMaxIters' reach) is reported by the caller instead of being returned silently.
 //
 // GEMM: v_mfma_f64_16x16x4_f64 (A[l&15][k=l>>4], B[k=l>>4][l&15], D col=l&15,
 // row=(l>>4)+4r). Tiles BT x BT (64 or 128) x 16, 256 threads = 2x2 waves, operands
@@ -48,6 +55,9 @@ struct G64Args {
   const void* B2;
   void* C2;
   int dual;
+  // Newton-Schulz early exit: batch entry b is skipped when state[b] >= skip_at
+  const int* state;
+  int skip_at;
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -132,6 +142,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
     gB = g.B2;
     gC = g.C2;
   }
+  if (g.state && g.state[b] >= g.skip_at) return;  // converged matrix (block-uniform)
   const int m0 = ti * BT, n0 = tj * BT;
   // split-K ranges are whole BK tiles
   const int kper = ((g.K + g.ksplit - 1) / g.ksplit + BK - 1) / BK * BK;
@@ -392,6 +403,51 @@ __global__ __launch_bounds__(256, 2) void wct_transform_f32_kernel(
     }
 }
 
+// out = Tf^T-staged product: out[b] = T[b] (X[b] - muc[b]) + mus[b] for fp32 features
+static int wct_transform_f32(const float* Tf, const float* X, const float* muc, const float* mus,
+                             float* out, int n, int C, int64_t HW, hipStream_t st) {
+  dim3 grid((unsigned)((HW + 127) / 128), (C + 127) / 128, n);
+  const bool vec = (HW % 4 == 0) && (C % 4 == 0) && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+  if (vec)
+    wct_transform_f32_kernel<true><<<grid, 256, 0, st>>>(Tf, X, muc, mus, out, C, (int)HW);
+  else
+    wct_transform_f32_kernel<false><<<grid, 256, 0, st>>>(Tf, X, muc, mus, out, C, (int)HW);
+  return launch_status("wct_transform_f32_kernel");
+}
+
+// Tf[b][k][m] = T[b][m][k] (fp32), muc = 0, mus = c (fp32): the operands of wct_transform_f32
+// for z = T x + c
+__global__ void wct_apply_prep_kernel(const double* __restrict__ T, const double* __restrict__ c,
+                                      float* __restrict__ Tf, float* __restrict__ muc,
+                                      float* __restrict__ mus, int64_t nT, int64_t nc, int C) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < nT) {
+    const int64_t cc = (int64_t)C * C, b = i / cc, r = i - b * cc;
+    const int m = (int)(r / C), k = (int)(r - (int64_t)m * C);
+    Tf[b * cc + (int64_t)k * C + m] = (float)T[i];
+  }
+  if (i < nc) {
+    muc[i] = 0.f;
+    mus[i] = (float)c[i];
+  }
+}
+
+size_t wct_apply_scratch_floats(int n, int C) {
+  return (size_t)n * C * C + 2 * (size_t)n * C + 64;
+}
+
+int wct_apply_f32(const double* T, const double* c, const float* x, float* z, int n, int C,
+                  int64_t HW, float* scratch, hipStream_t st) {
+  float* Tf = scratch;
+  float* muc = Tf + (size_t)n * C * C;
+  float* mus = muc + (size_t)n * C;
+  const int64_t nT = (int64_t)n * C * C, nc = (int64_t)n * C;
+  wct_apply_prep_kernel<<<(unsigned)((std::max(nT, nc) + 255) / 256), 256, 0, st>>>(
+      T, c, Tf, muc, mus, nT, nc, C);
+  if (int e = launch_status("wct_apply_prep_kernel")) return e;
+  return wct_transform_f32(Tf, x, muc, mus, z, n, C, HW, st);
+}
+
 // Row means in fp64 of `rows` rows of length L (one workgroup per row).
 template <typename T>
 __global__ __launch_bounds__(256) void rowmean_kernel(const T* __restrict__ x0,
@@ -476,15 +532,6 @@ __global__ __launch_bounds__(256) void ns_init_kernel(const double* __restrict__
   }
 }
 
-// out_b = in_b * s_b^p
-__global__ void scale_pow_kernel(const double* __restrict__ in, double* __restrict__ out,
-                                 const double* __restrict__ svec, double p, int64_t per,
-                                 int batch) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= per * batch) return;
-  out[i] = in[i] * pow(svec[i / per], p);
-}
-
 // ---- host-side pipeline ------------------------------------------------------------
 template <int BT, int SRCA, int SRCB, int BLAY, int OUT>
 static void gemm64(const G64Args& g, dim3 grid, hipStream_t st) {
@@ -509,13 +556,17 @@ static int env_int(const char* name, int dflt);
 static void small_gemm(const double* A, const double* B, double* C, int n, int batch,
                        double alpha, double beta_diag, const double* avec, hipStream_t st,
                        const double* A2 = nullptr, const double* B2 = nullptr,
-                       double* C2 = nullptr) {
+                       double* C2 = nullptr, const int* state = nullptr, int skip_at = 0) {
   if (A2 && 2 * batch > 65535) {  // grid.z limit: two launches
-    small_gemm(A, B, C, n, batch, alpha, beta_diag, avec, st);
-    small_gemm(A2, B2, C2, n, batch, alpha, beta_diag, avec, st);
+    small_gemm(A, B, C, n, batch, alpha, beta_diag, avec, st, nullptr, nullptr, nullptr, state,
+               skip_at);
+    small_gemm(A2, B2, C2, n, batch, alpha, beta_diag, avec, st, nullptr, nullptr, nullptr,
+               state, skip_at);
     return;
   }
   G64Args g{};
+  g.state = state;
+  g.skip_at = skip_at;
   g.A = A;
   g.B = B;
   g.C = C;
@@ -545,11 +596,57 @@ static void small_gemm(const double* A, const double* B, double* C, int n, int b
   }
 }
 
-constexpr int kNSIters = 40;
+constexpr int kNSMaxIters = 64;
+constexpr double kNSTol = 1e-10;  // on ||I - Z Y||_F (||I||_F = sqrt(n)); quadratic from here
+
+// Newton-Schulz state per matrix: 0 running, 1 converged (this iteration's update still
+// applies), 2 done (skipped); last[b] = the last iteration whose update ran.
+// r_k = 2 ||T_k - I||_F of iteration k (one workgroup per matrix, fixed-order reduction).
+__global__ __launch_bounds__(256) void ns_residual_kernel(const double* __restrict__ T,
+                                                          int* __restrict__ state,
+                                                          int* __restrict__ last,
+                                                          double* __restrict__ res, int n,
+                                                          int it) {
+  const int b = blockIdx.x;
+  const int st = state[b];
+  if (st >= 1) {  // the update of iteration it - 1 was this matrix's last
+    if (threadIdx.x == 0 && st == 1) state[b] = 2;
+    return;
+  }
+  const double* t = T + (int64_t)b * n * n;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n * n; i += 256) {
+    const double v = t[i] - ((i / n) == (i % n) ? 1.0 : 0.0);
+    s += v * v;
+  }
+  s = wave_sum(s);
+  __shared__ double red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double r = 2.0 * sqrt((red[0] + red[1]) + (red[2] + red[3]));
+    res[b] = r;
+    last[b] = it;
+    if (r < kNSTol) state[b] = 1;
+  }
+}
+
+// out_b = buf[(last_b + 1) & 1]_b * s_b^p: the matrix's newest iterate (the ping-pong
+// buffers swap every iteration on the host, a converged matrix stops being updated)
+__global__ void ns_final_kernel(const double* __restrict__ buf0, const double* __restrict__ buf1,
+                                double* __restrict__ out, const double* __restrict__ svec,
+                                const int* __restrict__ last, double p, int64_t per, int batch) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= per * batch) return;
+  const int64_t b = i / per;
+  const double* src = ((last[b] + 1) & 1) ? buf1 : buf0;
+  out[i] = src[i] * pow(svec[b], p);
+}
 
 // out = (A + add I)^p for p = +-1/2 (both if both outputs are given), batched n x n.
-static void ns_power(const double* A, double add, double* sqrt_out, double* isqrt_out, int n,
-                     int batch, double* work, hipStream_t st) {
+// work: ns_work_doubles(n, batch); res: per-matrix final residual (may be null).
+static int ns_power(const double* A, double add, double* sqrt_out, double* isqrt_out, int n,
+                    int batch, double* work, hipStream_t st, double* res_out = nullptr) {
   const int64_t nn = (int64_t)n * n * batch;
   double* Y = work;
   double* Z = Y + nn;
@@ -557,10 +654,18 @@ static void ns_power(const double* A, double add, double* sqrt_out, double* isqr
   double* Y2 = T + nn;
   double* Z2 = Y2 + nn;
   double* svec = Z2 + nn;
+  double* res = svec + batch;
+  int* state = reinterpret_cast<int*>(res + batch);
+  int* last = state + batch;
+  double* const buf0[2] = {Y, Z};
+  double* const buf1[2] = {Y2, Z2};
+  hipMemsetAsync(state, 0, 2 * sizeof(int) * batch, st);  // state = 0, last = 0
   ns_init_kernel<<<batch, 256, 0, st>>>(A, Y, Z, svec, n, add);
-  for (int it = 0; it < kNSIters; ++it) {
-    small_gemm(Z, Y, T, n, batch, -0.5, 1.5, nullptr, st);  // T = (3I - ZY)/2
-    small_gemm(Y, T, Y2, n, batch, 1.0, 0.0, nullptr, st, T, Z, Z2);  // Y <- Y T, Z <- T Z
+  for (int it = 0; it < kNSMaxIters; ++it) {
+    small_gemm(Z, Y, T, n, batch, -0.5, 1.5, nullptr, st, nullptr, nullptr, nullptr, state, 1);
+    ns_residual_kernel<<<batch, 256, 0, st>>>(T, state, last, res, n, it);
+    // Y <- Y T, Z <- T Z
+    small_gemm(Y, T, Y2, n, batch, 1.0, 0.0, nullptr, st, T, Z, Z2, state, 2);
     double* t = Y;
     Y = Y2;
     Y2 = t;
@@ -569,26 +674,35 @@ static void ns_power(const double* A, double add, double* sqrt_out, double* isqr
     Z2 = t;
   }
   const unsigned blocks = (unsigned)((nn + 255) / 256);
-  if (sqrt_out) scale_pow_kernel<<<blocks, 256, 0, st>>>(Y, sqrt_out, svec, 0.5, (int64_t)n * n, batch);
-  if (isqrt_out) scale_pow_kernel<<<blocks, 256, 0, st>>>(Z, isqrt_out, svec, -0.5, (int64_t)n * n, batch);
+  // iteration it wrote buffer set (it + 1) & 1 (set 0 = Y/Z, set 1 = Y2/Z2 of the start)
+  if (sqrt_out)
+    ns_final_kernel<<<blocks, 256, 0, st>>>(buf0[0], buf1[0], sqrt_out, svec, last, 0.5,
+                                            (int64_t)n * n, batch);
+  if (isqrt_out)
+    ns_final_kernel<<<blocks, 256, 0, st>>>(buf0[1], buf1[1], isqrt_out, svec, last, -0.5,
+                                            (int64_t)n * n, batch);
+  if (res_out) hipMemcpyAsync(res_out, res, sizeof(double) * batch, hipMemcpyDeviceToDevice, st);
+  return launch_status("newton-schulz");
 }
 
-static size_t ns_work_doubles(int n, int batch) { return 5 * (size_t)n * n * batch + batch; }
+static size_t ns_work_doubles(int n, int batch) {
+  return 5 * (size_t)n * n * batch + 2 * (size_t)batch + (size_t)batch;  // + svec, res, state/last
+}
 
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return (e && *e) ? atoi(e) : dflt;
 }
 
-static int pick_ksplit(int batch, int tiles, int64_t K) {
-  // aim for ~4096 workgroups per covariance launch, each with >= kmin K values
-  // (profiles/r01_wct_blocks.log: 8192 -> 27.6 ms vs 28.9 at 4096)
-  const int64_t target = env_int("RPST_WCT_BLOCKS", 8192);
+// Split-K of the covariance SYRK: a function of the per-image K only, so an image's
+// summation order (and its bits) never depend on how many images share the launch (the
+// per-image multi-GPU split relies on that). K >= kmin per split, at most 128 splits:
+// at 512^2, 64 splits of 4096 (profiles/r01_wct_blocks.log: ~8192 workgroups at n = 16,
+// 27.6 ms vs 28.9 at 4096 for the whole fuse).
+static int pick_ksplit(int64_t K) {
   const int64_t kmin = env_int("RPST_WCT_KMIN", 4096);
-  int s = (int)((target + (int64_t)batch * tiles - 1) / ((int64_t)batch * tiles));
-  const int64_t maxs = K / kmin > 1 ? K / kmin : 1;
-  if (s > maxs) s = (int)maxs;
-  return s < 1 ? 1 : (s > 128 ? 128 : s);
+  const int64_t s = K / kmin;
+  return s < 1 ? 1 : (s > 128 ? 128 : (int)s);
 }
 
 struct WctLayout {
@@ -607,7 +721,7 @@ static WctLayout wct_layout(int n, int C, int64_t HW) {
   L.BT = (C >= 128 && env_int("RPST_WCT_COV_BT", 128) == 128) ? 128 : 64;
   L.tiles = (C + L.BT - 1) / L.BT;
   L.symtiles = L.tiles * (L.tiles + 1) / 2;
-  L.ksplit = pick_ksplit(2 * n, L.symtiles, HW);
+  L.ksplit = pick_ksplit(HW);
   const size_t cc = (size_t)C * C * n;
   size_t o = 0;
   L.mu_c = o; o += (size_t)n * C;
@@ -626,25 +740,56 @@ static WctLayout wct_layout(int n, int C, int64_t HW) {
   return L;
 }
 
-// Shared WCT body. SRC is SRC_F32C (fp32 features) or SRC_F64C (fp64 features).
-template <int SRC, int OUTM>
-static int wct_run(const void* cF, const void* sF, void* out, int n, int C, int64_t HW,
-                   void* workspace, hipStream_t st) {
-  const WctLayout L = wct_layout(n, C, HW);
-  double* ws = static_cast<double*>(workspace);
+// means (fp32, e.g. from the encoder's statistics epilogue: content rows then style rows,
+// 2n x C) widened to fp64
+__global__ void widen_means_kernel(const float* __restrict__ m, double* __restrict__ out,
+                                   int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) out[i] = (double)m[i];
+}
+
+// c[b][m] = mu_s[b][m] - sum_k T[b][m][k] mu_c[b][k]  (fixed order, fp64): the constant of
+// T (x - mu_c) + mu_s = T x + c
+__global__ void wct_offset_kernel(const double* __restrict__ T, const double* __restrict__ mu_c,
+                                  const double* __restrict__ mu_s, double* __restrict__ c,
+                                  int n, int C) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)n * C) return;
+  const int64_t b = i / C;
+  const double* t = T + i * C;  // row m of image b
+  const double* mc = mu_c + b * C;
+  double s = 0.0;
+  for (int k = 0; k < C; ++k) s = fma(t[k], mc[k], s);
+  c[i] = mu_s[i] - s;
+}
+
+// WCT matrices of every image: means (mu_c, mu_s in the workspace), covariances, the
+// Newton-Schulz powers and T = Ic Mid Ic (wct_rp.py:85-109). SRC is SRC_F32C (fp32
+// features) or SRC_F64C (fp64). means: optional fp32 (2n x C) row means; residual (2n,
+// optional): final Newton-Schulz residuals of (Cc + 1e-4 I) and of Mid's argument.
+template <int SRC>
+static int wct_matrices(const void* cF, const void* sF, const float* means, int n, int C,
+                        int64_t HW, const WctLayout& L, double* ws, double* residual,
+                        hipStream_t st) {
   double *mu_c = ws + L.mu_c, *mu_s = ws + L.mu_s, *part = ws + L.part;
   double *Cc = ws + L.cc, *Cs = ws + L.cs, *Sc = ws + L.sc, *Ic = ws + L.ic;
   double *M0 = ws + L.m0, *Mid = ws + L.mid, *tmp = ws + L.tmp, *Tm = ws + L.tm;
   double* nsw = ws + L.ns;
 
-  // 1. means (content rows then style rows)
-  if (SRC == SRC_F32C)
-    rowmean_kernel<float><<<2 * n * C, 256, 0, st>>>(static_cast<const float*>(cF),
-                                                    static_cast<const float*>(sF), n * C, HW, mu_c);
-  else
-    rowmean_kernel<double><<<2 * n * C, 256, 0, st>>>(static_cast<const double*>(cF),
-                                                     static_cast<const double*>(sF), n * C, HW, mu_c);
-  if (int e = launch_status("rowmean_kernel")) return e;
+  // 1. means (content rows then style rows; mu_s follows mu_c in the workspace)
+  if (means) {
+    const int64_t cnt = (int64_t)2 * n * C;
+    widen_means_kernel<<<(unsigned)((cnt + 255) / 256), 256, 0, st>>>(means, mu_c, cnt);
+    if (int e = launch_status("widen_means_kernel")) return e;
+  } else {
+    if (SRC == SRC_F32C)
+      rowmean_kernel<float><<<2 * n * C, 256, 0, st>>>(static_cast<const float*>(cF),
+                                                      static_cast<const float*>(sF), n * C, HW, mu_c);
+    else
+      rowmean_kernel<double><<<2 * n * C, 256, 0, st>>>(static_cast<const double*>(cF),
+                                                       static_cast<const double*>(sF), n * C, HW, mu_c);
+    if (int e = launch_status("rowmean_kernel")) return e;
+  }
 
   // 2. covariances: upper-triangular tiles, split-K partials, fixed-order reduce
   for (int which = 0; which < 2; ++which) {
@@ -677,15 +822,27 @@ static int wct_run(const void* cF, const void* sF, void* out, int n, int C, int6
   if (int e = launch_status("cov_reduce_kernel")) return e;
 
   // 3. Sc, Ic = (Cc + 1e-4 I)^(+-1/2)
-  ns_power(Cc, 1e-4, Sc, Ic, C, n, nsw, st);
+  if (int e = ns_power(Cc, 1e-4, Sc, Ic, C, n, nsw, st, residual)) return e;
   // 4. Mid = (Sc Cs Sc + 1e-4 I)^(1/2)
   small_gemm(Sc, Cs, tmp, C, n, 1.0, 0.0, nullptr, st);
   small_gemm(tmp, Sc, M0, C, n, 1.0, 0.0, nullptr, st);
-  ns_power(M0, 1e-4, Mid, nullptr, C, n, nsw, st);
+  if (int e = ns_power(M0, 1e-4, Mid, nullptr, C, n, nsw, st, residual ? residual + n : nullptr))
+    return e;
   // 5. T = Ic Mid Ic
   small_gemm(Ic, Mid, tmp, C, n, 1.0, 0.0, nullptr, st);
   small_gemm(tmp, Ic, Tm, C, n, 1.0, 0.0, nullptr, st);
-  if (int e = launch_status("wct matrix functions")) return e;
+  return launch_status("wct matrix functions");
+}
+
+// Shared WCT body: the matrices, then out = T (cF - mu_c) + mu_s.
+template <int SRC, int OUTM>
+static int wct_run(const void* cF, const void* sF, void* out, int n, int C, int64_t HW,
+                   void* workspace, double* residual, hipStream_t st) {
+  const WctLayout L = wct_layout(n, C, HW);
+  double* ws = static_cast<double*>(workspace);
+  if (int e = wct_matrices<SRC>(cF, sF, nullptr, n, C, HW, L, ws, residual, st)) return e;
+  double *mu_c = ws + L.mu_c, *mu_s = ws + L.mu_s;
+  double *M0 = ws + L.m0, *Mid = ws + L.mid, *Tm = ws + L.tm;
 
   // 6. out = T (cF - mu_c) + mu_s; fp32 features -> fp32 MFMA (RPST_WCT_T_F64=1: fp64)
   if (SRC == SRC_F32C && OUTM == OUT_F32_BIAS && !env_int("RPST_WCT_T_F64", 0)) {
@@ -694,18 +851,8 @@ static int wct_run(const void* cF, const void* sF, void* out, int n, int C, int6
     const int64_t nT = (int64_t)n * C * C, nmu = (int64_t)2 * n * C;  // mu_c, mu_s adjacent
     wct_f32_prep_kernel<<<(unsigned)((std::max(nT, nmu) + 255) / 256), 256, 0, st>>>(Tm, mu_c, Tf, muf, nT, nmu, C);
     if (int e = launch_status("wct_f32_prep_kernel")) return e;
-    dim3 grid((unsigned)((HW + 127) / 128), (C + 127) / 128, n);
-    const bool vec = (HW % 4 == 0) && (C % 4 == 0) &&
-                     (reinterpret_cast<uintptr_t>(cF) & 15) == 0;
-    if (vec)
-      wct_transform_f32_kernel<true><<<grid, 256, 0, st>>>(
-          Tf, static_cast<const float*>(cF), muf, muf + (size_t)n * C, static_cast<float*>(out),
-          C, (int)HW);
-    else
-      wct_transform_f32_kernel<false><<<grid, 256, 0, st>>>(
-          Tf, static_cast<const float*>(cF), muf, muf + (size_t)n * C, static_cast<float*>(out),
-          C, (int)HW);
-    return launch_status("wct_transform_f32_kernel");
+    return wct_transform_f32(Tf, static_cast<const float*>(cF), muf, muf + (size_t)n * C,
+                             static_cast<float*>(out), n, C, HW, st);
   }
   G64Args g{};
   g.A = Tm;
@@ -744,8 +891,8 @@ extern "C" size_t rpst_wct_workspace_size(int n, int C, int64_t HW) {
 }
 
 extern "C" int rpst_wct_fuse(const float* content, const float* style, float* out, int n, int C,
-                             int64_t HW, void* workspace, size_t workspace_bytes,
-                             rpst_stream_t stream) {
+                             int64_t HW, double* residual, void* workspace,
+                             size_t workspace_bytes, rpst_stream_t stream) {
   RPST_REQUIRE(content && style && out, "wct_fuse: null pointer");
   RPST_REQUIRE(n > 0 && C > 0 && HW > 1, "wct_fuse: bad shape n=%d C=%d HW=%lld", n, C, (long long)HW);
   RPST_REQUIRE(HW <= 0x7fffffffLL && n <= 65535, "wct_fuse: shape too large");
@@ -753,19 +900,45 @@ extern "C" int rpst_wct_fuse(const float* content, const float* style, float* ou
     set_error("wct_fuse: workspace %zu < %zu bytes", workspace_bytes, rpst_wct_workspace_size(n, C, HW));
     return RPST_EWORKSPACE;
   }
-  return wct_run<SRC_F32C, OUT_F32_BIAS>(content, style, out, n, C, HW, workspace, as_stream(stream));
+  return wct_run<SRC_F32C, OUT_F32_BIAS>(content, style, out, n, C, HW, workspace, residual,
+                                         as_stream(stream));
+}
+
+extern "C" int rpst_wct_params(const float* content, const float* style, const float* means,
+                               double* T, double* offset, int n, int C, int64_t HW,
+                               double* residual, void* workspace, size_t workspace_bytes,
+                               rpst_stream_t stream) {
+  RPST_REQUIRE(content && style && T && offset, "wct_params: null pointer");
+  RPST_REQUIRE(n > 0 && C > 0 && HW > 1, "wct_params: bad shape n=%d C=%d HW=%lld", n, C,
+               (long long)HW);
+  RPST_REQUIRE(HW <= 0x7fffffffLL && n <= 65535, "wct_params: shape too large");
+  if (!workspace || workspace_bytes < rpst_wct_workspace_size(n, C, HW)) {
+    set_error("wct_params: workspace %zu < %zu bytes", workspace_bytes,
+              rpst_wct_workspace_size(n, C, HW));
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  const WctLayout L = wct_layout(n, C, HW);
+  double* ws = static_cast<double*>(workspace);
+  if (int e = wct_matrices<SRC_F32C>(content, style, means, n, C, HW, L, ws, residual, st)) return e;
+  hipMemcpyAsync(T, ws + L.tm, sizeof(double) * n * C * C, hipMemcpyDeviceToDevice, st);
+  const int64_t nc = (int64_t)n * C;
+  wct_offset_kernel<<<(unsigned)((nc + 255) / 256), 256, 0, st>>>(ws + L.tm, ws + L.mu_c,
+                                                                  ws + L.mu_s, offset, n, C);
+  return launch_status("wct_offset_kernel");
 }
 
 extern "C" int rpst_whiten_and_color_f64(const double* cF, const double* sF, double* out, int C,
-                                         int64_t HW, void* workspace, size_t workspace_bytes,
-                                         rpst_stream_t stream) {
+                                         int64_t HW, double* residual, void* workspace,
+                                         size_t workspace_bytes, rpst_stream_t stream) {
   RPST_REQUIRE(cF && sF && out, "whiten_and_color: null pointer");
   RPST_REQUIRE(C > 0 && HW > 1 && HW <= 0x7fffffffLL, "whiten_and_color: bad shape");
   if (!workspace || workspace_bytes < rpst_wct_workspace_size(1, C, HW)) {
     set_error("whiten_and_color: workspace too small");
     return RPST_EWORKSPACE;
   }
-  return wct_run<SRC_F64C, OUT_F64_BIAS>(cF, sF, out, 1, C, HW, workspace, as_stream(stream));
+  return wct_run<SRC_F64C, OUT_F64_BIAS>(cF, sF, out, 1, C, HW, workspace, residual,
+                                         as_stream(stream));
 }
 
 extern "C" size_t rpst_matrix_power_workspace_size(int n, int batch) {
@@ -774,8 +947,8 @@ extern "C" size_t rpst_matrix_power_workspace_size(int n, int batch) {
 }
 
 extern "C" int rpst_matrix_power_psd_f64(const double* A, double* out, int n, int batch,
-                                         int inverse, void* workspace, size_t workspace_bytes,
-                                         rpst_stream_t stream) {
+                                         int inverse, double* residual, void* workspace,
+                                         size_t workspace_bytes, rpst_stream_t stream) {
   RPST_REQUIRE(A && out, "matrix_power: null pointer");
   RPST_REQUIRE(n > 0 && batch > 0 && batch <= 65535, "matrix_power: bad shape");
   if (!workspace || workspace_bytes < rpst_matrix_power_workspace_size(n, batch)) {
@@ -784,9 +957,6 @@ extern "C" int rpst_matrix_power_psd_f64(const double* A, double* out, int n, in
   }
   hipStream_t st = as_stream(stream);
   double* w = static_cast<double*>(workspace);
-  if (inverse)
-    ns_power(A, 1e-4, nullptr, out, n, batch, w, st);
-  else
-    ns_power(A, 1e-4, out, nullptr, n, batch, w, st);
-  return launch_status("matrix_power_psd");
+  if (inverse) return ns_power(A, 1e-4, nullptr, out, n, batch, w, st, residual);
+  return ns_power(A, 1e-4, out, nullptr, n, batch, w, st, residual);
 }

@@ -63,10 +63,17 @@ static_assert(kW4WCH % (64 * 4) == 0, "weight slice = whole 1-KiB LDS-DMA pieces
 // ci = c*8 + 4s + (l >> 4): lane l's A operands of positions 2q, 2q+1 (both channel halves)
 // are one 16-B word, and one (co tile, chunk) slice is contiguous (the LDS-DMA copies it
 // verbatim).
-__global__ void wino4_pack_kernel(const float* __restrict__ w, float* __restrict__ pk, int Cout,
-                                  int Cin, int nch, int64_t total) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// TW = float (the layer's weights) or double (per-image folded weights, wino4_mix): image
+// b's weights at w + b * Cout * Cin * 9 pack to pk + b * per.
+template <typename TW>
+__global__ void wino4_pack_kernel(const TW* __restrict__ w, float* __restrict__ pk, int Cout,
+                                  int Cin, int nch, int64_t per, int64_t total) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
+  const int64_t img = t / per;
+  pk += img * per;
+  w += img * (int64_t)Cout * Cin * 9;
+  t -= img * per;
   const int e = (int)(t & 3);
   int64_t r = t >> 2;
   const int l = (int)(r & 63);
@@ -91,7 +98,7 @@ __global__ void wino4_pack_kernel(const float* __restrict__ w, float* __restrict
                             {1.0 / 24, 1.0 / 12, 1.0 / 6},
                             {1.0 / 24, -1.0 / 12, 1.0 / 6},
                             {0, 0, 1}};
-    const float* g = w + ((int64_t)co * Cin + ci) * 9;
+    const TW* g = w + ((int64_t)co * Cin + ci) * 9;
     double acc = 0.0;
 #pragma unroll
     for (int u = 0; u < 3; ++u)
@@ -111,7 +118,7 @@ size_t wino4_packed_floats(int Cout, int Cin) {
 int wino4_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st) {
   const int nch = (Cin + kW4CK - 1) / kW4CK;
   const int64_t t = (int64_t)wino4_packed_floats(Cout, Cin);
-  wino4_pack_kernel<<<(unsigned)((t + 255) / 256), 256, 0, st>>>(w, pk, Cout, Cin, nch, t);
+  wino4_pack_kernel<float><<<(unsigned)((t + 255) / 256), 256, 0, st>>>(w, pk, Cout, Cin, nch, t, t);
   return launch_status("wino4_pack_kernel");
 }
 
@@ -673,6 +680,92 @@ int wino4_fold(ConvArgs& a, const float* direct_packed, int direct_cout_pad, flo
       direct_packed, a.bias, a.aux, bt, a.N, a.Cin, a.Cout, direct_cout_pad,
       a.pad == RPST_PAD_REFLECT);
   if (int e = launch_status("wino4_fold_b_kernel")) return e;
+  a.wpk = wf;
+  a.wstride = per;
+  a.btab = bt;
+  return RPST_OK;
+}
+
+// ---- a channel-mixing input folded into the weights (WCT feeding the decoder) --------
+// conv(pad(T_n x + c_n)) = conv_{W T_n}(pad(x)) + sum_m c_n[m] sum_{taps inside} W[co][m][tap]
+// (T_n commutes with the padding: zero padding maps to zero, reflection is spatial). Image
+// n gets weights W'_n = W T_n (fp64, from the direct-packed image: W[co][m][tap] =
+// dpk[(m / 8 * 9 + tap) * 8 * cout_pad + (m % 8) * cout_pad + co]), packed as U'_n = G W'_n
+// G^T with one rounding to fp32, and a bias per (n, co) and border class from c_n. With
+// T_n = diag(s), c_n = b this is the AdaIN fold above.
+size_t wino4_mix_floats(int N, int Cin, int Cout) {
+  return wino4_fold_floats(N, Cin, Cout) + 2 * (size_t)N * Cout * Cin * 9;
+}
+
+__global__ void mix_weights_kernel(const float* __restrict__ dpk, const double* __restrict__ T,
+                                   double* __restrict__ wm, int N, int Cin, int Cout,
+                                   int cout_pad) {
+  // t -> (n, co, tap, k), k fastest: the T[n][m][k] reads of a wave are contiguous
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * Cout * 9 * Cin) return;
+  const int k = (int)(t % Cin);
+  int64_t r = t / Cin;
+  const int tap = (int)(r % 9);
+  r /= 9;
+  const int co = (int)(r % Cout);
+  const int n = (int)(r / Cout);
+  const double* Tn = T + (int64_t)n * Cin * Cin + k;
+  double acc = 0.0;
+  for (int m = 0; m < Cin; ++m)
+    acc = fma((double)dpk[((int64_t)(m >> 3) * 9 + tap) * 8 * cout_pad + (m & 7) * cout_pad + co],
+              Tn[(int64_t)m * Cin], acc);
+  wm[(((int64_t)n * Cout + co) * Cin + k) * 9 + tap] = acc;
+}
+
+// btab[(n * Cout + co) * 9 + cls] = bias[co] + sum_m cvec[n][m] sum_{taps of the class} W
+__global__ void wino4_mix_bias_kernel(const float* __restrict__ dpk, const float* __restrict__ bias,
+                                      const double* __restrict__ cvec, float* __restrict__ btab,
+                                      int N, int Cin, int Cout, int cout_pad, int reflect) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * Cout * 9) return;
+  const int co = (int)(t % Cout);
+  const int64_t r = t / Cout;
+  const int cls = (int)(r % 9), n = (int)(r / 9);
+  const int rc = cls / 3, cc = cls % 3;
+  double acc = 0.0;
+  for (int ci = 0; ci < Cin; ++ci) {
+    const float* w = dpk + ((int64_t)(ci >> 3) * 9 * 8 + (ci & 7)) * cout_pad + co;
+    double tap = 0.0;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const bool in = reflect || ((rc != 0 || u != 0) && (rc != 2 || u != 2) &&
+                                    (cc != 0 || p != 0) && (cc != 2 || p != 2));
+        if (in) tap += (double)w[(int64_t)(u * 3 + p) * 8 * cout_pad];
+      }
+    acc += cvec[(int64_t)n * Cin + ci] * tap;
+  }
+  btab[((int64_t)n * Cout + co) * 9 + cls] = (float)((bias ? (double)bias[co] : 0.0) + acc);
+}
+
+int wino4_mix(ConvArgs& a, const double* T, const double* cvec, const float* direct_packed,
+              int direct_cout_pad, float* ws, hipStream_t st) {
+  RPST_REQUIRE(a.H >= 2 && a.W >= 2, "conv2d_mix: needs H, W >= 2");
+  const int nch = (a.Cin + kW4CK - 1) / kW4CK;
+  const int64_t per = (int64_t)wino4_packed_floats(a.Cout, a.Cin);
+  float* wf = ws;
+  float* bt = ws + (int64_t)a.N * per;
+  double* wm = reinterpret_cast<double*>(bt + (int64_t)a.N * a.Cout * 9 + 1);  // 8-B aligned below
+  wm = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(wm) + 7) & ~uintptr_t(7));
+  const int64_t nw = (int64_t)a.N * a.Cout * 9 * a.Cin;
+  mix_weights_kernel<<<(unsigned)((nw + 255) / 256), 256, 0, st>>>(direct_packed, T, wm, a.N, a.Cin,
+                                                                   a.Cout, direct_cout_pad);
+  if (int e = launch_status("mix_weights_kernel")) return e;
+  const int64_t tot = (int64_t)a.N * per;
+  wino4_pack_kernel<double><<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(wm, wf, a.Cout, a.Cin,
+                                                                           nch, per, tot);
+  if (int e = launch_status("wino4_pack_kernel(mix)")) return e;
+  const int64_t nb = (int64_t)a.N * a.Cout * 9;
+  wino4_mix_bias_kernel<<<(unsigned)((nb + 127) / 128), 128, 0, st>>>(
+      direct_packed, a.bias, cvec, bt, a.N, a.Cin, a.Cout, direct_cout_pad,
+      a.pad == RPST_PAD_REFLECT);
+  if (int e = launch_status("wino4_mix_bias_kernel")) return e;
   a.wpk = wf;
   a.wstride = per;
   a.btab = bt;

@@ -9,15 +9,37 @@ fp32, widened to fp64 in registers, and the fused feature is written back as fp3
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
-from rpst import ops
+from rpst import ops, plan
 from rpst.plan import KernelSequential
 
 from .adain_rp import AdaINRPNet, encode_both  # noqa: F401 (re-export, wct_rp.py:3)
 from .base import (BaseNet, build_decrease_depth_rp_blocks, build_increase_depth_rp_blocks,
                    calc_mean_std, mse)
+
+
+# RPST_FUSE_WCT=0 disables the fused path (A/B measurements, debugging)
+FUSED_WCT = os.environ.get("RPST_FUSE_WCT", "1") != "0"
+
+
+def wct_rp_fused(encoder, decoder, content, style):
+    """enc -> WCT -> dec (wct_rp.py:139-147) with the colour transform fused away: the
+    encoder runs once over [content; style] and its last conv reduces the row means in its
+    epilogue; the closed-form matrices T and c = mu_s - T mu_c come from rpst_wct_params
+    (fp64), and the decoder's first conv reads T_n x + c_n through per-image folded weights
+    (rpst_conv2d_mix), so the fused feature T (cF - mu_c) + mu_s is never written."""
+    n = content.shape[0]
+    assert content.size() == style.size()
+    feats, mean, _ = plan.run(plan.compile_layers(encoder.children()),
+                              torch.cat([content, style], dim=0), stats_last=True)
+    T, c, res = ops.wct_params(feats[:n], feats[n:], means=mean.reshape(2 * n, -1))
+    out = plan.run(plan.compile_layers(decoder.children()), feats[:n], first_mix=(T, c))
+    ops.check_ns_residual(res, "WCTRPNet.test")  # after every launch is queued
+    return out
 
 
 def matrix_inv_sqrt(A):
@@ -86,9 +108,12 @@ class WCTRPNet(BaseNet):
     def test(self, content, style, iterations=0, bid=0, c_mask_path=None, s_mask_path=None):
         self.eval()
         with torch.no_grad():
-            content_feat, style_feat = encode_both(self.rp_shared_encoder, content, style)
-            fusion_feat = self.fuse(content_feat, style_feat)
-            stylized = self.rp_decoder(fusion_feat)
+            if type(self).fuse is WCTRPNet.fuse and FUSED_WCT:
+                stylized = wct_rp_fused(self.rp_shared_encoder, self.rp_decoder, content, style)
+            else:
+                content_feat, style_feat = encode_both(self.rp_shared_encoder, content, style)
+                fusion_feat = self.fuse(content_feat, style_feat)
+                stylized = self.rp_decoder(fusion_feat)
             self.train()
             return stylized
 

@@ -69,10 +69,14 @@ SIGNATURES = {
     "rpst_adaptive_attention": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _F, _F, _P,
                                      _P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
     "rpst_matrix_power_workspace_size": (_SZ, [_I, _I]),
-    "rpst_matrix_power_psd_f64": (_I, [_P, _P, _I, _I, _I, _P, _SZ, _P]),
+    "rpst_matrix_power_psd_f64": (_I, [_P, _P, _I, _I, _I, _P, _P, _SZ, _P]),
     "rpst_wct_workspace_size": (_SZ, [_I, _I, _I64]),
-    "rpst_whiten_and_color_f64": (_I, [_P, _P, _P, _I, _I64, _P, _SZ, _P]),
-    "rpst_wct_fuse": (_I, [_P, _P, _P, _I, _I, _I64, _P, _SZ, _P]),
+    "rpst_whiten_and_color_f64": (_I, [_P, _P, _P, _I, _I64, _P, _P, _SZ, _P]),
+    "rpst_wct_fuse": (_I, [_P, _P, _P, _I, _I, _I64, _P, _P, _SZ, _P]),
+    "rpst_wct_params": (_I, [_P, _P, _P, _P, _P, _I, _I, _I64, _P, _P, _SZ, _P]),
+    "rpst_conv2d_mix_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
+    "rpst_conv2d_mix": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _SZ,
+                             _P]),
 }
 
 _lib = None

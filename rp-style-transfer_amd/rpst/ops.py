@@ -434,9 +434,26 @@ def adaptive_attention(F: torch.Tensor, G: torch.Tensor, H: torch.Tensor,
     return out, claim, before, after
 
 
+# Newton-Schulz convergence bar of the library (include/rpst.h, a7): a residual at or
+# above it means the matrix was not symmetric positive semi-definite (after +1e-4 I)
+NS_TOL = 1e-10
+
+
+def check_ns_residual(res: torch.Tensor, what: str) -> None:
+    """Raise if any Newton-Schulz residual missed the bar (one host sync). The reference's
+    SVD form (wct_rp.py:7-40) would return V |S|^p V^T for an indefinite input; the
+    kernels reject such inputs instead of returning a silently different power."""
+    bad = ~(res < NS_TOL)
+    if bool(bad.any()):
+        raise RuntimeError(
+            f"rpst {what}: Newton-Schulz did not converge for {int(bad.sum())} matrix(es) "
+            f"(residual {float(res.max()):.3e} >= {NS_TOL}); the input must be symmetric "
+            "positive semi-definite")
+
+
 def matrix_power_psd(A: torch.Tensor, p: float) -> torch.Tensor:
     """(A + 1e-4 I)^p, p = +-1/2, for symmetric PSD fp64 (n,n) or (b,n,n) matrices
-    (wct_rp.py:7-40)."""
+    (wct_rp.py:7-40). Non-PSD inputs raise RuntimeError (see check_ns_residual)."""
     assert p in (0.5, -0.5)
     _check(A, dtype=torch.float64)
     A = _c(A)
@@ -444,10 +461,12 @@ def matrix_power_psd(A: torch.Tensor, p: float) -> torch.Tensor:
     assert A.shape[-2] == n
     batch = A.numel() // (n * n)
     out = torch.empty_like(A)
+    res = torch.empty(batch, device=A.device, dtype=torch.float64)
     nbytes = _lib.load().rpst_matrix_power_workspace_size(n, batch)
     ws = torch.empty(nbytes, device=A.device, dtype=torch.uint8)
     _lib.call("rpst_matrix_power_psd_f64", A.data_ptr(), out.data_ptr(), n, batch,
-              int(p < 0), ws.data_ptr(), nbytes, _stream(A))
+              int(p < 0), res.data_ptr(), ws.data_ptr(), nbytes, _stream(A))
+    check_ns_residual(res, "matrix_power")
     return out
 
 
@@ -458,23 +477,75 @@ def whiten_and_color(cF: torch.Tensor, sF: torch.Tensor) -> torch.Tensor:
     cF, sF = _c(cF), _c(sF)
     C, hw = cF.shape
     out = torch.empty_like(cF)
+    res = torch.empty(2, device=cF.device, dtype=torch.float64)
     nbytes = _lib.load().rpst_wct_workspace_size(1, C, hw)
     ws = torch.empty(nbytes, device=cF.device, dtype=torch.uint8)
     _lib.call("rpst_whiten_and_color_f64", cF.data_ptr(), sF.data_ptr(), out.data_ptr(), C, hw,
-              ws.data_ptr(), nbytes, _stream(cF))
+              res.data_ptr(), ws.data_ptr(), nbytes, _stream(cF))
+    check_ns_residual(res, "whiten_and_color")
     return out
 
 
-def wct_fuse(content: torch.Tensor, style: torch.Tensor) -> torch.Tensor:
+def wct_fuse(content: torch.Tensor, style: torch.Tensor, check: bool = True) -> torch.Tensor:
     """WCTRPNet.fuse (wct_rp.py:157-166): (n,C,h,w) fp32 -> fp32, fp64 internals."""
     assert content.dim() == 4 and content.shape == style.shape
     _check(content, style)
     content, style = _c(content), _c(style)
     n, C, h, w = content.shape
     out = torch.empty_like(content)
+    res = torch.empty(2 * n, device=content.device, dtype=torch.float64)
     nbytes = _lib.load().rpst_wct_workspace_size(n, C, h * w)
     ws = torch.empty(nbytes, device=content.device, dtype=torch.uint8)
     with _traced(f"wct_fuse C{C} {h * w}px N{n}", 6.0 * n * C * C * h * w, 0.0):
         _lib.call("rpst_wct_fuse", content.data_ptr(), style.data_ptr(), out.data_ptr(), n, C,
-                  h * w, ws.data_ptr(), nbytes, _stream(content))
+                  h * w, res.data_ptr(), ws.data_ptr(), nbytes, _stream(content))
+    if check:
+        check_ns_residual(res, "wct_fuse")
+    return out
+
+
+def wct_params(content: torch.Tensor, style: torch.Tensor, means: Optional[torch.Tensor] = None):
+    """The closed-form WCT matrices of every image without the product (wct_rp.py:85-109):
+    returns (T (n,C,C) fp64, offset c = mu_s - T mu_c (n,C) fp64, residual (2n,) fp64).
+    means: optional (2n, C) fp32 row means, content rows first (the encoder epilogue's)."""
+    assert content.dim() == 4 and content.shape == style.shape
+    _check(content, style, means)
+    content, style = _c(content), _c(style)
+    n, C, h, w = content.shape
+    if means is not None:
+        means = _c(means)
+        assert means.numel() == 2 * n * C
+    T = torch.empty((n, C, C), device=content.device, dtype=torch.float64)
+    c = torch.empty((n, C), device=content.device, dtype=torch.float64)
+    res = torch.empty(2 * n, device=content.device, dtype=torch.float64)
+    nbytes = _lib.load().rpst_wct_workspace_size(n, C, h * w)
+    ws = torch.empty(nbytes, device=content.device, dtype=torch.uint8)
+    with _traced(f"wct_params C{C} {h * w}px N{n}", 4.0 * n * C * C * h * w, 0.0):
+        _lib.call("rpst_wct_params", content.data_ptr(), style.data_ptr(), _ptr(means),
+                  T.data_ptr(), c.data_ptr(), n, C, h * w, res.data_ptr(), ws.data_ptr(), nbytes,
+                  _stream(content))
+    return T, c, res
+
+
+def conv2d_mix(x: torch.Tensor, T: torch.Tensor, offset: torch.Tensor, packed: torch.Tensor,
+               bias: Optional[torch.Tensor], cout: int, ksize: int, pad: int = PAD_ZERO,
+               relu=False) -> torch.Tensor:
+    """out = act(conv(pad(T_n x + c_n)) + bias) per image (include/rpst.h rpst_conv2d_mix):
+    the WCT colour transform (wct_rp.py:109-113) applied inside the consumer conv."""
+    assert x.dim() == 4
+    _check(x, packed, bias)
+    _check(T, offset, dtype=torch.float64)
+    x, T, offset = _c(x), _c(T), _c(offset)
+    n, cin, h, w = x.shape
+    assert tuple(T.shape) == (n, cin, cin) and tuple(offset.shape) == (n, cin)
+    out = torch.empty((n, cout, h, w), device=x.device, dtype=torch.float32)
+    nbytes = _lib.load().rpst_conv2d_mix_workspace_size(n, cin, h, w, cout, ksize)
+    ws = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
+    with _traced(_conv_name(ksize, cin, cout, h, w, n, IN_NONE).replace(" op0", " mix"),
+                 2.0 * n * cout * h * w * cin * ksize * ksize,
+                 4.0 * (x.numel() + n * cout * h * w)):
+        _lib.call("rpst_conv2d_mix", x.data_ptr(), T.data_ptr(), offset.data_ptr(),
+                  packed.data_ptr(), _ptr(None if bias is None else _c(bias.detach())),
+                  out.data_ptr(), n, cin, h, w, cout, ksize, pad, _act(relu), ws.data_ptr(),
+                  nbytes, _stream(x))
     return out

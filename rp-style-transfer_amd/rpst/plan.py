@@ -138,13 +138,22 @@ def run_conv_step(step: ConvStep, x: torch.Tensor, aux=None, residual=None) -> t
 
 
 def run(steps: List[object], x: torch.Tensor, first_aux=None, first_in_op=None,
-        stats_last: bool = False, first_content=None):
+        stats_last: bool = False, first_content=None, first_mix=None):
     """Run a compiled plan. first_in_op/first_aux override the first conv's input operator
     (e.g. RPST_IN_ADAIN to fuse AdaIN into the decoder's first conv; RPST_IN_ADD_ADAIN
-    with first_content = the skip feature, for x + AdaIN(content)); stats_last makes the
-    last conv also return calc_mean_std of its output -> (x, mean, std)."""
+    with first_content = the skip feature, for x + AdaIN(content)); first_mix = (T, c)
+    makes the first conv read T_n x + c_n (the WCT colour transform, rpst_conv2d_mix);
+    stats_last makes the last conv also return calc_mean_std of its output -> (x, mean,
+    std)."""
     mean = std = None
     for i, s in enumerate(steps):
+        if isinstance(s, ConvStep) and i == 0 and first_mix is not None:
+            if s.in_op != ops.IN_NONE or (stats_last and len(steps) == 1):
+                raise NotImplementedError("rpst plan: mixed first conv with an input op / stats")
+            c = s.conv
+            x = ops.conv2d_mix(x, first_mix[0], first_mix[1], packed_weight(c), c.bias,
+                               c.out_channels, c.kernel_size[0], pad=s.pad, relu=s.relu)
+            continue
         if isinstance(s, ConvStep):
             in_op, aux = s.in_op, None
             if i == 0 and first_in_op is not None:

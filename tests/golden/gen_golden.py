@@ -334,6 +334,60 @@ def gen_multiscale(net):
     np.savez_compressed(os.path.join(HERE, "multiscale.npz"), n=len(cases), **out)
 
 
+def gen_deeper(net):
+    """MultiScaleAdaINRPNet.test, 'deeper' stack (rp_deeper_conv_blocks encoder with 1x1
+    inception convs, rp_shallower_conv_blocks decoder; adain_rp.py:152-156 as configured by
+    config/rl/train_deeper_multiscale_rp_adain.yaml:31-33, hidden 16, inception 3)."""
+    out = {}
+    cases = [(4, 5, 3, (1, 3, 24, 32), 44), (16, 5, 3, (1, 3, 16, 16), 45),
+             (8, 3, 1, (2, 3, 9, 13), 46)]
+    for i, (hid, blocks, inc, shp, seed) in enumerate(cases):
+        cfg = multiscale_config(hid, blocks, inc)
+        cfg["enc_stack_way"] = "deeper"
+        m = net.MultiScaleAdaINRPNet(cfg, copy.deepcopy(net.vgg))
+        ck = synth_model_(m, seed)
+        c = synth.image(4300 + i, shp)
+        s = synth.image(4400 + i, shp)
+        y = m.test(t(c), t(s))
+        out.update({f"hidden{i}": hid, f"blocks{i}": blocks, f"inception{i}": inc,
+                    f"seed{i}": seed, f"checksum{i}": ck, f"content{i}": c, f"style{i}": s,
+                    f"out{i}": y.numpy()})
+    np.savez_compressed(os.path.join(HERE, "deeper.npz"), n=len(cases), **out)
+
+
+def gen_grads(net):
+    """Reference training gradients: AdaINRPNet.forward + total_loss.backward()
+    (adain_rp.py:110-138, train.py:186-189) on CPU; the RP encoder / decoder parameter
+    gradients (the VGG is frozen, adain_rp.py:27-29) and the loss values."""
+    out = {}
+    cases = [(4, (2, 3, 32, 32), 24, 1.0, 10.0), (16, (1, 3, 128, 128), 25, 1.0, 1.0)]
+    for i, (hid, shp, seed, cw, sw) in enumerate(cases):
+        cfg = rp_config(hid)
+        cfg.update(content_weight=cw, style_weight=sw)
+        m = net.AdaINRPNet(cfg, copy.deepcopy(net.vgg))
+        ck = synth_model_(m, seed)
+        c = synth.image(3100 + i, shp)
+        s = synth.image(3200 + i, shp)
+        m.zero_grad()
+        d, tot = m.forward(t(c), t(s))
+        tot.backward()
+        out.update({f"hidden{i}": hid, f"seed{i}": seed, f"checksum{i}": ck, f"cw{i}": cw,
+                    f"sw{i}": sw, f"content{i}": c, f"style{i}": s,
+                    f"style_loss{i}": d["style_loss"].detach().numpy(),
+                    f"content_loss{i}": d["content_loss"].detach().numpy(),
+                    f"total_loss{i}": tot.detach().numpy()})
+        names = []
+        for name, p in m.named_parameters():
+            if p.requires_grad:
+                assert p.grad is not None, name
+                out[f"grad{i}:{name}"] = p.grad.numpy()
+                names.append(name)
+            else:
+                assert p.grad is None, name
+        out[f"names{i}"] = np.array(names)
+    np.savez_compressed(os.path.join(HERE, "grads.npz"), n=len(cases), **out)
+
+
 def gen_sourcenet(net):
     """SourceNet.test, classic AdaIN on VGG relu4_1."""
     out = {}
@@ -375,7 +429,7 @@ def gen_keys(net):
 GENERATORS = {"keys": gen_keys, "stats": gen_stats, "adain_rp": gen_adain_rp,
               "forward": gen_forward, "wct": gen_wct, "sanet": gen_sanet, "vgg": gen_vgg,
               "multiscale": gen_multiscale, "sourcenet": gen_sourcenet,
-              "adaptive": gen_adaptive}
+              "adaptive": gen_adaptive, "deeper": gen_deeper, "grads": gen_grads}
 
 
 def main():

@@ -49,3 +49,11 @@ def multiscale_config(hidden, blocks=5, inception=0):
 
 
 SOURCE_CONFIG = {"use_mask": False, "content_weight": 1.0, "style_weight": 10.0}
+
+
+def deeper_config(hidden, blocks=5, inception=3):
+    """MultiScaleAdaINRPNet 'deeper' stack (config/rl/train_deeper_multiscale_rp_adain.yaml:
+    enc_stack_way deeper, inception_num 3, hidden 16)."""
+    cfg = multiscale_config(hidden, blocks, inception)
+    cfg["enc_stack_way"] = "deeper"
+    return cfg

@@ -176,6 +176,99 @@ def test_wct_rp_vs_oracle_hidden16(cuda):
     assert max_abs_ratio(out, ref) < TOL_NET_MAXABS
 
 
+def test_matrix_power_rejects_indefinite(cuda):
+    """The reference's SVD form returns V |S|^p V^T for an indefinite symmetric input
+    (wct_rp.py:7-40); Newton-Schulz cannot converge there, so the kernels report it."""
+    import network as net
+    a = torch.diag(torch.tensor([4.0, 1.0, -2.0, 0.5], dtype=torch.float64)).to(cuda)
+    with pytest.raises(RuntimeError, match="positive semi-definite"):
+        net.matrix_sqrt(a)
+    with pytest.raises(RuntimeError, match="positive semi-definite"):
+        net.matrix_inv_sqrt(a)
+
+
+def test_matrix_power_residual_and_conditioning(cuda):
+    """Ill-conditioned PSD batch (eigenvalues 1e-4 .. 1e4 after the shift): every matrix
+    converges (residual < 1e-10) and matches an eigendecomposition."""
+    from rpst import _lib, ops
+    g = torch.Generator().manual_seed(5)
+    mats = []
+    for b in range(3):
+        q, _ = torch.linalg.qr(torch.randn(96, 96, generator=g, dtype=torch.float64))
+        ev = torch.logspace(-6 + b, 4, 96, dtype=torch.float64)
+        mats.append(q @ torch.diag(ev) @ q.T)
+    a = torch.stack(mats)
+    out = ops.matrix_power_psd(a.to(cuda), 0.5)
+    w, v = torch.linalg.eigh(a + 1e-4 * torch.eye(96, dtype=torch.float64))
+    ref = v @ torch.diag_embed(w.sqrt()) @ v.transpose(1, 2)
+    assert rel_l2(out, ref) < 1e-10
+    res = torch.empty(3, device=cuda, dtype=torch.float64)
+    ws = torch.empty(_lib.load().rpst_matrix_power_workspace_size(96, 3), device=cuda,
+                     dtype=torch.uint8)
+    o2 = torch.empty_like(out)
+    _lib.call("rpst_matrix_power_psd_f64", a.to(cuda).data_ptr(), o2.data_ptr(), 96, 3, 1,
+              res.data_ptr(), ws.data_ptr(), ws.numel(), 0)
+    assert bool((res < ops.NS_TOL).all()), res
+
+
+@pytest.mark.parametrize("shape,pad", [((2, 256, 20, 72), 0), ((1, 64, 33, 70), 1),
+                                       ((2, 8, 9, 13), 0)])
+def test_conv2d_mix_vs_fp64(cuda, shape, pad):
+    """conv(pad(T_n x + c_n)): the F(4x4) fold (per-image weights W T_n, border-class
+    biases) and, for an 8-channel input, the materialised T x + c path."""
+    import torch.nn.functional as F
+    from rpst import _lib, ops
+    n, cin, h, w = shape
+    cout = 32
+    x = gen(31, shape, 2.0, 0.3, relu=True)
+    T = gen(32, (n, cin, cin), 0.2).double() + 3.0 * torch.eye(cin, dtype=torch.float64)
+    c = gen(33, (n, cin), 1.0).double()
+    wt = gen(34, (cout, cin, 3, 3), (2.0 / (cin * 9)) ** 0.5)
+    b = gen(35, (cout,), 0.05)
+    z = torch.einsum("nmk,nkhw->nmhw", T, x.double()) + c[:, :, None, None]
+    zp = F.pad(z, (1, 1, 1, 1), mode="reflect" if pad else "constant")
+    ref = F.relu(F.conv2d(zp, wt.double(), b.double()))
+    algo = _lib.load().rpst_conv2d_algorithm(cout, cin, h, w, 3, 0)
+    assert (algo == 2) == (cin >= 16)
+    out = ops.conv2d_mix(x.to(cuda), T.to(cuda), c.to(cuda), ops.pack_conv_weight(wt.to(cuda)),
+                         b.to(cuda), cout, 3, pad=pad, relu=True)
+    assert rel_l2(out, ref) < 1e-5, rel_l2(out, ref)
+
+
+def test_wct_params_match_whiten_and_color(cuda):
+    """T and c = mu_s - T mu_c from rpst_wct_params reproduce the oracle's fused feature,
+    with the row means computed inside or passed in (the encoder epilogue's)."""
+    from rpst import ops
+    c = gen(41, (2, 64, 24, 40), 2.0, 0.3, relu=True)
+    s = gen(42, (2, 64, 24, 40), 1.5, 0.5, relu=True)
+    ref = R.wct_fuse(c, s).double()
+    for means in (None, torch.cat([c.mean(dim=(2, 3)), s.mean(dim=(2, 3))]).to(cuda)):
+        T, off, res = ops.wct_params(c.to(cuda), s.to(cuda), means=means)
+        assert bool((res < ops.NS_TOL).all())
+        z = torch.einsum("nmk,nkp->nmp", T.cpu(), c.double().flatten(2)) + off.cpu()[:, :, None]
+        assert rel_l2(z.view_as(ref), ref) < 1e-6
+
+
+def test_wct_rp_fused_vs_unfused(cuda):
+    """WCTRPNet.test with the colour transform folded into the decoder's first conv equals
+    the materialised path (wct_fuse + decoder) to fp32 accumulation order."""
+    import network as net
+    import network.wct_rp as wrp
+    from rpst import synth
+    m = net.WCTRPNet(rp_config(16), copy.deepcopy(net.vgg))
+    synth_(m, 13)
+    m = m.to(cuda)
+    c = torch.from_numpy(synth.image(43, (2, 3, 64, 96))).to(cuda)
+    s = torch.from_numpy(synth.image(44, (2, 3, 64, 96))).to(cuda)
+    fused = m.test(c, s)
+    wrp.FUSED_WCT = False
+    try:
+        plain = m.test(c, s)
+    finally:
+        wrp.FUSED_WCT = True
+    assert rel_l2(fused, plain) < 1e-5, rel_l2(fused, plain)
+
+
 def test_sharded_model_bit_identical(cuda):
     """Per-image split over 2 replicas (both on cuda:0 here; one per GPU on a node) must
     reproduce the single-replica output bit for bit: every kernel is deterministic and

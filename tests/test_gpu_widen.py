@@ -13,8 +13,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from helpers import (SOURCE_CONFIG, TOL_NET, TOL_NET_MAXABS, max_abs_ratio, multiscale_config,
-                     rel_l2, state_dict_of, synth_)
+from helpers import (SOURCE_CONFIG, TOL_NET, TOL_NET_MAXABS, deeper_config, max_abs_ratio,
+                     multiscale_config, rel_l2, state_dict_of, synth_)
 from oracle import restate as R
 
 pytestmark = pytest.mark.gpu
@@ -111,6 +111,36 @@ def test_multiscale_vs_oracle_hidden32(cuda):
     s = torch.from_numpy(synth.image(32, (2, 3, 64, 96)))
     out = m.to(cuda).test(c.to(cuda), s.to(cuda))
     ref = R.multiscale_test(c, s, sd, 5)
+    assert rel_l2(out, ref) < TOL_NET and max_abs_ratio(out, ref) < TOL_NET_MAXABS
+
+
+def test_deeper_multiscale_golden(cuda, golden, conv_algo):
+    """enc_stack_way 'deeper' (adain_rp.py:152-156; config/rl/train_deeper_multiscale_rp_adain
+    .yaml: hidden 16, inception 3) against the reference's outputs."""
+    import network as net
+    g = golden("deeper")
+    for i in range(int(g["n"])):
+        cfg = deeper_config(int(g[f"hidden{i}"]), int(g[f"blocks{i}"]), int(g[f"inception{i}"]))
+        m = net.MultiScaleAdaINRPNet(cfg, copy.deepcopy(net.vgg))
+        np.testing.assert_allclose(synth_(m, int(g[f"seed{i}"])), g[f"checksum{i}"], rtol=1e-12)
+        out = m.to(cuda).test(t(g[f"content{i}"]).to(cuda), t(g[f"style{i}"]).to(cuda))
+        ref = g[f"out{i}"]
+        assert rel_l2(out, ref) < TOL_NET, (i, rel_l2(out, ref))
+        assert max_abs_ratio(out, ref) < TOL_NET_MAXABS
+
+
+def test_deeper_multiscale_vs_oracle_hidden16(cuda):
+    """The configured deeper stack (hidden 16 -> 256 channels, 3 inception convs per encoder
+    block) at 128x192 against the oracle."""
+    import network as net
+    from rpst import synth
+    m = net.MultiScaleAdaINRPNet(deeper_config(16, 5, 3), copy.deepcopy(net.vgg))
+    synth_(m, 12)
+    sd = state_dict_of(m)
+    c = torch.from_numpy(synth.image(51, (2, 3, 128, 192)))
+    s = torch.from_numpy(synth.image(52, (2, 3, 128, 192)))
+    out = m.to(cuda).test(c.to(cuda), s.to(cuda))
+    ref = R.multiscale_test(c, s, sd, 5, 3)
     assert rel_l2(out, ref) < TOL_NET and max_abs_ratio(out, ref) < TOL_NET_MAXABS
 
 

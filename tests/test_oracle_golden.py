@@ -13,7 +13,8 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import SOURCE_CONFIG, multiscale_config, rel_l2, rp_config, state_dict_of, synth_
+from helpers import (SOURCE_CONFIG, deeper_config, multiscale_config, rel_l2, rp_config,
+                     state_dict_of, synth_)
 from oracle import restate as R
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -144,6 +145,37 @@ def test_multiscale_test(golden):
         out = R.multiscale_test(t(g[f"content{i}"]), t(g[f"style{i}"]), state_dict_of(m),
                                 blocks, inc)
         assert rel_l2(out, g[f"out{i}"]) < 1e-6, (i, rel_l2(out, g[f"out{i}"]))
+
+
+def test_deeper_multiscale_test(golden):
+    """MultiScaleAdaINRPNet.test with enc_stack_way 'deeper' (adain_rp.py:152-156): deeper
+    encoder with 1x1 inception convs, shallower decoder, against the reference's outputs."""
+    import network as net
+    g = golden("deeper")
+    for i in range(int(g["n"])):
+        hid, blocks, inc = int(g[f"hidden{i}"]), int(g[f"blocks{i}"]), int(g[f"inception{i}"])
+        m = net.MultiScaleAdaINRPNet(deeper_config(hid, blocks, inc), copy.deepcopy(net.vgg))
+        np.testing.assert_allclose(synth_(m, int(g[f"seed{i}"])), g[f"checksum{i}"], rtol=1e-12)
+        out = R.multiscale_test(t(g[f"content{i}"]), t(g[f"style{i}"]), state_dict_of(m),
+                                blocks, inc)
+        assert rel_l2(out, g[f"out{i}"]) < 1e-6, (i, rel_l2(out, g[f"out{i}"]))
+
+
+def test_reference_training_gradients(golden):
+    """The oracle's autograd gradients (R.adain_rp_grads) against the reference's own
+    AdaINRPNet.forward + total_loss.backward() (adain_rp.py:110-138) gradients."""
+    g = golden("grads")
+    for i in range(int(g["n"])):
+        m = _adain_model(int(g[f"hidden{i}"]))
+        np.testing.assert_allclose(synth_(m, int(g[f"seed{i}"])), g[f"checksum{i}"], rtol=1e-12)
+        losses, grads = R.adain_rp_grads(t(g[f"content{i}"]), t(g[f"style{i}"]), state_dict_of(m),
+                                         5, float(g[f"cw{i}"]), float(g[f"sw{i}"]))
+        for k in ("style_loss", "content_loss", "total_loss"):
+            np.testing.assert_allclose(losses[k].numpy(), g[f"{k}{i}"], rtol=1e-5)
+        names = [str(n) for n in g[f"names{i}"]]
+        assert sorted(names) == sorted(grads)
+        for name in names:
+            assert rel_l2(grads[name], g[f"grad{i}:{name}"]) < 1e-5, (i, name)
 
 
 def test_sourcenet_test(golden):

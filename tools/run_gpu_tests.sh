@@ -1,5 +1,12 @@
-# GPU parity suite (optionally a subset: FILES="tests/x.py ..."), then optional extra command.
-set -e
-cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-timeout -k 10 ${TMO:-500} python -u -m pytest ${FILES:-tests} -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
+# GPU test suite (optionally a subset): python -m pytest -m gpu, one process, per-test timeout.
+# Usage: bash tools/run_gpu_tests.sh <tag> [pytest args...]
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${1:-tests}
+shift
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest ${@:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+rc=$?
+grep -E "PASSED|FAILED|ERROR|passed|failed" $O/tests.log | tail -25
+exit $rc
