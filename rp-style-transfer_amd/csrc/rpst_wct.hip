@@ -31,6 +31,9 @@
 
 namespace rpst {
 
+constexpr int kNSMaxIters = 64;
+constexpr double kNSTol = 1e-10;  // on ||I - Z Y||_F (||I||_F = sqrt(n)); quadratic from here
+
 enum { SRC_F64 = 0, SRC_F64C = 1, SRC_F32C = 2 };  // plain fp64 / centered fp64 / centered fp32
 enum { B_KN = 0, B_NK = 1 };
 enum { OUT_F64 = 0, OUT_PARTIAL = 1, OUT_F32_BIAS = 2, OUT_F64_BIAS = 3 };
@@ -55,9 +58,16 @@ struct G64Args {
   const void* B2;
   void* C2;
   int dual;
-  // Newton-Schulz early exit: batch entry b is skipped when state[b] >= skip_at
-  const int* state;
-  int skip_at;
+  // Newton-Schulz early exit (iteration `iter`): batch entry b is skipped once it converged
+  // in an earlier iteration (stop[b] < iter). With tile_sq set (the T = (3I - ZY)/2
+  // product), every block also reduces sum (T - I)^2 over its tile; the last block of a
+  // matrix to finish sums the tiles in fixed order: res[b] = 2 ||T - I||_F =
+  // ||I - Z Y||_F, and stop[b] = iter once res[b] < kNSTol.
+  int* stop;
+  int iter;
+  double* tile_sq;
+  int* tile_cnt;
+  double* res;
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -142,7 +152,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
     gB = g.B2;
     gC = g.C2;
   }
-  if (g.state && g.state[b] >= g.skip_at) return;  // converged matrix (block-uniform)
+  if (g.stop && g.stop[b] < g.iter) return;  // converged matrix (block-uniform)
   const int m0 = ti * BT, n0 = tj * BT;
   // split-K ranges are whole BK tiles
   const int kper = ((g.K + g.ksplit - 1) / g.ksplit + BK - 1) / BK * BK;
@@ -244,6 +254,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
 
   // epilogue: D col = lane&15, row = (lane>>4) + 4r
   const double alpha = g.alpha * (g.avec ? g.avec[b] : 1.0);
+  double sq = 0.0;  // Newton-Schulz residual: sum over this thread's outputs of (out - I)^2
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
 #pragma unroll
@@ -259,13 +270,42 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
         if (OUT == OUT_PARTIAL) {
           static_cast<double*>(gC)[(int64_t)z * g.sC + (int64_t)m * g.ldc + n] = v;
         } else if (OUT == OUT_F64) {
-          static_cast<double*>(gC)[b * g.sC + (int64_t)m * g.ldc + n] =
-              alpha * v + (m == n ? g.beta_diag : 0.0);
+          const double o = alpha * v + (m == n ? g.beta_diag : 0.0);
+          static_cast<double*>(gC)[b * g.sC + (int64_t)m * g.ldc + n] = o;
+          const double dv = o - (m == n ? 1.0 : 0.0);
+          sq = fma(dv, dv, sq);
         } else if (OUT == OUT_F32_BIAS) {
           static_cast<float*>(gC)[b * g.sC + (int64_t)m * g.ldc + n] = (float)(v + bias);
         } else {
           static_cast<double*>(gC)[b * g.sC + (int64_t)m * g.ldc + n] = v + bias;
         }
+      }
+    }
+  }
+  if (OUT == OUT_F64 && g.tile_sq) {
+    // block sum (fixed order), then the last block of matrix b reduces the tiles
+    // (MI355X_MICROARCH.md, inter-workgroup visibility: release fence + explicit vmcnt
+    // wait before the counter add, acquire fence before reading the other tiles' partials)
+    sq = wave_sum(sq);
+    __shared__ double red[4];
+    if (lane == 0) red[wave] = sq;
+    __syncthreads();
+    if (tid == 0) {
+      const int ntiles = (int)(gridDim.x * gridDim.y);
+      const int tile = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+      g.tile_sq[(int64_t)b * ntiles + tile] = (red[0] + red[1]) + (red[2] + red[3]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(g.tile_cnt + b, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      if (old == ntiles - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        double tot = 0.0;
+        for (int t = 0; t < ntiles; ++t) tot += g.tile_sq[(int64_t)b * ntiles + t];
+        const double r = 2.0 * sqrt(tot);
+        g.res[b] = r;
+        if (r < kNSTol) g.stop[b] = g.iter;
+        g.tile_cnt[b] = 0;  // the next iteration's launch starts from 0
       }
     }
   }
@@ -556,17 +596,20 @@ static int env_int(const char* name, int dflt);
 static void small_gemm(const double* A, const double* B, double* C, int n, int batch,
                        double alpha, double beta_diag, const double* avec, hipStream_t st,
                        const double* A2 = nullptr, const double* B2 = nullptr,
-                       double* C2 = nullptr, const int* state = nullptr, int skip_at = 0) {
+                       double* C2 = nullptr, const G64Args* ns = nullptr) {
   if (A2 && 2 * batch > 65535) {  // grid.z limit: two launches
-    small_gemm(A, B, C, n, batch, alpha, beta_diag, avec, st, nullptr, nullptr, nullptr, state,
-               skip_at);
-    small_gemm(A2, B2, C2, n, batch, alpha, beta_diag, avec, st, nullptr, nullptr, nullptr,
-               state, skip_at);
+    small_gemm(A, B, C, n, batch, alpha, beta_diag, avec, st, nullptr, nullptr, nullptr, ns);
+    small_gemm(A2, B2, C2, n, batch, alpha, beta_diag, avec, st, nullptr, nullptr, nullptr, ns);
     return;
   }
   G64Args g{};
-  g.state = state;
-  g.skip_at = skip_at;
+  if (ns) {  // Newton-Schulz early-exit / residual fields
+    g.stop = ns->stop;
+    g.iter = ns->iter;
+    g.tile_sq = ns->tile_sq;
+    g.tile_cnt = ns->tile_cnt;
+    g.res = ns->res;
+  }
   g.A = A;
   g.B = B;
   g.C = C;
@@ -596,55 +639,31 @@ static void small_gemm(const double* A, const double* B, double* C, int n, int b
   }
 }
 
-constexpr int kNSMaxIters = 64;
-constexpr double kNSTol = 1e-10;  // on ||I - Z Y||_F (||I||_F = sqrt(n)); quadratic from here
 
-// Newton-Schulz state per matrix: 0 running, 1 converged (this iteration's update still
-// applies), 2 done (skipped); last[b] = the last iteration whose update ran.
-// r_k = 2 ||T_k - I||_F of iteration k (one workgroup per matrix, fixed-order reduction).
-__global__ __launch_bounds__(256) void ns_residual_kernel(const double* __restrict__ T,
-                                                          int* __restrict__ state,
-                                                          int* __restrict__ last,
-                                                          double* __restrict__ res, int n,
-                                                          int it) {
-  const int b = blockIdx.x;
-  const int st = state[b];
-  if (st >= 1) {  // the update of iteration it - 1 was this matrix's last
-    if (threadIdx.x == 0 && st == 1) state[b] = 2;
-    return;
-  }
-  const double* t = T + (int64_t)b * n * n;
-  double s = 0.0;
-  for (int i = threadIdx.x; i < n * n; i += 256) {
-    const double v = t[i] - ((i / n) == (i % n) ? 1.0 : 0.0);
-    s += v * v;
-  }
-  s = wave_sum(s);
-  __shared__ double red[4];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const double r = 2.0 * sqrt((red[0] + red[1]) + (red[2] + red[3]));
-    res[b] = r;
-    last[b] = it;
-    if (r < kNSTol) state[b] = 1;
-  }
-}
-
-// out_b = buf[(last_b + 1) & 1]_b * s_b^p: the matrix's newest iterate (the ping-pong
-// buffers swap every iteration on the host, a converged matrix stops being updated)
+// out_b = buf[(last_b + 1) & 1]_b * s_b^p with last_b = min(stop_b, kNSMaxIters - 1): the
+// matrix's newest iterate (the ping-pong buffers swap every iteration on the host, a
+// converged matrix stops being updated after its iteration stop_b)
 __global__ void ns_final_kernel(const double* __restrict__ buf0, const double* __restrict__ buf1,
                                 double* __restrict__ out, const double* __restrict__ svec,
-                                const int* __restrict__ last, double p, int64_t per, int batch) {
+                                const int* __restrict__ stop, double p, int64_t per, int batch) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= per * batch) return;
   const int64_t b = i / per;
-  const double* src = ((last[b] + 1) & 1) ? buf1 : buf0;
+  const int last = min(stop[b], kNSMaxIters - 1);
+  const double* src = ((last + 1) & 1) ? buf1 : buf0;
   out[i] = src[i] * pow(svec[b], p);
 }
 
+__global__ void ns_state_init_kernel(int* stop, int* cnt, double* res, int batch) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  stop[b] = 1 << 30;
+  cnt[b] = 0;
+  res[b] = __longlong_as_double(0x7ff0000000000000LL);  // +inf until measured
+}
+
 // out = (A + add I)^p for p = +-1/2 (both if both outputs are given), batched n x n.
-// work: ns_work_doubles(n, batch); res: per-matrix final residual (may be null).
+// work: ns_work_doubles(n, batch); res_out: per-matrix final residual (may be null).
 static int ns_power(const double* A, double add, double* sqrt_out, double* isqrt_out, int n,
                     int batch, double* work, hipStream_t st, double* res_out = nullptr) {
   const int64_t nn = (int64_t)n * n * batch;
@@ -655,17 +674,24 @@ static int ns_power(const double* A, double add, double* sqrt_out, double* isqrt
   double* Z2 = Y2 + nn;
   double* svec = Z2 + nn;
   double* res = svec + batch;
-  int* state = reinterpret_cast<int*>(res + batch);
-  int* last = state + batch;
+  const int tiles = (n + 31) / 32;  // small_gemm's 32 x 32 tiles (RPST_WCT_NS_BT=64: 64)
+  double* tile_sq = res + batch;
+  int* stop = reinterpret_cast<int*>(tile_sq + (size_t)batch * tiles * tiles);
+  int* cnt = stop + batch;
   double* const buf0[2] = {Y, Z};
   double* const buf1[2] = {Y2, Z2};
-  hipMemsetAsync(state, 0, 2 * sizeof(int) * batch, st);  // state = 0, last = 0
+  ns_state_init_kernel<<<(batch + 255) / 256, 256, 0, st>>>(stop, cnt, res, batch);
   ns_init_kernel<<<batch, 256, 0, st>>>(A, Y, Z, svec, n, add);
+  G64Args ns{};
+  ns.stop = stop;
   for (int it = 0; it < kNSMaxIters; ++it) {
-    small_gemm(Z, Y, T, n, batch, -0.5, 1.5, nullptr, st, nullptr, nullptr, nullptr, state, 1);
-    ns_residual_kernel<<<batch, 256, 0, st>>>(T, state, last, res, n, it);
-    // Y <- Y T, Z <- T Z
-    small_gemm(Y, T, Y2, n, batch, 1.0, 0.0, nullptr, st, T, Z, Z2, state, 2);
+    ns.iter = it;
+    ns.tile_sq = tile_sq;
+    ns.tile_cnt = cnt;
+    ns.res = res;
+    small_gemm(Z, Y, T, n, batch, -0.5, 1.5, nullptr, st, nullptr, nullptr, nullptr, &ns);
+    ns.tile_sq = nullptr;  // Y <- Y T, Z <- T Z (skipped after the converging iteration)
+    small_gemm(Y, T, Y2, n, batch, 1.0, 0.0, nullptr, st, T, Z, Z2, &ns);
     double* t = Y;
     Y = Y2;
     Y2 = t;
@@ -674,19 +700,21 @@ static int ns_power(const double* A, double add, double* sqrt_out, double* isqrt
     Z2 = t;
   }
   const unsigned blocks = (unsigned)((nn + 255) / 256);
-  // iteration it wrote buffer set (it + 1) & 1 (set 0 = Y/Z, set 1 = Y2/Z2 of the start)
   if (sqrt_out)
-    ns_final_kernel<<<blocks, 256, 0, st>>>(buf0[0], buf1[0], sqrt_out, svec, last, 0.5,
+    ns_final_kernel<<<blocks, 256, 0, st>>>(buf0[0], buf1[0], sqrt_out, svec, stop, 0.5,
                                             (int64_t)n * n, batch);
   if (isqrt_out)
-    ns_final_kernel<<<blocks, 256, 0, st>>>(buf0[1], buf1[1], isqrt_out, svec, last, -0.5,
+    ns_final_kernel<<<blocks, 256, 0, st>>>(buf0[1], buf1[1], isqrt_out, svec, stop, -0.5,
                                             (int64_t)n * n, batch);
   if (res_out) hipMemcpyAsync(res_out, res, sizeof(double) * batch, hipMemcpyDeviceToDevice, st);
   return launch_status("newton-schulz");
 }
 
 static size_t ns_work_doubles(int n, int batch) {
-  return 5 * (size_t)n * n * batch + 2 * (size_t)batch + (size_t)batch;  // + svec, res, state/last
+  const size_t tiles = (size_t)(n + 31) / 32;
+  // Y Z T Y2 Z2, svec, res, per-tile residual partials, stop + counter (ints)
+  return 5 * (size_t)n * n * batch + 2 * (size_t)batch + (size_t)batch * tiles * tiles +
+         (size_t)batch;
 }
 
 static int env_int(const char* name, int dflt) {

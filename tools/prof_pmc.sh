@@ -1,9 +1,9 @@
-# Round-2 measurement pass: GPU kernel tests of the changed conv paths, the default bench,
+# Measurement pass: GPU kernel tests of the changed conv paths, the default bench,
 # per-dispatch PMC traffic (FETCH / WRITE in separate passes) attributed per layer, and two
-# SQ counter passes on one bench step, attributed per layer. Usage: bash tools/prof_r02.sh <tag>
+# SQ counter passes on one bench step, attributed per layer. Usage: bash tools/prof_pmc.sh <tag> (SKIP_TESTS=1 skips the kernel tests)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-T=${1:-r02}
+T=${1:-pmc}
 O=$R/gpurun_out/$T
 mkdir -p $O
 cd $R

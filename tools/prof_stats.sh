@@ -1,4 +1,4 @@
-# rocprofv3 kernel-trace + stats summaries of the three bench workloads (short runs).
+# rocprofv3 kernel-trace + stats summaries of bench workloads (short runs): MODELS="adain wct sanet".
 set -e
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out

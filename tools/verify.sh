@@ -1,0 +1,23 @@
+# End-of-round verification on one MI355X: the whole GPU test suite, smoke(), every bench
+# line (default = BASELINE configs[1], then configs[2]-[4] and the SURVEY 8(f) workloads) and
+# rocprofv3 kernel summaries of the default and WCT benches. Usage: bash tools/verify.sh <tag>
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${1:-verify}
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+tail -2 $O/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
+timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail $O/bench_default.err; exit 1; }
+cat $O/bench_default.json
+for m in ${RUNS:-"--config 2" "--config 3" "--config 4" "--model multiscale" "--model source" "--model adaptive" "--model train"}; do
+  f=$O/bench_$(echo $m | tr -d ' -').json
+  timeout -k 10 400 python bench.py $m --no-cpu-baseline > $f 2> $f.err || { tail $f.err; exit 1; }
+  python -c "import json;d=json.load(open('$f'));r=d['roofline'];print('$m', d['value'], d['ms_per_step'], r['kernel'], r['frac'])"
+done
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_adain -o adain -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_adain.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_wct -o wct -- python3 $R/bench.py --config 2 --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_wct.log 2>&1 || exit 1
+echo done
