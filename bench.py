@@ -50,9 +50,12 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (matrix = vector rate), MI355X_MI
 PEAK_FP64_TFLOPS = 78.6    # MI355X dense FP64 matrix (vendor spec)
 PEAK_HBM_GBS = 8000.0      # HBM3E 8 TB/s
 
-# BASELINE.json configs[i] -> (model, image side, per-GPU batch or None, global batch, gather)
-CONFIGS = {1: ("adain", 512, 32, None, False), 2: ("wct", 512, 16, None, False),
-           3: ("sanet", 512, 32, None, False), 4: ("adain", 1024, None, 128, True)}
+# BASELINE.json configs[i] -> (model, image side, per-GPU batch or None, global batch, gather,
+# micro-batch). configs[4] is 128 images at 1024^2 "sharded across 8 GPUs": 16 per GPU, so
+# a rank holding more than 16 (fewer GPUs) runs them 16 at a time (the per-GPU working set
+# of the 8-GPU split; 128 at once would need ~270 GB for the 256-channel encoder output)
+CONFIGS = {1: ("adain", 512, 32, None, False, None), 2: ("wct", 512, 16, None, False, None),
+           3: ("sanet", 512, 32, None, False, None), 4: ("adain", 1024, None, 128, True, 16)}
 
 
 def build_model(kind, dev):
@@ -129,7 +132,7 @@ def cpu_info():
 
 def cpu_baseline(kind, size, reps=3):
     """Time the CPU oracle on a bounded sample: B=2 content/style pairs at size^2 (B=1 for
-    WCT and training), one warm-up then the median of `reps` runs."""
+    WCT, training and 1024^2), one warm-up then the median of `reps` runs."""
     import torch
     from oracle import restate as R
     from rpst import synth
@@ -159,7 +162,7 @@ def cpu_baseline(kind, size, reps=3):
     synth.synth_module_(m, 0)
     # (.cpu(): SourceNet shares the module-level decoder, which build_model moved to the GPU)
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
-    b = CPU_SAMPLE_BATCH.get(kind, 2)
+    b = CPU_SAMPLE_BATCH.get(kind, 2) if size <= 512 else 1  # 1024^2: ~6 s per image
     c = torch.from_numpy(synth.image(11, (b, 3, size, size)))
     s = torch.from_numpy(synth.image(12, (b, 3, size, size)))
     threads = torch.get_num_threads()
@@ -327,8 +330,9 @@ class HostGather:
             self.pinned = int(rc) == 0
         self.cudart = torch.cuda.cudart() if self.pinned else None
 
-    def put(self, out):
-        self.slice.copy_(out, non_blocking=self.pinned)
+    def put(self, out, at=0):
+        """Copy `out` into this rank's images [at, at + len(out)) (stream-ordered)."""
+        self.slice[at:at + out.shape[0]].copy_(out, non_blocking=self.pinned)
 
     def close(self):
         if self.pinned:
@@ -365,14 +369,17 @@ def main():
     ap.add_argument("--size", type=int, default=None)
     ap.add_argument("--gather", action="store_true",
                     help="copy each step's output into a shared host buffer (timed)")
+    ap.add_argument("--micro-batch", type=int, default=None,
+                    help="images per test() call within a step (default: the whole batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--layer-order", default=None,
                     help="write the traced launch names of one step (tools/pmc_traffic.py)")
     args = ap.parse_args()
 
-    model_kind, size, batch, gbatch, gather = CONFIGS[args.config or 1]
+    model_kind, size, batch, gbatch, gather, micro = CONFIGS[args.config or 1]
     if args.config is None:
-        model_kind, size, batch, gbatch, gather = "adain", 512, None, None, False
+        model_kind, size, batch, gbatch, gather, micro = "adain", 512, None, None, False, None
+    micro = args.micro_batch or micro
     model_kind = args.model or model_kind
     size = args.size or size
     gbatch = args.global_batch if args.global_batch is not None else gbatch
@@ -430,19 +437,33 @@ def main():
                 reduce_grads()
             optimizer.step()
             return tot
-    else:
-        def step():
-            return model.test(content, style)
-
     host = None
     if gather:
         tag = f"{os.environ.get('MASTER_PORT', 'solo')}_{os.getppid() if world > 1 else os.getpid()}"
         host = HostGather(tag, (total, 3, size, size), start, end, rank, cuda)
+    mb = micro if micro and micro < B else B
+    # the D2H gather of chunk i runs on a copy stream while chunk i + 1 computes
+    copy_stream = torch.cuda.Stream(dev) if (cuda and host is not None) else None
+
+    if model_kind != "train":
+        def step():
+            out = None
+            for s0 in range(0, B, mb):
+                out = model.test(content[s0:s0 + mb], style[s0:s0 + mb])
+                if host is not None:
+                    if copy_stream is None:
+                        host.put(out, s0)
+                        continue
+                    done = torch.cuda.Event()
+                    done.record()
+                    with torch.cuda.stream(copy_stream):
+                        copy_stream.wait_event(done)
+                        host.put(out, s0)
+                        out.record_stream(copy_stream)
+            return out
 
     for _ in range(args.warmup):
         out = step()
-        if host is not None:
-            host.put(out)
     sync()
 
     ops.TRACE = ops.Trace() if cuda else None
@@ -452,8 +473,6 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = step()
-        if host is not None:
-            host.put(out)
     sync()
     dt_rank = time.perf_counter() - t0
     if world > 1:
@@ -466,7 +485,9 @@ def main():
         order = {"steps": args.steps, "warmup": args.warmup,
                  "per_step": names[:len(names) // max(args.steps, 1)]}
     ops.TRACE = None
-    assert torch.isfinite(out).all() and (model_kind == "train" or out.shape == shape)
+    last_chunk = B - mb * ((B - 1) // mb)
+    assert torch.isfinite(out).all() and (model_kind == "train" or
+                                          out.shape == (last_chunk,) + shape[1:])
 
     per_rank = [dt_rank]
     if world > 1:
@@ -502,7 +523,8 @@ def main():
                        "parallelism": (f"data parallel over {world} GPU(s), one gradient "
                                        "all-reduce per step") if model_kind == "train" else
                        f"per-image batch split over {world} GPU(s), no collectives",
-                       "host_gather": bool(host is not None)},
+                       "host_gather": bool(host is not None),
+                       "micro_batch": mb},
             "per_rank_s": [round(v, 4) for v in per_rank],
         }
         if host is not None:
@@ -519,7 +541,7 @@ def main():
                 order["stats_name"] = next((k for k in adain_summary if k.startswith("stats")), None)
                 json.dump(order, open(args.layer_order, "w"), indent=1)
             if world == 1 and not args.no_cpu_baseline:
-                rec["cpu_baseline"] = cpu_baseline(model_kind, min(size, 512))
+                rec["cpu_baseline"] = cpu_baseline(model_kind, size)
             else:
                 rec["cpu_baseline"] = None
             kernels = sorted(summary.items(), key=lambda kv: -kv[1]["ms"])[:12]

@@ -36,10 +36,12 @@ def test_single_process_line():
     assert rec["value"] > 0 and len(rec["per_rank_s"]) == 1
 
 
-@pytest.mark.parametrize("gpus,gbatch", [(2, 7), (3, 6)])
-def test_launcher_strong_split_with_host_gather(gpus, gbatch):
+@pytest.mark.parametrize("gpus,gbatch,micro", [(2, 7, None), (3, 6, None), (2, 9, 2)])
+def test_launcher_strong_split_with_host_gather(gpus, gbatch, micro):
+    extra = ("--micro-batch", str(micro)) if micro else ()
     rec = _bench("--gpus", str(gpus), "--global-batch", str(gbatch), "--gather",
-                 "--steps", "2", "--warmup", "1", "--size", "8")
+                 "--steps", "2", "--warmup", "1", "--size", "8", *extra)
+    assert rec["config"]["micro_batch"] == (micro or (gbatch + gpus - 1) // gpus)
     assert rec["n_gpus"] == gpus and rec["scaling"] == "strong"
     assert rec["config"]["global_batch"] == gbatch
     assert len(rec["per_rank_s"]) == gpus and all(t > 0 for t in rec["per_rank_s"])
