@@ -75,6 +75,8 @@ def build_model(kind, dev):
         m = net.AdaptiveSAModel(ADAPTIVE_CONFIG, copy.deepcopy(net.vgg), 0, 512)
     elif kind == "train":
         m = net.AdaINRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
+    elif kind == "train_wct":
+        m = net.WCTRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, 512)
     synth.synth_module_(m, 0)
@@ -105,12 +107,15 @@ WORKLOADS = {
     "train": "AdaINRPNet training iteration: forward() losses + total_loss.backward() + Adam "
              "step, rp_blocks=5 hidden_dim=16 (SURVEY 8(f) rank 2; gradients all-reduced "
              "over ranks)",
+    "train_wct": "WCTRPNet training iteration: forward() losses + total_loss.backward() + Adam "
+                 "step (RP decoder; fuse() detaches the encoder features), rp_blocks=5 "
+                 "hidden_dim=16 (SURVEY 8(f) rank 2)",
     "selftest": "CPU stand-in per-image function (launcher / timing / gather test only)",
 }
 DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32, "multiscale": 32, "source": 32,
-                 "adaptive": 32, "train": 8, "selftest": 4}
+                 "adaptive": 32, "train": 8, "train_wct": 8, "selftest": 4}
 # CPU-baseline sample per workload (BASELINE.md plan: B=2 at 512^2, B=1 for WCT)
-CPU_SAMPLE_BATCH = {"wct": 1, "train": 1}
+CPU_SAMPLE_BATCH = {"wct": 1, "train": 1, "train_wct": 1}
 
 
 def cpu_info():
@@ -156,6 +161,9 @@ def cpu_baseline(kind, size, reps=3):
     elif kind == "train":
         m = net.AdaINRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
         fn = lambda c, s, sd: R.adain_rp_grads(c, s, sd, 5, 1.0, 1.0)  # noqa: E731
+    elif kind == "train_wct":
+        m = net.WCTRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
+        fn = lambda c, s, sd: R.wct_rp_grads(c, s, sd, 5, 1.0, 1.0)  # noqa: E731
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, size)
         fn = R.samodel_test
@@ -423,9 +431,10 @@ def main():
     content = torch.from_numpy(synth.image_range(1000, (total, 3, size, size), start, end)).to(dev)
     style = torch.from_numpy(synth.image_range(2000, (total, 3, size, size), start, end)).to(dev)
 
-    if model_kind == "train":
+    if model_kind in ("train", "train_wct"):
         from rpst.shard import GradientAllReduce
-        params = [p for p in model.parameters() if p.requires_grad]
+        trained = model.rp_decoder if model_kind == "train_wct" else model
+        params = [p for p in trained.parameters() if p.requires_grad]
         optimizer = torch.optim.Adam(params, lr=1e-4)
         reduce_grads = GradientAllReduce(params) if world > 1 else None
 
@@ -445,7 +454,7 @@ def main():
     # the D2H gather of chunk i runs on a copy stream while chunk i + 1 computes
     copy_stream = torch.cuda.Stream(dev) if (cuda and host is not None) else None
 
-    if model_kind != "train":
+    if model_kind not in ("train", "train_wct"):
         def step():
             out = None
             for s0 in range(0, B, mb):
@@ -486,7 +495,7 @@ def main():
                  "per_step": names[:len(names) // max(args.steps, 1)]}
     ops.TRACE = None
     last_chunk = B - mb * ((B - 1) // mb)
-    assert torch.isfinite(out).all() and (model_kind == "train" or
+    assert torch.isfinite(out).all() and (model_kind.startswith("train") or
                                           out.shape == (last_chunk,) + shape[1:])
 
     per_rank = [dt_rank]
@@ -521,7 +530,7 @@ def main():
                        "global_batch": total, "image": f"{size}x{size}",
                        "baseline_config": args.config,
                        "parallelism": (f"data parallel over {world} GPU(s), one gradient "
-                                       "all-reduce per step") if model_kind == "train" else
+                                       "all-reduce per step") if model_kind.startswith("train") else
                        f"per-image batch split over {world} GPU(s), no collectives",
                        "host_gather": bool(host is not None),
                        "micro_batch": mb},

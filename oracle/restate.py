@@ -267,6 +267,36 @@ def wct_rp_test(content, style, sd, rp_blocks):
         return rp_stack(wct_fuse(cf, sf), sd, "rp_decoder.", rp_blocks)
 
 
+def wct_rp_losses(content, style, sd, rp_blocks, content_weight, style_weight):
+    """WCTRPNet.forward loss dict (wct_rp.py:168-194). fuse() detaches the encoder features
+    (wct_rp.py:161-162), so only the RP decoder receives gradients."""
+    with torch.no_grad():
+        cf = rp_stack(content, sd, "rp_shared_encoder.", rp_blocks)
+        sf = rp_stack(style, sd, "rp_shared_encoder.", rp_blocks)
+        t = wct_fuse(cf, sf)
+    stylized = rp_stack(t, sd, "rp_decoder.", rp_blocks)
+    ds = encode_with_intermediate(stylized, sd)
+    dt = encode_with_intermediate(style, sd)
+    dc = encode_with_intermediate(content, sd)
+    ls = style_loss(ds[0], dt[0])
+    for i in range(1, 4):
+        ls = ls + style_loss(ds[i], dt[i])
+    lc = F.mse_loss(ds[-1], dc[-1])
+    tot = content_weight * lc + style_weight * ls
+    return {"style_loss": ls, "content_loss": lc, "total_loss": tot}
+
+
+def wct_rp_grads(content, style, sd, rp_blocks, content_weight, style_weight):
+    """(loss dict, {name: d total_loss / d param}) for the RP decoder parameters."""
+    sd = {k: (v.detach().clone().requires_grad_(k.startswith("rp_decoder."))
+              if v.is_floating_point() else v) for k, v in sd.items()}
+    with torch.enable_grad():
+        losses = wct_rp_losses(content, style, sd, rp_blocks, content_weight, style_weight)
+        names = [k for k, v in sd.items() if v.requires_grad]
+        grads = torch.autograd.grad(losses["total_loss"], [sd[k] for k in names])
+    return ({k: v.detach() for k, v in losses.items()}, dict(zip(names, grads)))
+
+
 # ---- a10-a13: SANet ---------------------------------------------------------------
 def sanet(content: Tensor, style: Tensor, sd: SD, prefix: str) -> Tensor:
     """SANet.forward (sanet.py:82-99): softmax(F^T G) over keys, no 1/sqrt(d) scale."""

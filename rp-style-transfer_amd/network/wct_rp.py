@@ -126,7 +126,14 @@ class WCTRPNet(BaseNet):
         return ops.wct_fuse(content_feats, style_feats)
 
     def forward(self, content, style, alpha=1.0):
+        """Loss dict of wct_rp.py:168-194. With autograd enabled and a trainable decoder
+        the losses come from rpst.autograd (fuse() detaches the encoder features, so the
+        RP decoder is what total_loss.backward() trains); under no_grad op by op."""
         assert 0 <= alpha <= 1
+        if type(self) is WCTRPNet and torch.is_grad_enabled() and any(
+                p.requires_grad for p in self.rp_decoder.parameters()):
+            from rpst.autograd import wct_rp_losses
+            return wct_rp_losses(self, content, style)
         content_feat, style_feat = encode_both(self.rp_shared_encoder, content, style)
         stylized = self.rp_decoder(self.fuse(content_feat, style_feat))
         down_stylized_feats = self.encode_with_intermediate(stylized)

@@ -1,4 +1,4 @@
-"""Training step of AdaINRPNet on the MI355X kernels.
+"""Training steps of AdaINRPNet and WCTRPNet on the MI355X kernels.
 
 AdaINRPNet.forward (network/adain_rp.py:110-138) returns the loss dict and total_loss;
 train.py:186-189 then calls total_loss.backward() and optimizer.step(). Here the whole
@@ -140,6 +140,74 @@ def _rp_backward(steps, saved, g, grads: Dict[int, torch.Tensor], need_input_gra
     return g
 
 
+class _VGGLoss:
+    """calc_style_loss on relu1_1..relu4_1 + calc_content_loss on relu4_1 of a stylized
+    batch (adain_rp.py:120-138, wct_rp.py:176-194) against the VGG features of the style
+    and content batches: forward keeps what the backward needs, backward returns
+    d total / d stylized through the frozen VGG."""
+
+    def __init__(self, model, stylized, content, style, cw, sw):
+        n = stylized.shape[0]
+        vgg_steps, vgg_saved, taps, x = [], [], [], stylized
+        for i in range(4):
+            st = plan.compile_layers(getattr(model, f"enc_{i + 1}").children())
+            x, sv = _run_steps_saving(st, x)
+            vgg_steps += st
+            vgg_saved += sv
+            taps.append(len(vgg_steps) - 1)
+        ref = torch.cat([style, content], dim=0)
+        targets = []
+        for i in range(4):
+            ref = getattr(model, f"enc_{i + 1}")(ref)
+            targets.append(ref)
+        stats, loss_s = [], []
+        for i, k in enumerate(taps):
+            F = vgg_saved[k][1]
+            mu, sd = ops.calc_mean_std(F)
+            mut, sdt = ops.calc_mean_std(targets[i][:n])
+            stats.append(torch.cat([mu.reshape(-1), sd.reshape(-1), mut.reshape(-1),
+                                    sdt.reshape(-1)]))
+            loss_s.append(sq_diff_mean(mu, mut) + sq_diff_mean(sd, sdt))
+        self.ls = loss_s[0] + loss_s[1] + loss_s[2] + loss_s[3]
+        self.content4 = targets[3][n:].contiguous()
+        self.lc = sq_diff_mean(vgg_saved[taps[3]][1], self.content4)
+        self.total = cw * self.lc + sw * self.ls
+        self.cw, self.sw = cw, sw
+        self.steps, self.saved, self.taps, self.stats = vgg_steps, vgg_saved, taps, stats
+
+    def backward(self, g_total, g_ls, g_lc) -> torch.Tensor:
+        dev = self.content4.device
+        zero = torch.zeros((), device=dev)
+        g_total = zero if g_total is None else g_total
+        w_s = g_total * self.sw + (zero if g_ls is None else g_ls)
+        w_c = g_total * self.cw + (zero if g_lc is None else g_lc)
+        wts = torch.stack([w_s, w_c]).to(torch.float32).contiguous()
+        vs, vsv, taps = self.steps, self.saved, self.taps
+        g = None
+        for k in range(len(vs) - 1, -1, -1):
+            x_in, y = vsv[k]
+            if k in taps:
+                i = taps.index(k)
+                planes = y.shape[0] * y.shape[1]
+                hw = y.shape[2] * y.shape[3]
+                if g is None:
+                    g = torch.empty_like(y)
+                acc = int(i != 3)
+                _lib.call("rpst_style_content_loss_grad", y.data_ptr(),
+                          self.content4.data_ptr() if i == 3 else None, self.stats[i].data_ptr(),
+                          wts.data_ptr(), g.data_ptr(), planes, hw, acc, _stream(y))
+            s = vs[k]
+            if s.relu:
+                g = relu_backward(g, y)
+            g = conv_dgrad(g, s)
+            if s.in_op == ops.IN_MAXPOOL2:
+                g = maxpool_backward(x_in, g, relu_mask=False)
+            elif s.in_op != ops.IN_NONE:
+                raise NotImplementedError("rpst autograd: VGG input operator")
+        self.saved = None
+        return g
+
+
 class _AdaINRPStep(torch.autograd.Function):
     @staticmethod
     def forward(ctx, content, style, model, cw, sw, *params):
@@ -162,72 +230,19 @@ class _AdaINRPStep(torch.autograd.Function):
         ms, ss = ops.calc_mean_std(sf)
         t = ops.adaptive_instance_normalization(cf, sf)
         stylized, dec_saved = _run_steps_saving(dec_steps, t)
-        # VGG relu1_1..relu4_1 of the stylized batch (kept) and of [style; content]
-        vgg_steps, vgg_saved, taps, x = [], [], [], stylized
-        for i in range(4):
-            st = plan.compile_layers(getattr(model, f"enc_{i + 1}").children())
-            x, sv = _run_steps_saving(st, x)
-            vgg_steps += st
-            vgg_saved += sv
-            taps.append(len(vgg_steps) - 1)
-        ref = torch.cat([style, content], dim=0)
-        targets = []
-        for i in range(4):
-            ref = getattr(model, f"enc_{i + 1}")(ref)
-            targets.append(ref)
-        # losses (calc_style_loss on the four taps, calc_content_loss on relu4_1)
-        stats, loss_s = [], []
-        for i, k in enumerate(taps):
-            F = vgg_saved[k][1]
-            mu, sd = ops.calc_mean_std(F)
-            mut, sdt = ops.calc_mean_std(targets[i][:n])
-            stats.append(torch.cat([mu.reshape(-1), sd.reshape(-1), mut.reshape(-1),
-                                    sdt.reshape(-1)]))
-            loss_s.append(sq_diff_mean(mu, mut) + sq_diff_mean(sd, sdt))
-        ls = loss_s[0] + loss_s[1] + loss_s[2] + loss_s[3]
-        content4 = targets[3][n:].contiguous()
-        lc = sq_diff_mean(vgg_saved[taps[3]][1], content4)
-        total = cw * lc + sw * ls
-        ctx.model, ctx.cw, ctx.sw, ctx.n = model, cw, sw, n
-        ctx.enc_steps, ctx.dec_steps, ctx.vgg_steps = enc_steps, dec_steps, vgg_steps
-        ctx.enc_saved, ctx.dec_saved, ctx.vgg_saved = enc_saved, dec_saved, vgg_saved
-        ctx.taps, ctx.stats, ctx.content4 = taps, stats, content4
+        loss = _VGGLoss(model, stylized, content, style, cw, sw)
+        ctx.loss, ctx.n = loss, n
+        ctx.enc_steps, ctx.dec_steps = enc_steps, dec_steps
+        ctx.enc_saved, ctx.dec_saved = enc_saved, dec_saved
         ctx.adain = (cf, sf, torch.cat([mc.reshape(-1), sc.reshape(-1), ms.reshape(-1),
                                         ss.reshape(-1)]))
         ctx.params = params
-        return total, ls, lc
+        return loss.total, loss.ls, loss.lc
 
     @staticmethod
     def _backward(ctx, g_total, g_ls, g_lc):
-        dev = ctx.content4.device
-        zero = torch.zeros((), device=dev)
-        g_total = zero if g_total is None else g_total
-        w_s = g_total * ctx.sw + (zero if g_ls is None else g_ls)
-        w_c = g_total * ctx.cw + (zero if g_lc is None else g_lc)
-        wts = torch.stack([w_s, w_c]).to(torch.float32).contiguous()
         # ---- VGG (frozen): loss seeds at the taps, back to d stylized
-        vs, vsv, taps = ctx.vgg_steps, ctx.vgg_saved, ctx.taps
-        g = None
-        for k in range(len(vs) - 1, -1, -1):
-            x_in, y = vsv[k]
-            if k in taps:
-                i = taps.index(k)
-                planes = y.shape[0] * y.shape[1]
-                hw = y.shape[2] * y.shape[3]
-                if g is None:
-                    g = torch.empty_like(y)
-                acc = int(i != 3)
-                _lib.call("rpst_style_content_loss_grad", y.data_ptr(),
-                          ctx.content4.data_ptr() if i == 3 else None, ctx.stats[i].data_ptr(),
-                          wts.data_ptr(), g.data_ptr(), planes, hw, acc, _stream(y))
-            s = vs[k]
-            if s.relu:
-                g = relu_backward(g, y)
-            g = conv_dgrad(g, s)
-            if s.in_op == ops.IN_MAXPOOL2:
-                g = maxpool_backward(x_in, g, relu_mask=False)
-            elif s.in_op != ops.IN_NONE:
-                raise NotImplementedError("rpst autograd: VGG input operator")
+        g = ctx.loss.backward(g_total, g_ls, g_lc)
         # ---- RP decoder and AdaIN
         grads: Dict[int, torch.Tensor] = {}
         g = _rp_backward(ctx.dec_steps, ctx.dec_saved, g, grads, need_input_grad=True)
@@ -235,7 +250,7 @@ class _AdaINRPStep(torch.autograd.Function):
         dc, ds = torch.empty_like(cf), torch.empty_like(sf)
         planes = cf.shape[0] * cf.shape[1]
         hw = cf.shape[2] * cf.shape[3]
-        ws = torch.empty(2 * planes, device=dev, dtype=torch.float32)
+        ws = torch.empty(2 * planes, device=g.device, dtype=torch.float32)
         _lib.call("rpst_adain_backward", g.data_ptr(), cf.data_ptr(), sf.data_ptr(), st.data_ptr(),
                   dc.data_ptr(), ds.data_ptr(), planes, hw, ws.data_ptr(), ws.numel() * 4,
                   _stream(g))
@@ -243,8 +258,38 @@ class _AdaINRPStep(torch.autograd.Function):
         _rp_backward(ctx.enc_steps, ctx.enc_saved, torch.cat([dc, ds], dim=0), grads,
                      need_input_grad=False)
         out = [grads.get(id(p)) for p in ctx.params]
-        ctx.enc_saved = ctx.dec_saved = ctx.vgg_saved = None
+        ctx.enc_saved = ctx.dec_saved = None
         return (None, None, None, None, None, *out)
+
+
+class _WCTRPStep(torch.autograd.Function):
+    """WCTRPNet.forward (wct_rp.py:168-194): fuse() detaches the encoder features
+    (wct_rp.py:161-162), so the WCT feature is a constant of the step and only the RP
+    decoder is trained: forward = encoder + fp64 WCT without grad (the inference
+    kernels), decoder with kept activations, VGG losses; backward = VGG dgrad, decoder
+    wgrad / dgrad."""
+
+    @staticmethod
+    def forward(ctx, content, style, model, cw, sw, *params):
+        with ops.precise_convs():
+            n = content.shape[0]
+            feats = plan.run(plan.compile_layers(model.rp_shared_encoder.children()),
+                             torch.cat([content, style], dim=0))
+            t = ops.wct_fuse(feats[:n], feats[n:])
+            dec_steps = plan.compile_layers(model.rp_decoder.children())
+            stylized, dec_saved = _run_steps_saving(dec_steps, t)
+            loss = _VGGLoss(model, stylized, content, style, cw, sw)
+        ctx.loss, ctx.dec_steps, ctx.dec_saved, ctx.params = loss, dec_steps, dec_saved, params
+        return loss.total, loss.ls, loss.lc
+
+    @staticmethod
+    def backward(ctx, g_total, g_ls, g_lc):
+        with ops.precise_convs():
+            g = ctx.loss.backward(g_total, g_ls, g_lc)
+            grads: Dict[int, torch.Tensor] = {}
+            _rp_backward(ctx.dec_steps, ctx.dec_saved, g, grads, need_input_grad=False)
+        ctx.dec_saved = None
+        return (None, None, None, None, None, *[grads.get(id(p)) for p in ctx.params])
 
 
 def adain_rp_losses(model, content: torch.Tensor, style: torch.Tensor
@@ -258,4 +303,17 @@ def adain_rp_losses(model, content: torch.Tensor, style: torch.Tensor
     sw = float(model.config['style_weight'])
     total, ls, lc = _AdaINRPStep.apply(content.detach().contiguous(),
                                        style.detach().contiguous(), model, cw, sw, *params)
+    return {'style_loss': ls, 'content_loss': lc, 'total_loss': total}, total
+
+
+def wct_rp_losses(model, content: torch.Tensor, style: torch.Tensor
+                  ) -> Tuple[Dict[str, torch.Tensor], torch.Tensor]:
+    """WCTRPNet.forward with autograd: the loss dict and total_loss, differentiable w.r.t.
+    the RP decoder parameters (the only ones the reference's graph reaches)."""
+    ops._check(content, style)
+    params: List[torch.Tensor] = list(model.rp_decoder.parameters())
+    cw = float(model.config['content_weight'])
+    sw = float(model.config['style_weight'])
+    total, ls, lc = _WCTRPStep.apply(content.detach().contiguous(), style.detach().contiguous(),
+                                     model, cw, sw, *params)
     return {'style_loss': ls, 'content_loss': lc, 'total_loss': total}, total

@@ -18,7 +18,9 @@ WORLD_SIZE > 1 every rank draws its own batches and the gradients are averaged b
 all-reduce of a flat buffer per step (rpst.shard.GradientAllReduce; RCCL over xGMI).
 Scalars go to <output>/logs/train.jsonl (tensorboardX is not available offline); the
 reference's per-iteration try/except that swallows errors is not reproduced.
-Only network 'adain' (AdaINRPNet) has backward kernels; the others raise.
+Networks with backward kernels: 'adain' (AdaINRPNet: RP encoder + decoder) and 'wct'
+(WCTRPNet: RP decoder; its fuse() detaches the encoder features, wct_rp.py:161-162); the
+others raise.
 """
 from __future__ import annotations
 
@@ -38,6 +40,8 @@ if HERE not in sys.path:
 logging.basicConfig(level=logging.INFO,
                     format="%(asctime)s - %(name)s - %(levelname)s - %(message)s")
 logger = logging.getLogger("train")
+
+TRAINABLE = {"adain", "wct"}  # networks with backward kernels (rpst.autograd)
 
 
 def adjust_learning_rate(opt, optimizer, iteration_count):
@@ -127,9 +131,9 @@ def main(argv=None) -> int:
     args = ap.parse_args(argv)
     with open(args.config) as f:
         opt = yaml.safe_load(f)
-    if opt["network"] != "adain":
+    if opt["network"] not in TRAINABLE:
         raise NotImplementedError(f"training network '{opt['network']}': backward kernels "
-                                  "exist for 'adain' (AdaINRPNet) only (DESIGN.md §7)")
+                                  f"exist for {sorted(TRAINABLE)} only (DESIGN.md §7)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -170,7 +174,7 @@ def main(argv=None) -> int:
         optimizer.step()
         if rank != 0:
             continue
-        scalars = {k: float(v) for k, v in loss_dict.items()}
+        scalars = {k: float(v.detach()) for k, v in loss_dict.items()}
         elapsed = round(time.time() - start, 2)
         log.write(json.dumps({"iteration": network.begin + i, "elapsed": elapsed,
                               **scalars}) + "\n")

@@ -388,6 +388,35 @@ def gen_grads(net):
     np.savez_compressed(os.path.join(HERE, "grads.npz"), n=len(cases), **out)
 
 
+def gen_grads_wct(net):
+    """Reference WCTRPNet.forward + total_loss.backward() (wct_rp.py:168-194): fuse()
+    detaches the encoder features, so only RP decoder gradients exist."""
+    out = {}
+    cases = [(4, (2, 3, 32, 32), 26, 1.0, 1.0), (8, (1, 3, 48, 40), 27, 1.0, 10.0)]
+    for i, (hid, shp, seed, cw, sw) in enumerate(cases):
+        cfg = rp_config(hid)
+        cfg.update(content_weight=cw, style_weight=sw)
+        m = net.WCTRPNet(cfg, copy.deepcopy(net.vgg))
+        ck = synth_model_(m, seed)
+        c = synth.image(3300 + i, shp)
+        s = synth.image(3400 + i, shp)
+        m.zero_grad()
+        d, tot = m.forward(t(c), t(s))
+        tot.backward()
+        out.update({f"hidden{i}": hid, f"seed{i}": seed, f"checksum{i}": ck, f"cw{i}": cw,
+                    f"sw{i}": sw, f"content{i}": c, f"style{i}": s,
+                    f"style_loss{i}": d["style_loss"].detach().numpy(),
+                    f"content_loss{i}": d["content_loss"].detach().numpy(),
+                    f"total_loss{i}": tot.detach().numpy()})
+        names = []
+        for name, p in m.named_parameters():
+            if p.grad is not None:
+                out[f"grad{i}:{name}"] = p.grad.numpy()
+                names.append(name)
+        out[f"names{i}"] = np.array(names)
+    np.savez_compressed(os.path.join(HERE, "grads_wct.npz"), n=len(cases), **out)
+
+
 def gen_sourcenet(net):
     """SourceNet.test, classic AdaIN on VGG relu4_1."""
     out = {}
@@ -429,7 +458,8 @@ def gen_keys(net):
 GENERATORS = {"keys": gen_keys, "stats": gen_stats, "adain_rp": gen_adain_rp,
               "forward": gen_forward, "wct": gen_wct, "sanet": gen_sanet, "vgg": gen_vgg,
               "multiscale": gen_multiscale, "sourcenet": gen_sourcenet,
-              "adaptive": gen_adaptive, "deeper": gen_deeper, "grads": gen_grads}
+              "adaptive": gen_adaptive, "deeper": gen_deeper, "grads": gen_grads,
+              "grads_wct": gen_grads_wct}
 
 
 def main():

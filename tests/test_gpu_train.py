@@ -158,6 +158,34 @@ def test_training_gradients_match_reference(cuda, golden):
             assert e < 1e-4, (i, name, e)
 
 
+def test_wct_training_gradients_match_reference(cuda, golden):
+    """WCTRPNet.forward + total_loss.backward() on the kernels (rpst.autograd._WCTRPStep)
+    against the reference's own gradients (tests/golden/grads_wct.npz): the RP decoder's,
+    and none for the encoder (fuse() detaches, wct_rp.py:161-162)."""
+    import network as net
+    g = golden("grads_wct")
+    for i in range(int(g["n"])):
+        cfg = dict(rp_config(int(g[f"hidden{i}"])), content_weight=float(g[f"cw{i}"]),
+                   style_weight=float(g[f"sw{i}"]))
+        m = net.WCTRPNet(cfg, copy.deepcopy(net.vgg))
+        synth_(m, int(g[f"seed{i}"]))
+        m = m.to(cuda)
+        m.zero_grad()
+        losses, total = m(torch.from_numpy(g[f"content{i}"]).to(cuda),
+                          torch.from_numpy(g[f"style{i}"]).to(cuda))
+        total.backward()
+        for k in ("style_loss", "content_loss", "total_loss"):
+            assert rel_l2(losses[k].detach(), g[f"{k}{i}"]) < 1e-5, (i, k)
+        named = dict(m.named_parameters())
+        names = [str(n) for n in g[f"names{i}"]]
+        for name, p in named.items():
+            if name not in names:
+                assert p.grad is None, name
+        for name in names:
+            e = rel_l2(named[name].grad, g[f"grad{i}:{name}"])
+            assert e < 1e-4, (i, name, e)
+
+
 def test_adam_trajectory_matches_cpu(cuda):
     """Three train.py iterations (zero_grad, forward, backward, Adam step) on the kernels and
     on CPU autograd of the oracle from the same weights: same losses, same parameters."""
@@ -200,7 +228,8 @@ def test_training_step_deterministic(cuda):
     assert all(torch.equal(a, b) for a, b in zip(*gs))
 
 
-def test_train_driver_end_to_end(cuda, tmp_path):
+@pytest.mark.parametrize("network", ["adain", "wct"])
+def test_train_driver_end_to_end(cuda, tmp_path, network):
     """rp-style-transfer_amd/train.py on a tiny folder dataset: logs every iteration,
     stylises the test pairs at test_iter, saves {'encoder', 'decoder'} checkpoints."""
     import json
@@ -220,7 +249,7 @@ def test_train_driver_end_to_end(cuda, tmp_path):
     for d in ("test/content", "test/style"):
         Image.fromarray(rng.integers(0, 256, (32, 32, 3), dtype=np.uint8)).save(
             tmp_path / d / "t.png")
-    cfg = dict(rp_config(4), network="adain", vgg="unused", lr=1e-4, lr_decay=5e-5,
+    cfg = dict(rp_config(4), network=network, vgg="unused", lr=1e-4, lr_decay=5e-5,
                max_iter=5, batch_size=2, num_workers=2, img_size=32,
                content_dir=str(tmp_path / "content"), style_dir=str(tmp_path / "style"),
                test_dir=str(tmp_path / "test"), test_dataset="paired", test_iter=2,

@@ -178,6 +178,24 @@ def test_reference_training_gradients(golden):
             assert rel_l2(grads[name], g[f"grad{i}:{name}"]) < 1e-5, (i, name)
 
 
+def test_reference_wct_training_gradients(golden):
+    """R.wct_rp_grads against the reference's WCTRPNet.forward + backward (wct_rp.py:168-194):
+    decoder gradients only (fuse() detaches the encoder features)."""
+    import network as net
+    g = golden("grads_wct")
+    for i in range(int(g["n"])):
+        m = net.WCTRPNet(rp_config(int(g[f"hidden{i}"])), copy.deepcopy(net.vgg))
+        np.testing.assert_allclose(synth_(m, int(g[f"seed{i}"])), g[f"checksum{i}"], rtol=1e-12)
+        losses, grads = R.wct_rp_grads(t(g[f"content{i}"]), t(g[f"style{i}"]), state_dict_of(m),
+                                       5, float(g[f"cw{i}"]), float(g[f"sw{i}"]))
+        for k in ("style_loss", "content_loss", "total_loss"):
+            np.testing.assert_allclose(losses[k].numpy(), g[f"{k}{i}"], rtol=1e-5)
+        names = [str(n) for n in g[f"names{i}"]]
+        assert sorted(names) == sorted(grads)
+        for name in names:
+            assert rel_l2(grads[name], g[f"grad{i}:{name}"]) < 1e-5, (i, name)
+
+
 def test_sourcenet_test(golden):
     """SourceNet.test (classic AdaIN) against the reference."""
     import network as net
