@@ -795,7 +795,8 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
     a.wpk = packed_weight + direct_packed_floats(Cout, Cin, ksize) + wino_packed_floats(Cout, Cin);
     a.stat_part = stat_part;
     int op = in_op;
-    if (in_op == RPST_IN_ADAIN && fold_ws && a.H >= 2 && a.W >= 2) {  // AdaIN in the weights
+    // AdaIN in the weights (not with the statistics epilogue: that layer keeps the loader)
+    if (in_op == RPST_IN_ADAIN && fold_ws && !stat_part && a.H >= 2 && a.W >= 2) {
       if (int e = wino4_fold(a, packed_weight, pad_cout(Cout), fold_ws, st)) return e;
       op = RPST_IN_NONE;
     }

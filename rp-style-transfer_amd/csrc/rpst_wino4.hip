@@ -31,6 +31,8 @@
 // one-per-SIMD software-pipelined form and register-staged patches were slower.
 #include "rpst_conv.h"
 
+#include <type_traits>
+
 namespace rpst {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -132,10 +134,7 @@ bool wino4_fits(int N, int Cin, int Hs, int Ws, int in_op) {
   const int64_t plane = (int64_t)Hs * Ws * 4;
   return (int64_t)(3 * Cin + 8) * plane < (1LL << 32) - (1LL << 20);
 }
-int wino4_persist() {
-  const char* e = getenv("RPST_WINO4_PERSIST");  // A/B switch
-  return (e && *e) ? atoi(e) != 0 : 1;
-}
+int wino4_persist() { return 1; }  // one block per spatial tile loops over the co tiles
 
 // B^T row transform of one 6-vector (in place): the shared terms of rows (1,2) and (3,4)
 __device__ __forceinline__ void bt6(float& d0, float& d1, float& d2, float& d3, float& d4,
@@ -171,11 +170,13 @@ __device__ __forceinline__ bool resolve_bf(int& v, int n, bool zero_pad) {
   return in || !zero_pad;
 }
 
-// DBG (timing experiments only, tools/wino4_dbg.sh; results are wrong): bit0 no patch
-// loads, bit1 no weight DMA, bit2 no patch stores, bit3 no input transform, bit4 no
-// barriers in the main loop, bit5 no epilogue, bit6 no weight LDS reads.
-template <int INOP, bool PERSIST, int DBG = 0>
+// STATS: the calc_mean_std partials epilogue (a.stat_part); BTAB: the folded per-(n, co)
+// border-class bias table (a.btab). Both are template arguments so a plain layer's
+// epilogue carries none of their VALU; the two transformed-row halves (ph, waves 0-3 and
+// 4-7) run epilogues specialised for their half.
+template <int INOP, bool STATS, bool BTAB>
 __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
+  constexpr int DBG = 0;
   static_assert(RawN<INOP>::R == 1, "one raw load per patch element");
   // one __shared__ object per ring stage: the stage a K step reads and the one its DMA
   // fills are then distinct objects, so the compiler's wait insertion does not drain the
@@ -187,17 +188,15 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) float dummy[256];  // target of padding DMA pieces
 
   // block -> (column tile, row tile, image), XCD-swizzled (neighbouring spatial tiles share
-  // halo rows and every block of an XCD streams the same weight slices through its L2)
-  int bid = xcd_swizzle(blockIdx.x, (int)gridDim.x), ct0 = 0;
-  if (!PERSIST) {
-    ct0 = bid % a.co_tiles;
-    bid /= a.co_tiles;
-  }
+  // halo rows and every block of an XCD streams the same weight slices through its L2);
+  // one block loops over every co tile of its spatial tile
+  int bid = xcd_swizzle(blockIdx.x, (int)gridDim.x);
+  const int ct0 = 0;
   const int tx = bid % a.tiles_x;
   bid /= a.tiles_x;
   const int ty = bid % a.tiles_y;
   const int n = bid / a.tiles_y;
-  const int nct = PERSIST ? a.co_tiles : 1;
+  const int nct = a.co_tiles;
   const int nch = a.nchunks, K4 = 2 * nch, G = nct * K4;  // K steps per co tile / in total
   const int y0 = ty * kW4TH, x0 = tx * kW4TW;
 
@@ -275,10 +274,11 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // 1 KiB, pieces w, w + 8, w + 16 of wave w) and patch into its stage by LDS-DMA; every
   // wave issues the same number of pieces per step (the padding ones read out of range
   // into the dummy target), so the ring's waits are counted: kPer per step
-  auto issue = [&](int g, float* st) {
-    const int ct = ct0 + g / K4, ks = g - (g / K4) * K4;
+  // (weights of global step g are slice g of the block's weight image: no division; ks =
+  // g % K4 is tracked by the caller)
+  auto issue = [&](int g, int ks, float* st) {
     if (!(DBG & 2)) {
-      const unsigned base = (unsigned)(ct * K4 + ks) * (unsigned)kW4SW * 4u + (unsigned)lane * 16u;
+      const unsigned base = (unsigned)(ct0 * K4 + g) * (unsigned)kW4SW * 4u + (unsigned)lane * 16u;
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const int p = wave + 8 * i;
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   auto fix_own = [&](int g, float* st) {
     if constexpr (kAff) {
       if (DBG & 4) return;
-      const int ks = g - (g / K4) * K4, ch = 4 * ks + chl;
+      const int ks = g % K4, ch = 4 * ks + chl;
       const bool chok = ch < a.Cin;
       const int cc = chok ? ch : 0;
       const float mc = aparm[cc], sc = aparm[kW4AffC + cc], ms = aparm[2 * kW4AffC + cc];
@@ -412,8 +412,9 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   };
 
   // this wave's partial output tile of channel half mt, accumulator element r:
-  // sum over its transformed rows i = 3ph + i' of A^T[:, i] (M[i, :] A)
-  auto partial = [&](int mt, int r, float (&Y)[16]) {
+  // sum over its transformed rows i = 3ph + i' of A^T[:, i] (M[i, :] A); PH = ph
+  auto partial = [&](auto PHc, int mt, int r, float (&Y)[16]) {
+    constexpr int PH = decltype(PHc)::value;
     float P[3][4];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
-      if (ph == 0) {
+      if constexpr (PH == 0) {
         const float s12 = P[1][x] + P[2][x], d12 = P[1][x] - P[2][x];
         Y[0 * 4 + x] = P[0][x] + s12;
         Y[1 * 4 + x] = d12;
@@ -449,18 +450,18 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   auto finish = [&](int co, float (&Y)[16]) {
     const bool cok = co < a.Cout;
     float bv = (a.bias && cok) ? a.bias[co] : 0.f;
-    // folded AdaIN: the bias depends on which taps of the zero-padded input were inside
-    // the image (border class); interior tiles take the interior entry
-    const float* bt = a.btab ? a.btab + ((int64_t)n * a.Cout + (cok ? co : 0)) * 9 : nullptr;
-    if (bt) bv = cok ? bt[4] : 0.f;
-    const bool edge = bt && (gy0 == 0 || gy0 + 4 >= a.H || gx0 == 0 || gx0 + 4 >= a.W);
+    // folded AdaIN / WCT: the bias depends on which taps of the zero-padded input were
+    // inside the image (border class); interior tiles take the interior entry
+    const float* bt = BTAB ? a.btab + ((int64_t)n * a.Cout + (cok ? co : 0)) * 9 : nullptr;
+    if (BTAB) bv = cok ? bt[4] : 0.f;
+    const bool edge = BTAB && (gy0 == 0 || gy0 + 4 >= a.H || gx0 == 0 || gx0 + 4 >= a.W);
     float sum = 0.f;
 #pragma unroll
     for (int yy = 0; yy < 4; ++yy)
 #pragma unroll
       for (int xx = 0; xx < 4; ++xx) {
         float b = bv;
-        if (edge) {
+        if (BTAB && edge) {
           const int gy = gy0 + yy, gx = gx0 + xx;
           const int rc = gy == 0 ? 0 : (gy >= a.H - 1 ? 2 : 1);
           const int cc = gx == 0 ? 0 : (gx >= a.W - 1 ? 2 : 1);
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         }
         const float v = activate(Y[yy * 4 + xx] + b, a.relu);
         Y[yy * 4 + xx] = v;
-        sum += (yy < rows && gx0 + xx < a.W) ? v : 0.f;
+        if (STATS) sum += (yy < rows && gx0 + xx < a.W) ? v : 0.f;
       }
     if (cok) {
       float* o = a.out + (((int64_t)n * a.Cout + co) * a.H + gy0) * a.W + gx0;
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         }
       }
     }
-    if (a.stat_part) {
+    if constexpr (STATS) {
 #pragma unroll
       for (int m = 1; m < 16; m <<= 1) sum += __shfl_xor(sum, m, 64);
       const float mean = sum * inv;
@@ -514,41 +515,41 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
-  auto epilogue = [&](int ct, float* xs) {
+  // PH = ph: the half this wave finishes is channel half PH; it hands the other half's
+  // partial tile to its partner wave
+  auto epilogue_ph = [&](auto PHc, int ct, float* xs) {
+    constexpr int PH = decltype(PHc)::value;
     lds_barrier();  // every wave is done reading the stage
     float* xb = xs + wr * 2048;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float own[16];
       {
-        float y0v[16], y1v[16];
-        partial(0, r, y0v);
-        partial(1, r, y1v);
+        float give[16];
+        partial(PHc, PH, r, own);
+        partial(PHc, 1 - PH, r, give);
 #pragma unroll
-        for (int v = 0; v < 16; ++v) own[v] = ph ? y1v[v] : y0v[v];
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          float4 o4;
-          o4.x = ph ? y0v[4 * g4] : y1v[4 * g4];
-          o4.y = ph ? y0v[4 * g4 + 1] : y1v[4 * g4 + 1];
-          o4.z = ph ? y0v[4 * g4 + 2] : y1v[4 * g4 + 2];
-          o4.w = ph ? y0v[4 * g4 + 3] : y1v[4 * g4 + 3];
-          *reinterpret_cast<float4*>(xb + ((ph * 4 + g4) * 64 + lane) * 4) = o4;
-        }
+        for (int g4 = 0; g4 < 4; ++g4)
+          *reinterpret_cast<float4*>(xb + ((PH * 4 + g4) * 64 + lane) * 4) =
+              make_float4(give[4 * g4], give[4 * g4 + 1], give[4 * g4 + 2], give[4 * g4 + 3]);
       }
       lds_barrier();
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float4 o4 =
-            *reinterpret_cast<const float4*>(xb + (((1 - ph) * 4 + g4) * 64 + lane) * 4);
+            *reinterpret_cast<const float4*>(xb + (((1 - PH) * 4 + g4) * 64 + lane) * 4);
         own[4 * g4] += o4.x;
         own[4 * g4 + 1] += o4.y;
         own[4 * g4 + 2] += o4.z;
         own[4 * g4 + 3] += o4.w;
       }
-      finish(ct * kW4BM + 16 * ph + 4 * k + r, own);
+      finish(ct * kW4BM + 16 * PH + 4 * k + r, own);
       if (r < 3) lds_barrier();  // the next pass overwrites the exchange region
     }
+  };
+  auto epilogue = [&](int ct, float* xs) {
+    if (ph) epilogue_ph(std::integral_constant<int, 1>{}, ct, xs);
+    else epilogue_ph(std::integral_constant<int, 0>{}, ct, xs);
   };
 
   // ---- pipeline: ring of 4 stages, K step g in stage g % 4, issued 3 steps ahead --------
@@ -566,9 +567,10 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     else if (allowed >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
-  issue(0, smem0);
-  if (G > 1) issue(1, smem1);
-  if (G > 2) issue(2, smem2);
+  issue(0, 0, smem0);
+  if (G > 1) issue(1, 1 % K4, smem1);
+  if (G > 2) issue(2, 2 % K4, smem2);
+  int ks3 = 3 % K4;  // chunk step of g + 3
   if constexpr (kAff) {  // step 0's affine (published by the first step's barrier)
     wait_ahead(min(2, G - 1));
     fix_own(0, smem0);
@@ -580,7 +582,8 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
       wait_ahead(min(2, G - 1 - g));
       lds_barrier();  // step g's stage is complete; nx3 is free
     }
-    if (g + 3 < G) issue(g + 3, nx3);
+    if (g + 3 < G) issue(g + 3, ks3, nx3);
+    ks3 = ks3 + 1 == K4 ? 0 : ks3 + 1;
     compute(cur);
     if ((g + 1) % K4 == 0) {
       if (!(DBG & 32) || a.N < 0) epilogue(ct0 + g / K4, cur);
@@ -782,32 +785,29 @@ int wino4_launch(ConvArgs& a, int in_op, hipStream_t st) {
   a.tiles_y = (a.H + kW4TH - 1) / kW4TH;
   a.co_tiles = a.Cout_pad / kW4BM;
   a.stat_P = a.tiles_x * a.tiles_y * 4;
-  a.persist = wino4_persist();
+  a.persist = 1;
   RPST_REQUIRE((int64_t)a.co_tiles * a.nchunks * kW4WCH * 4 < (1LL << 31),
                "conv2d: winograd4 weight image exceeds 2 GiB");
-  const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.N * (a.persist ? 1 : a.co_tiles);
+  const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.N;
   RPST_REQUIRE(blocks <= 0x7fffffffLL, "conv2d: grid too large");
   const unsigned nb = (unsigned)blocks;
-  const char* dbg = getenv("RPST_WINO4_DBG");
-  if (dbg && *dbg && in_op == RPST_IN_NONE && a.persist) {
-    switch (atoi(dbg)) {
-#define RPST_W4_DBGCASE(D) \
-  case D: wino4_mfma_kernel<RPST_IN_NONE, true, D><<<nb, kW4NTH, 0, st>>>(a); break;
-      RPST_W4_DBGCASE(1) RPST_W4_DBGCASE(2) RPST_W4_DBGCASE(4) RPST_W4_DBGCASE(8)
-      RPST_W4_DBGCASE(16) RPST_W4_DBGCASE(32) RPST_W4_DBGCASE(64) RPST_W4_DBGCASE(7)
-      RPST_W4_DBGCASE(23) RPST_W4_DBGCASE(87) RPST_W4_DBGCASE(95) RPST_W4_DBGCASE(256)
-#undef RPST_W4_DBGCASE
-      default: break;
-    }
-    return launch_status("wino4_mfma_kernel(debug)");
-  }
-#define RPST_W4_GO(OP)                                                                     \
-  (a.persist ? (void)(wino4_mfma_kernel<OP, true><<<nb, kW4NTH, 0, st>>>(a))                \
-             : (void)(wino4_mfma_kernel<OP, false><<<nb, kW4NTH, 0, st>>>(a)))
+  const bool stats = a.stat_part != nullptr, btab = a.btab != nullptr;
+  RPST_REQUIRE(!btab || in_op == RPST_IN_NONE, "conv2d: winograd4 bias table with a loader op");
+#define RPST_W4_GO(OP, S, B) wino4_mfma_kernel<OP, S, B><<<nb, kW4NTH, 0, st>>>(a)
   switch (in_op) {
-    case RPST_IN_ADAIN: RPST_W4_GO(RPST_IN_ADAIN); break;
-    case RPST_IN_UPSAMPLE2: RPST_W4_GO(RPST_IN_UPSAMPLE2); break;
-    default: RPST_W4_GO(RPST_IN_NONE);
+    case RPST_IN_ADAIN:
+      if (stats) RPST_W4_GO(RPST_IN_ADAIN, true, false);
+      else RPST_W4_GO(RPST_IN_ADAIN, false, false);
+      break;
+    case RPST_IN_UPSAMPLE2:
+      if (stats) RPST_W4_GO(RPST_IN_UPSAMPLE2, true, false);
+      else RPST_W4_GO(RPST_IN_UPSAMPLE2, false, false);
+      break;
+    default:
+      RPST_REQUIRE(!(stats && btab), "conv2d: winograd4 folded bias with statistics");
+      if (stats) RPST_W4_GO(RPST_IN_NONE, true, false);
+      else if (btab) RPST_W4_GO(RPST_IN_NONE, false, true);
+      else RPST_W4_GO(RPST_IN_NONE, false, false);
   }
 #undef RPST_W4_GO
   return launch_status("wino4_mfma_kernel");
