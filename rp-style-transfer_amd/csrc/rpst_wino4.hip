@@ -204,6 +204,9 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int k = lane >> 4, tn = lane & 15;
   const int wr = wave & 3, ph = wave >> 2;  // tile row, transformed-row half
+  // static priority for the second-dispatched half (waves 4-7), the arbitration loser on
+  // every segment (MI355X_MICROARCH.md, two waves per SIMD, item 4); a.persist & 2 = A/B off
+  if (ph && !(a.persist & 2)) __builtin_amdgcn_s_setprio(1);
 
   const bool pooled = INOP == RPST_IN_UPSAMPLE2;
   const unsigned in_plane = pooled ? (unsigned)(a.Hs * a.Ws) : (unsigned)(a.H * a.W);
@@ -276,9 +279,10 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // into the dummy target), so the ring's waits are counted: kPer per step
   // (weights of global step g are slice g of the block's weight image: no division; ks =
   // g % K4 is tracked by the caller)
-  auto issue = [&](int g, int ks, float* st) {
+  auto issue = [&](int g, int ks, bool live, float* st) {
     if (!(DBG & 2)) {
-      const unsigned base = (unsigned)(ct0 * K4 + g) * (unsigned)kW4SW * 4u + (unsigned)lane * 16u;
+      const unsigned base = live ? (unsigned)(ct0 * K4 + g) * (unsigned)kW4SW * 4u + (unsigned)lane * 16u
+                                 : wbytes;
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const int p = wave + 8 * i;
@@ -291,7 +295,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     {
       if (DBG & 1) return;
       const unsigned ch = (unsigned)(4 * ks + chl);
-      const int so = __builtin_amdgcn_readfirstlane((int)(ch * in_plane * 4u));
+      const int so = __builtin_amdgcn_readfirstlane(live ? (int)(ch * in_plane * 4u) : (int)oob);
       float* xs = st + chl * kW4CS;
       if (wide) {
 #pragma unroll
@@ -447,15 +451,14 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   const bool vec = (a.W & 3) == 0 && gx0 + 3 < a.W;
   const int rows = max(0, min(4, a.H - gy0)), cols = max(0, min(kW4TW, a.W - x0));
   const float inv = rows * cols > 0 ? 1.f / (float)(rows * cols) : 0.f;
-  auto finish = [&](int co, float (&Y)[16]) {
+  // bv: the layer's bias of channel co (loaded by the caller ahead of time)
+  auto finish = [&](int co, float bv, float (&Y)[16]) {
     const bool cok = co < a.Cout;
-    float bv = (a.bias && cok) ? a.bias[co] : 0.f;
     // folded AdaIN / WCT: the bias depends on which taps of the zero-padded input were
     // inside the image (border class); interior tiles take the interior entry
     const float* bt = BTAB ? a.btab + ((int64_t)n * a.Cout + (cok ? co : 0)) * 9 : nullptr;
     if (BTAB) bv = cok ? bt[4] : 0.f;
     const bool edge = BTAB && (gy0 == 0 || gy0 + 4 >= a.H || gx0 == 0 || gx0 + 4 >= a.W);
-    float sum = 0.f;
 #pragma unroll
     for (int yy = 0; yy < 4; ++yy)
 #pragma unroll
@@ -467,10 +470,23 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
           const int cc = gx == 0 ? 0 : (gx >= a.W - 1 ? 2 : 1);
           b = cok ? bt[rc * 3 + cc] : 0.f;
         }
-        const float v = activate(Y[yy * 4 + xx] + b, a.relu);
-        Y[yy * 4 + xx] = v;
-        if (STATS) sum += (yy < rows && gx0 + xx < a.W) ? v : 0.f;
+        Y[yy * 4 + xx] += b;
       }
+    // the activation mode is uniform: one branch per tile, not per element
+    if (a.relu == RPST_ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) Y[e] = fmaxf(Y[e], 0.f);
+    } else if (a.relu == RPST_ACT_LRELU) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) Y[e] = Y[e] > 0.f ? Y[e] : Y[e] * 0.2f;
+    }
+    float sum = 0.f;
+    if (STATS) {
+#pragma unroll
+      for (int yy = 0; yy < 4; ++yy)
+#pragma unroll
+        for (int xx = 0; xx < 4; ++xx) sum += (yy < rows && gx0 + xx < a.W) ? Y[yy * 4 + xx] : 0.f;
+    }
     if (cok) {
       float* o = a.out + (((int64_t)n * a.Cout + co) * a.H + gy0) * a.W + gx0;
 #pragma unroll
@@ -521,6 +537,12 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     constexpr int PH = decltype(PHc)::value;
     lds_barrier();  // every wave is done reading the stage
     float* xb = xs + wr * 2048;
+    // the four biases this wave applies, loaded once ahead of the passes
+    const int co0 = ct * kW4BM + 16 * PH + 4 * k;
+    float bias4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      bias4[r] = (!BTAB && a.bias && co0 + r < a.Cout) ? a.bias[co0 + r] : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float own[16];
@@ -543,7 +565,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         own[4 * g4 + 2] += o4.z;
         own[4 * g4 + 3] += o4.w;
       }
-      finish(ct * kW4BM + 16 * PH + 4 * k + r, own);
+      finish(co0 + r, bias4[r], own);
       if (r < 3) lds_barrier();  // the next pass overwrites the exchange region
     }
   };
@@ -553,49 +575,44 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   };
 
   // ---- pipeline: ring of 4 stages, K step g in stage g % 4, issued 3 steps ahead --------
-  // Before the barrier that opens step g each wave retires its own DMA pieces of step g
-  // with a counted vmcnt (the pieces of steps g + 1, g + 2 stay in flight; ADAIN's register
-  // loads drain everything at their use, so its count is only ever conservative).
-  constexpr int kPerW = 3;                          // weight pieces per step and wave
-  const int per = kPerW + (wide ? 3 : kSlow);       // all pieces per step and wave
-  // wait until at most `ahead` steps' pieces issued after the awaited one are in flight
-  auto wait_ahead = [&](int ahead) {
-    const int allowed = ahead * per;
-    if (allowed >= 26) asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
-    else if (allowed >= 13) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
-    else if (allowed >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else if (allowed >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // Every step issues one group of `per` pieces per wave, also past the last step (those
+  // read out of range into a stage no later step reads), so the wait before the barrier
+  // that opens step g is one constant: the groups of steps g + 1, g + 2 stay in flight
+  // (ADAIN's register loads drain everything at their use, so the count stays conservative).
+  auto wait_ahead2 = [&]() {
+    if (wide) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // 2 x (3 + 3)
+    else asm volatile("s_waitcnt vmcnt(26)" ::: "memory");       // 2 x (3 + kSlow)
   };
-  issue(0, 0, smem0);
-  if (G > 1) issue(1, 1 % K4, smem1);
-  if (G > 2) issue(2, 2 % K4, smem2);
-  int ks3 = 3 % K4;  // chunk step of g + 3
+  issue(0, 0, true, smem0);
+  issue(1, 1 % K4, G > 1, smem1);
+  issue(2, 2 % K4, G > 2, smem2);
+  int ks3 = 3 % K4;          // chunk step of g + 3
+  int ks = 0, ct = ct0;      // chunk step and co tile of g
   if constexpr (kAff) {  // step 0's affine (published by the first step's barrier)
-    wait_ahead(min(2, G - 1));
+    wait_ahead2();
     fix_own(0, smem0);
   }
   // K step g from stage `cur`; step g + 3's DMA into `nx3` (the stage step g - 1 used);
   // ADAIN: step g + 1's affine on this wave's own pieces in `nx1`, after the MFMAs
   auto step = [&](int g, float* cur, float* nx1, float* nx3) {
-    if (!(DBG & 16)) {
-      wait_ahead(min(2, G - 1 - g));
-      lds_barrier();  // step g's stage is complete; nx3 is free
-    }
-    if (g + 3 < G) issue(g + 3, ks3, nx3);
+    wait_ahead2();
+    lds_barrier();  // step g's stage is complete; nx3 is free
+    issue(g + 3, ks3, g + 3 < G, nx3);
     ks3 = ks3 + 1 == K4 ? 0 : ks3 + 1;
     compute(cur);
-    if ((g + 1) % K4 == 0) {
-      if (!(DBG & 32) || a.N < 0) epilogue(ct0 + g / K4, cur);
+    if (ks == K4 - 1) {
+      epilogue(ct, cur);
 #pragma unroll
       for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
     if constexpr (kAff) {
       if (g + 1 < G) {
-        wait_ahead(min(2, G - 2 - g));  // this wave's pieces of step g + 1 have landed
+        wait_ahead2();  // this wave's pieces of step g + 1 have landed
         fix_own(g + 1, nx1);
       }
     }
+    ct += ks == K4 - 1 ? 1 : 0;
+    ks = ks == K4 - 1 ? 0 : ks + 1;
   };
   for (int g = 0; g < G; g += kW4STG) {
     step(g, smem0, smem1, smem3);
@@ -603,6 +620,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     if (g + 2 < G) step(g + 2, smem2, smem3, smem1);
     if (g + 3 < G) step(g + 3, smem3, smem0, smem2);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the padding DMA has landed too
 }
 
 // ---- AdaIN folded into the weights (RPST_IN_ADAIN through the plain NONE loader) -------
@@ -785,7 +803,10 @@ int wino4_launch(ConvArgs& a, int in_op, hipStream_t st) {
   a.tiles_y = (a.H + kW4TH - 1) / kW4TH;
   a.co_tiles = a.Cout_pad / kW4BM;
   a.stat_P = a.tiles_x * a.tiles_y * 4;
-  a.persist = 1;
+  {
+    const char* e = getenv("RPST_WINO4_NOPRIO");  // A/B switch for the static priority
+    a.persist = 1 | ((e && *e && atoi(e)) ? 2 : 0);
+  }
   RPST_REQUIRE((int64_t)a.co_tiles * a.nchunks * kW4WCH * 4 < (1LL << 31),
                "conv2d: winograd4 weight image exceeds 2 GiB");
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.N;
