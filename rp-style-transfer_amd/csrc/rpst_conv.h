@@ -21,6 +21,7 @@ struct ConvArgs {
   int tiles_x, tiles_y, co_tiles;
   int pad, relu;
   int persist;        // Winograd: one block loops over all co tiles of its spatial tile
+  int cosplit;        // F(4x4): co tiles split over this many blocks per spatial tile
   float2* stat_part;  // optional: per-(n, co, wave tile) (mean, M2) of the output
   int stat_P;         // partials per (n, co) = tiles_x * tiles_y * WN
   // F(4x4) with AdaIN folded into per-image weights (wino4_fold): image n's packed weights

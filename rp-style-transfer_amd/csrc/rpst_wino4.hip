@@ -38,6 +38,27 @@ namespace rpst {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 constexpr int kW4CK = 8;                   // input channels per chunk
+#ifndef RPST_W4DBG
+#define RPST_W4DBG 0
+#endif
+// DMA of step g + 3 issued inside step g's MFMA stream (its address SALU then issues
+// beside the matrix pipe): weights after MFMA pair RPST_W4_HW, patch after RPST_W4_HP
+// (-1: before the input transform). 0 / 2 measured best (profiles/r02_wino4_variants.log)
+#ifndef RPST_W4_HW
+#define RPST_W4_HW 0
+#endif
+#ifndef RPST_W4_HP
+#define RPST_W4_HP 2
+#endif
+#ifndef RPST_W4_PAIR
+#define RPST_W4_PAIR 0
+#endif
+#ifndef RPST_W4_STAG
+#define RPST_W4_STAG 0
+#endif
+#ifndef RPST_W4_QD
+#define RPST_W4_QD 5
+#endif
 constexpr int kW4BM = 32;                  // output channels per co tile
 constexpr int kW4TH = 16, kW4TW = 64;      // output rows x columns per block
 constexpr int kW4PH = kW4TH + 2;           // patch rows
@@ -137,6 +158,38 @@ bool wino4_fits(int N, int Cin, int Hs, int Ws, int in_op) {
 int wino4_persist() { return 1; }  // one block per spatial tile loops over the co tiles
 
 // B^T row transform of one 6-vector (in place): the shared terms of rows (1,2) and (3,4)
+// what the F(4x4) epilogue needs besides the tile (wino4_mfma_kernel's epi_ctx)
+struct EpiCtx {
+  int W, H, Cout, relu, gy0, gx0, rows, n, sidx, statP;
+  bool vec;
+  float inv;
+  float* out;
+  const float* btab;
+  float2* statp;
+};
+
+// kernel arguments loaded at their use (s_load through an opaque copy of the kernarg
+// pointer, so the loads are not hoisted out of the loop that contains the use)
+typedef const __attribute__((address_space(4))) ConvArgs* KArgs;
+__device__ __forceinline__ KArgs late_args() {
+  KArgs p = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+#if __HIP_DEVICE_COMPILE__  // the host pass only emits the launch stub (no "s" registers)
+  asm volatile("" : "+s"(p));
+#endif
+  return p;
+}
+// buffer resource over `bytes` at p, or over zero records (every access reads 0) if !ok
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_or_zero(const float* p, unsigned bytes, bool ok) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, ok ? (int)bytes : 0, 0x00020000);
+}
+// a wave-uniform value made opaque at this point (not hoisted out of the enclosing loop)
+__device__ __forceinline__ int launder(int v) {
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+s"(v));
+#endif
+  return v;
+}
+
 __device__ __forceinline__ void bt6(float& d0, float& d1, float& d2, float& d3, float& d4,
                                     float& d5) {
   const float A = fmaf(-4.f, d2, d4), B = fmaf(-4.f, d1, d3);
@@ -176,7 +229,12 @@ __device__ __forceinline__ bool resolve_bf(int& v, int n, bool zero_pad) {
 // 4-7) run epilogues specialised for their half.
 template <int INOP, bool STATS, bool BTAB>
 __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
-  constexpr int DBG = 0;
+  // timing-only experiments (results wrong; tools/build_variants.sh -DRPST_W4DBG=n): 1 no
+  // patch DMA, 2 no weight DMA, 8 no input transform, 16 no barriers, 32 no epilogue,
+  // 64 no weight LDS reads, 128 no DMA waits
+  constexpr int DBG = RPST_W4DBG;
+  // DMA placement of step g + 3: before the transform (-1) or after MFMA pair q of step g
+  constexpr int kHW = RPST_W4_HW, kHP = RPST_W4_HP;
   static_assert(RawN<INOP>::R == 1, "one raw load per patch element");
   // one __shared__ object per ring stage: the stage a K step reads and the one its DMA
   // fills are then distinct objects, so the compiler's wait insertion does not drain the
@@ -191,12 +249,17 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // halo rows and every block of an XCD streams the same weight slices through its L2);
   // one block loops over every co tile of its spatial tile
   int bid = xcd_swizzle(blockIdx.x, (int)gridDim.x);
-  const int ct0 = 0;
+  // a.cosplit blocks per spatial tile (consecutive logical ids: one XCD, dispatched
+  // together, so the patch they all stream is served by that XCD's L2), each looping over
+  // co_tiles / cosplit co tiles
+  const int cog = bid % a.cosplit;
+  bid /= a.cosplit;
+  const int nct = a.co_tiles / a.cosplit;
+  const int ct0 = cog * nct;
   const int tx = bid % a.tiles_x;
   bid /= a.tiles_x;
   const int ty = bid % a.tiles_y;
   const int n = bid / a.tiles_y;
-  const int nct = a.co_tiles;
   const int nch = a.nchunks, K4 = 2 * nch, G = nct * K4;  // K steps per co tile / in total
   const int y0 = ty * kW4TH, x0 = tx * kW4TW;
 
@@ -213,11 +276,18 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // out-of-range offset for a padding position: the image's byte size, added to the
   // channel offset (wino4_fits keeps two of them plus the largest channel offset < 2^32)
   const unsigned oob = a.Cin * in_plane * 4u;
-  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.in + (int64_t)n * a.Cin * in_plane), (short)0, (int)oob, 0x00020000);
+  const float* in_img = a.in + (int64_t)n * a.Cin * in_plane;
   const unsigned wbytes = (unsigned)(a.co_tiles * nch * kW4WCH) * 4u;
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.wpk + (int64_t)n * a.wstride), (short)0, (int)wbytes, 0x00020000);
+  const float* w_img = a.wpk + (int64_t)n * a.wstride;
+  // descriptors per issue: a dead piece (past the last step, or a channel >= Cin) goes
+  // through a zero-record descriptor, so it reads 0 whatever its offsets (the range check
+  // covers only the per-lane offset, not the uniform soffset)
+  // (a __device__ helper: a lambda returning a buffer resource silently drops the kernel's
+  // host launch stub)
+  // LDS targets are re-derived inside each issue from one laundered wave-uniform offset
+  // (launder()): precomputed, the ~50 per-stage piece addresses overflow the scalar
+  // registers and come back by a VALU readlane each
+
 
   // ---- patch of one K step: 4 channels, [18 rows][68] (66 columns + 2 spare) at channel
   // stride 1280; wave w fills half w & 1 of channel w >> 1. One-load operators (NONE,
@@ -253,7 +323,8 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         const int f = 64 * (kSlow * hf + i) + lane;
         const int row = min(f / kW4PS, kW4PH - 1), col = f - (f / kW4PS) * kW4PS;
         int y = y0 - 1 + row, x = x0 - 1 + col;
-        const bool ok = col < kW4TW + 2 && resolve_bf(y, a.H, zp) & resolve_bf(x, a.W, zp);
+        const bool oky = resolve_bf(y, a.H, zp), okx = resolve_bf(x, a.W, zp);  // both clamp
+        const bool ok = col < kW4TW + 2 && oky && okx;
         poff[i] = ok ? ((unsigned)((pooled ? y >> 1 : y) * rs) + (unsigned)(pooled ? x >> 1 : x)) * 4u
                      : oob;
         pvalid |= ok ? (1u << i) : 0u;
@@ -279,38 +350,46 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // into the dummy target), so the ring's waits are counted: kPer per step
   // (weights of global step g are slice g of the block's weight image: no division; ks =
   // g % K4 is tracked by the caller)
-  auto issue = [&](int g, int ks, bool live, float* st) {
+  auto issue_w = [&](int g, bool live, float* st) {
     if (!(DBG & 2)) {
-      const unsigned base = live ? (unsigned)(ct0 * K4 + g) * (unsigned)kW4SW * 4u + (unsigned)lane * 16u
-                                 : wbytes;
+      const int wv = launder(wave);
+      const int sw = live ? (ct0 * K4 + g) * kW4SW * 4 + wv * 1024 : 0;  // piece wv's bytes
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        const int p = wave + 8 * i;
-        const bool real = p < 18;
+        const bool real = wv + 8 * i < 18;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rw, (lds_ptr_t)(real ? st + kW4SPATCH + p * 256 : dummy), 16,
-            (int)(real ? base + (unsigned)p * 1024u : wbytes), 0, 0, 0);
+            rsrc_or_zero(w_img, wbytes, live && real), (lds_ptr_t)(real ? st + kW4SPATCH + wv * 256 + 2048 * i : dummy), 16, lane * 16,
+            real ? sw + 8192 * i : 0, 0, 0);
       }
     }
+  };
+  auto issue_p = [&](int ks, bool live, float* st) {
     {
       if (DBG & 1) return;
-      const unsigned ch = (unsigned)(4 * ks + chl);
-      const int so = __builtin_amdgcn_readfirstlane(live ? (int)(ch * in_plane * 4u) : (int)oob);
-      float* xs = st + chl * kW4CS;
+      const int wv = launder(wave);
+      const int c = 4 * ks + (wv >> 1);
+      const bool ok = live && c < a.Cin;
+      const auto r = rsrc_or_zero(in_img, oob, ok);
+      const int so = ok ? (int)((unsigned)c * in_plane * 4u) : 0;  // < 2^32 (wino4_fits)
+      float* xs = st + (wv >> 1) * kW4CS;
       if (wide) {
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-          const int p = 3 * hf + i;
+          const int p = 3 * (wv & 1) + i;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rin, (lds_ptr_t)(p < kW4DMA4 ? xs + 256 * p : dummy), 16, (int)poff[i], so, 0, 0);
+              r, (lds_ptr_t)(p < kW4DMA4 ? xs + 256 * p : dummy), 16, (int)poff[i], so, 0, 0);
         }
       } else {
 #pragma unroll
         for (int i = 0; i < kSlow; ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_t)(xs + 64 * (kSlow * hf + i)),
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(xs + 64 * (kSlow * (wv & 1) + i)),
                                                    4, (int)poff[i], so, 0, 0);
       }
     }
+  };
+  [[maybe_unused]] auto issue = [&](int g, int ks, bool live, float* st) {
+    issue_w(g, live, st);
+    issue_p(ks, live, st);
   };
   // ADAIN, in place on the elements this lane's own DMA pieces of step g wrote (so a wave
   // needs only its own counted wait, no barrier): ((v - mean_c) / std_c) * std_s + mean_s
@@ -351,14 +430,39 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // one K step of 4 channels from a stage: 72 VALU of input transform + 36 MFMAs
-  auto compute = [&](const float* pbuf) {
+  // hw / hp: called after MFMA pair kHW / kHP (RPST_W4VAR placement experiments)
+  // RPST_W4_STAG: the ph = 1 waves (4-7, SIMD partners of waves 0-3) defer MFMA pairs
+  // q >= kQD of a step to after the next barrier (operands kept in registers), so on every
+  // SIMD one wave's deferred MFMAs run beside its partner's DMA issue, LDS reads and input
+  // transform; per accumulator the K order is unchanged (bit-identical results)
+  constexpr int kQD = RPST_W4_QD, kND = 9 - kQD;
+  float tdef[2 * kND];
+  // prv: the stage of the previous step (its weights stay until the next barrier: with
+  // RPST_W4_STAG the weight DMA runs two steps ahead, the patch DMA three)
+  [[maybe_unused]] auto mma_def = [&](const float* prv) {
+    const float* wq = prv + kW4SPATCH + 9 * 256 + lane * 4;
+    float4 wdef[kND];
+#pragma unroll
+    for (int j = 0; j < kND; ++j) wdef[j] = *reinterpret_cast<const float4*>(wq + (kQD + j) * 256);
+#pragma unroll
+    for (int j = 0; j < kND; ++j) {
+      const int p0 = 2 * (kQD + j), p1 = p0 + 1;
+      acc[p0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wdef[j].x, tdef[2 * j], acc[p0][0], 0, 0, 0);
+      acc[p0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wdef[j].y, tdef[2 * j], acc[p0][1], 0, 0, 0);
+      acc[p1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wdef[j].z, tdef[2 * j + 1], acc[p1][0], 0, 0, 0);
+      acc[p1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wdef[j].w, tdef[2 * j + 1], acc[p1][1], 0, 0, 0);
+    }
+  };
+  auto compute = [&](const float* pbuf, auto&& hw, auto&& hp, auto DEFc) {
+    constexpr bool DEF = decltype(DEFc)::value;
     {
       const float* wq = pbuf + kW4SPATCH + ph * 9 * 256 + lane * 4;
       float4 w4[9];
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        w4[q] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
-                           : *reinterpret_cast<const float4*>(wq + q * 256);
+        if (!(DEF && q >= kQD))
+          w4[q] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
+                             : *reinterpret_cast<const float4*>(wq + q * 256);
       // input rows ph .. ph + 4 of this lane's 6x6 window
       const float* pr = pbuf + k * kW4CS + (4 * wr + ph) * kW4PS + 4 * tn;
       float d[5][6];
@@ -402,15 +506,22 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         if (!(DBG & 8)) bt6(t[i][0], t[i][1], t[i][2], t[i][3], t[i][4], t[i][5]);
 #pragma unroll
       for (int q = 0; q < 9; ++q) {
-        if (q + 3 < 9)
+        if (q + 3 < 9 && !(DEF && q + 3 >= kQD))
           w4[q + 3] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
                                  : *reinterpret_cast<const float4*>(wq + (q + 3) * 256);
         const int p0 = 2 * q, p1 = 2 * q + 1;
         const float v0 = t[p0 / 6][p0 % 6], v1 = t[p1 / 6][p1 % 6];
+        if (DEF && q >= kQD) {
+          tdef[2 * (q - kQD)] = v0;
+          tdef[2 * (q - kQD) + 1] = v1;
+          continue;
+        }
         acc[p0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].x, v0, acc[p0][0], 0, 0, 0);
         acc[p0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].y, v0, acc[p0][1], 0, 0, 0);
         acc[p1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].z, v1, acc[p1][0], 0, 0, 0);
         acc[p1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].w, v1, acc[p1][1], 0, 0, 0);
+        if (q == kHW) hw();
+        if (q == kHP) hp();
       }
     }
   };
@@ -446,19 +557,44 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   };
 
   // bias, activation, store and the optional per-wave statistics of one finished tile:
-  // channel co of tile (wr, tn)
-  const int gy0 = y0 + 4 * wr, gx0 = x0 + 4 * tn;
-  const bool vec = (a.W & 3) == 0 && gx0 + 3 < a.W;
-  const int rows = max(0, min(4, a.H - gy0)), cols = max(0, min(kW4TW, a.W - x0));
-  const float inv = rows * cols > 0 ? 1.f / (float)(rows * cols) : 0.f;
+  // channel co of tile (wr, tn). Everything it needs besides the tile is re-derived per
+  // epilogue from the kernel arguments (EpiCtx): nothing of it stays live across the main
+  // loop, whose scalar registers are full (a spilled SGPR costs a VALU readlane per use)
+  auto epi_ctx = [&]() {
+    const KArgs L = late_args();
+    EpiCtx e;
+    e.W = L->W;
+    e.H = L->H;
+    e.Cout = L->Cout;
+    e.relu = L->relu;
+    int b = xcd_swizzle(blockIdx.x, (int)gridDim.x) / L->cosplit;
+    const int btx = b % L->tiles_x;
+    b /= L->tiles_x;
+    const int bty = b % L->tiles_y;
+    e.n = b / L->tiles_y;
+    const int bx0 = btx * kW4TW;
+    e.gy0 = bty * kW4TH + 4 * wr;
+    e.gx0 = bx0 + 4 * tn;
+    e.vec = (e.W & 3) == 0 && e.gx0 + 3 < e.W;
+    e.rows = max(0, min(4, e.H - e.gy0));
+    const int cols = max(0, min(kW4TW, e.W - bx0));
+    e.inv = e.rows * cols > 0 ? 1.f / (float)(e.rows * cols) : 0.f;
+    e.out = L->out;
+    e.btab = L->btab;
+    e.statp = L->stat_part;
+    e.statP = L->stat_P;
+    e.sidx = (bty * L->tiles_x + btx) * 4 + wr;
+    return e;
+  };
   // bv: the layer's bias of channel co (loaded by the caller ahead of time)
-  auto finish = [&](int co, float bv, float (&Y)[16]) {
-    const bool cok = co < a.Cout;
+  auto finish = [&](const EpiCtx& e, int co, float bv, float (&Y)[16]) {
+    const int gy0 = e.gy0, gx0 = e.gx0, rows = e.rows, n = e.n;
+    const bool cok = co < e.Cout;
     // folded AdaIN / WCT: the bias depends on which taps of the zero-padded input were
     // inside the image (border class); interior tiles take the interior entry
-    const float* bt = BTAB ? a.btab + ((int64_t)n * a.Cout + (cok ? co : 0)) * 9 : nullptr;
+    const float* bt = BTAB ? e.btab + ((int64_t)n * e.Cout + (cok ? co : 0)) * 9 : nullptr;
     if (BTAB) bv = cok ? bt[4] : 0.f;
-    const bool edge = BTAB && (gy0 == 0 || gy0 + 4 >= a.H || gx0 == 0 || gx0 + 4 >= a.W);
+    const bool edge = BTAB && (gy0 == 0 || gy0 + 4 >= e.H || gx0 == 0 || gx0 + 4 >= e.W);
 #pragma unroll
     for (int yy = 0; yy < 4; ++yy)
 #pragma unroll
@@ -466,39 +602,39 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         float b = bv;
         if (BTAB && edge) {
           const int gy = gy0 + yy, gx = gx0 + xx;
-          const int rc = gy == 0 ? 0 : (gy >= a.H - 1 ? 2 : 1);
-          const int cc = gx == 0 ? 0 : (gx >= a.W - 1 ? 2 : 1);
+          const int rc = gy == 0 ? 0 : (gy >= e.H - 1 ? 2 : 1);
+          const int cc = gx == 0 ? 0 : (gx >= e.W - 1 ? 2 : 1);
           b = cok ? bt[rc * 3 + cc] : 0.f;
         }
         Y[yy * 4 + xx] += b;
       }
     // the activation mode is uniform: one branch per tile, not per element
-    if (a.relu == RPST_ACT_RELU) {
+    if (e.relu == RPST_ACT_RELU) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) Y[e] = fmaxf(Y[e], 0.f);
-    } else if (a.relu == RPST_ACT_LRELU) {
+      for (int i = 0; i < 16; ++i) Y[i] = fmaxf(Y[i], 0.f);
+    } else if (e.relu == RPST_ACT_LRELU) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) Y[e] = Y[e] > 0.f ? Y[e] : Y[e] * 0.2f;
+      for (int i = 0; i < 16; ++i) Y[i] = Y[i] > 0.f ? Y[i] : Y[i] * 0.2f;
     }
     float sum = 0.f;
     if (STATS) {
 #pragma unroll
       for (int yy = 0; yy < 4; ++yy)
 #pragma unroll
-        for (int xx = 0; xx < 4; ++xx) sum += (yy < rows && gx0 + xx < a.W) ? Y[yy * 4 + xx] : 0.f;
+        for (int xx = 0; xx < 4; ++xx) sum += (yy < rows && gx0 + xx < e.W) ? Y[yy * 4 + xx] : 0.f;
     }
     if (cok) {
-      float* o = a.out + (((int64_t)n * a.Cout + co) * a.H + gy0) * a.W + gx0;
+      float* o = e.out + (((int64_t)n * e.Cout + co) * e.H + gy0) * e.W + gx0;
 #pragma unroll
       for (int yy = 0; yy < 4; ++yy) {
         if (yy < rows) {
-          if (vec) {
-            *reinterpret_cast<float4*>(o + yy * a.W) =
+          if (e.vec) {
+            *reinterpret_cast<float4*>(o + yy * e.W) =
                 make_float4(Y[yy * 4], Y[yy * 4 + 1], Y[yy * 4 + 2], Y[yy * 4 + 3]);
           } else {
 #pragma unroll
             for (int xx = 0; xx < 4; ++xx)
-              if (gx0 + xx < a.W) o[yy * a.W + xx] = Y[yy * 4 + xx];
+              if (gx0 + xx < e.W) o[yy * e.W + xx] = Y[yy * 4 + xx];
           }
         }
       }
@@ -506,20 +642,19 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     if constexpr (STATS) {
 #pragma unroll
       for (int m = 1; m < 16; m <<= 1) sum += __shfl_xor(sum, m, 64);
-      const float mean = sum * inv;
+      const float mean = sum * e.inv;
       float m2 = 0.f;
 #pragma unroll
       for (int yy = 0; yy < 4; ++yy)
 #pragma unroll
         for (int xx = 0; xx < 4; ++xx) {
           const float dv = Y[yy * 4 + xx] - mean;
-          m2 += (yy < rows && gx0 + xx < a.W) ? dv * dv : 0.f;
+          m2 += (yy < rows && gx0 + xx < e.W) ? dv * dv : 0.f;
         }
 #pragma unroll
       for (int m = 1; m < 16; m <<= 1) m2 += __shfl_xor(m2, m, 64);
       if (tn == 0 && cok)
-        a.stat_part[((int64_t)n * a.Cout + co) * a.stat_P + (ty * a.tiles_x + tx) * 4 + wr] =
-            make_float2(mean, m2);
+        e.statp[((int64_t)n * e.Cout + co) * e.statP + e.sidx] = make_float2(mean, m2);
     }
   };
 
@@ -529,7 +664,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // barriers (LDS only): the DMA prefetch of the next steps stays in flight.
   auto lds_barrier = [&]() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!(DBG & 16)) __builtin_amdgcn_s_barrier();
   };
   // PH = ph: the half this wave finishes is channel half PH; it hands the other half's
   // partial tile to its partner wave
@@ -538,11 +673,14 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     lds_barrier();  // every wave is done reading the stage
     float* xb = xs + wr * 2048;
     // the four biases this wave applies, loaded once ahead of the passes
+    const EpiCtx e = epi_ctx();
     const int co0 = ct * kW4BM + 16 * PH + 4 * k;
     float bias4[4];
+    if (!BTAB) {
+      const float* bias = late_args()->bias;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      bias4[r] = (!BTAB && a.bias && co0 + r < a.Cout) ? a.bias[co0 + r] : 0.f;
+      for (int r = 0; r < 4; ++r) bias4[r] = (bias && co0 + r < e.Cout) ? bias[co0 + r] : 0.f;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float own[16];
@@ -565,7 +703,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         own[4 * g4 + 2] += o4.z;
         own[4 * g4 + 3] += o4.w;
       }
-      finish(co0 + r, bias4[r], own);
+      finish(e, co0 + r, BTAB ? 0.f : bias4[r], own);
       if (r < 3) lds_barrier();  // the next pass overwrites the exchange region
     }
   };
@@ -580,28 +718,76 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // that opens step g is one constant: the groups of steps g + 1, g + 2 stay in flight
   // (ADAIN's register loads drain everything at their use, so the count stays conservative).
   auto wait_ahead2 = [&]() {
+    if (DBG & 128) return;
     if (wide) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // 2 x (3 + 3)
     else asm volatile("s_waitcnt vmcnt(26)" ::: "memory");       // 2 x (3 + kSlow)
   };
+  // RPST_W4_STAG: step g - 1 issued [w(g + 1), p(g + 2)], step g - 2 [w(g), p(g + 1)]: the
+  // weights of g have landed once only p(g + 1), w(g + 1), p(g + 2) may be outstanding
+  auto wait_step = [&]() {
+#if RPST_W4_STAG
+    if (DBG & 128) return;
+    if (wide) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");   // 3 + 3 + 3
+    else asm volatile("s_waitcnt vmcnt(23)" ::: "memory");       // kSlow + 3 + kSlow
+#else
+    wait_ahead2();
+#endif
+  };
+#if RPST_W4_STAG
+  // groups [w(g + 2), p(g + 3)] from step g on; the prologue issues the same shape:
+  // [w(-1) (out of range, zeros into stage 3's weights: w(3) follows at step 1), p(0)],
+  // [w(0), p(1)], [w(1), p(2)], so every counted wait is one constant
+  issue_w(0, false, smem3);
+  issue_p(0, true, smem0);
+  issue_w(0, true, smem0);
+  issue_p(1 % K4, G > 1, smem1);
+  issue_w(1, G > 1, smem1);
+  issue_p(2 % K4, G > 2, smem2);
+#else
   issue(0, 0, true, smem0);
   issue(1, 1 % K4, G > 1, smem1);
+#if !RPST_W4_PAIR
   issue(2, 2 % K4, G > 2, smem2);
+#endif
+#endif
   int ks3 = 3 % K4;          // chunk step of g + 3
   int ks = 0, ct = ct0;      // chunk step and co tile of g
   if constexpr (kAff) {  // step 0's affine (published by the first step's barrier)
+#if RPST_W4_PAIR
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    fix_own(0, smem0);
+    fix_own(1, smem1);
+#else
     wait_ahead2();
     fix_own(0, smem0);
+#endif
   }
   // K step g from stage `cur`; step g + 3's DMA into `nx3` (the stage step g - 1 used);
   // ADAIN: step g + 1's affine on this wave's own pieces in `nx1`, after the MFMAs
-  auto step = [&](int g, float* cur, float* nx1, float* nx3) {
-    wait_ahead2();
+  auto step = [&](int g, float* cur, float* nx1, float* nx2, float* nx3) {
+    (void)nx2;
+    wait_step();
     lds_barrier();  // step g's stage is complete; nx3 is free
-    issue(g + 3, ks3, g + 3 < G, nx3);
+    const bool live3 = g + 3 < G;
+#if RPST_W4_STAG
+    if (ph && ks != 0) mma_def(nx3);  // step g - 1's deferred pairs (none after an epilogue)
+    issue_w(g + 2, g + 2 < G, nx2);
+    issue_p(ks3, live3, nx3);
+#else
+    if constexpr (kHW < 0) issue_w(g + 3, live3, nx3);
+    if constexpr (kHP < 0) issue_p(ks3, live3, nx3);
+#endif
+    auto hw = [&]() { if constexpr (kHW >= 0) issue_w(g + 3, live3, nx3); };
+    auto hp = [&]() { if constexpr (kHP >= 0) issue_p(ks3, live3, nx3); };
+#if RPST_W4_STAG
+    if (ph && ks != K4 - 1) compute(cur, hw, hp, std::true_type{});
+    else compute(cur, hw, hp, std::false_type{});
+#else
+    compute(cur, hw, hp, std::false_type{});
+#endif
     ks3 = ks3 + 1 == K4 ? 0 : ks3 + 1;
-    compute(cur);
     if (ks == K4 - 1) {
-      epilogue(ct, cur);
+      if (!(DBG & 32)) epilogue(ct, cur);
 #pragma unroll
       for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
@@ -614,12 +800,47 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     ct += ks == K4 - 1 ? 1 : 0;
     ks = ks == K4 - 1 ? 0 : ks + 1;
   };
+#if RPST_W4_PAIR
+  // one barrier per PAIR of K steps (G is even: K4 = 2 nch): the barrier before step g
+  // (even) publishes steps g and g + 1 and frees the stages of g - 2, g - 1, which then take
+  // the DMA of g + 2, g + 3 (one pair ahead, so the wait drains everything: vmcnt(0))
+  (void)step;
+  auto pair = [&](int g, float* c0, float* c1, float* n0, float* n1) {
+    if (!(DBG & 128)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    issue(g + 2, ks3 == 0 ? K4 - 1 : ks3 - 1, g + 2 < G, n0);
+    issue(g + 3, ks3, g + 3 < G, n1);
+    ks3 = ks3 + 2 >= K4 ? ks3 + 2 - K4 : ks3 + 2;
+    compute(c0, [] {}, [] {}, std::false_type{});
+    ks += 1;  // g even, K4 even: never the last step of a co tile
+    compute(c1, [] {}, [] {}, std::false_type{});
+    if (ks == K4 - 1) {
+      if (!(DBG & 32)) epilogue(ct, c1);
+#pragma unroll
+      for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    if constexpr (kAff) {
+      if (g + 2 < G) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        fix_own(g + 2, n0);
+        fix_own(g + 3, n1);
+      }
+    }
+    ct += ks == K4 - 1 ? 1 : 0;
+    ks = ks == K4 - 1 ? 0 : ks + 1;
+  };
   for (int g = 0; g < G; g += kW4STG) {
-    step(g, smem0, smem1, smem3);
-    if (g + 1 < G) step(g + 1, smem1, smem2, smem0);
-    if (g + 2 < G) step(g + 2, smem2, smem3, smem1);
-    if (g + 3 < G) step(g + 3, smem3, smem0, smem2);
+    pair(g, smem0, smem1, smem2, smem3);
+    if (g + 2 < G) pair(g + 2, smem2, smem3, smem0, smem1);
   }
+#else
+  for (int g = 0; g < G; g += kW4STG) {
+    step(g, smem0, smem1, smem2, smem3);
+    if (g + 1 < G) step(g + 1, smem1, smem2, smem3, smem0);
+    if (g + 2 < G) step(g + 2, smem2, smem3, smem0, smem1);
+    if (g + 3 < G) step(g + 3, smem3, smem0, smem1, smem2);
+  }
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the padding DMA has landed too
 }
 
@@ -809,7 +1030,17 @@ int wino4_launch(ConvArgs& a, int in_op, hipStream_t st) {
   }
   RPST_REQUIRE((int64_t)a.co_tiles * a.nchunks * kW4WCH * 4 < (1LL << 31),
                "conv2d: winograd4 weight image exceeds 2 GiB");
-  const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.N;
+  {
+    // blocks per spatial tile: 2 once a co tile has >= 32 K steps (Cin >= 128) and there
+    // are >= 4 co tiles (the shorter blocks' prologue then costs less than the L2 reuse of
+    // the shared patch gains); RPST_WINO4_COSPLIT overrides (A/B)
+    const char* e = getenv("RPST_WINO4_COSPLIT");
+    int c = (e && *e) ? atoi(e) : (2 * a.nchunks >= 32 && a.co_tiles >= 4 ? 2 : 1);
+    c = c < 1 ? 1 : (c > a.co_tiles ? a.co_tiles : c);
+    while (a.co_tiles % c) --c;
+    a.cosplit = c;
+  }
+  const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.N * a.cosplit;
   RPST_REQUIRE(blocks <= 0x7fffffffLL, "conv2d: grid too large");
   const unsigned nb = (unsigned)blocks;
   const bool stats = a.stat_part != nullptr, btab = a.btab != nullptr;
