@@ -160,10 +160,13 @@ int wino4_persist() { return 1; }  // one block per spatial tile loops over the 
 // B^T row transform of one 6-vector (in place): the shared terms of rows (1,2) and (3,4)
 // what the F(4x4) epilogue needs besides the tile (wino4_mfma_kernel's epi_ctx)
 struct EpiCtx {
-  int W, H, Cout, relu, gy0, gx0, rows, n, sidx, statP;
-  bool vec;
-  float inv;
+  int W, H, Cout, gy0, gx0, rows, n, sidx, statP;
+  bool vec, full, bst, edge;
+  float inv, slope;      // slope: the activation as max(y, slope y): 0 ReLU, 0.2 LReLU, 1 none
+  unsigned voff[4];      // bst: byte offset of output row yy inside a channel plane (or OOB)
   float* out;
+  float* oimg;           // bst: image n's output planes, obytes bytes
+  unsigned obytes;
   const float* btab;
   float2* statp;
 };
@@ -181,6 +184,15 @@ __device__ __forceinline__ KArgs late_args() {
 // buffer resource over `bytes` at p, or over zero records (every access reads 0) if !ok
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_or_zero(const float* p, unsigned bytes, bool ok) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, ok ? (int)bytes : 0, 0x00020000);
+}
+// sum over the 16 lanes of a DPP row, in every lane: four DPP adds (quad xor 1, quad xor 2,
+// half-row mirror, row mirror) instead of four ds_bpermute round trips through the LDS
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
 }
 // a wave-uniform value made opaque at this point (not hoisted out of the enclosing loop)
 __device__ __forceinline__ int launder(int v) {
@@ -343,6 +355,9 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     }
     __syncthreads();
   }
+  floatx4 acc[18][2];
+#pragma unroll
+  for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // K step g (co tile ct0 + g / K4, channels 4 (g % K4)..+3): weight slice (18 pieces of
   // 1 KiB, pieces w, w + 8, w + 16 of wave w) and patch into its stage by LDS-DMA; every
@@ -425,9 +440,6 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     }
   };
 
-  floatx4 acc[18][2];
-#pragma unroll
-  for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // one K step of 4 channels from a stage: 72 VALU of input transform + 36 MFMAs
   // hw / hp: called after MFMA pair kHW / kHP (RPST_W4VAR placement experiments)
@@ -566,7 +578,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     e.W = L->W;
     e.H = L->H;
     e.Cout = L->Cout;
-    e.relu = L->relu;
+    e.slope = L->relu == RPST_ACT_RELU ? 0.f : (L->relu == RPST_ACT_LRELU ? 0.2f : 1.f);
     int b = xcd_swizzle(blockIdx.x, (int)gridDim.x) / L->cosplit;
     const int btx = b % L->tiles_x;
     b /= L->tiles_x;
@@ -579,7 +591,21 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     e.rows = max(0, min(4, e.H - e.gy0));
     const int cols = max(0, min(kW4TW, e.W - bx0));
     e.inv = e.rows * cols > 0 ? 1.f / (float)(e.rows * cols) : 0.f;
+    e.full = e.rows == 4 && bx0 + kW4TW <= e.W;
+    // some output of the wave is on the first / last image row or column (BTAB classes)
+    e.edge = e.gy0 == 0 || e.gy0 + 4 >= e.H || bx0 == 0 || bx0 + kW4TW >= e.W;
     e.out = L->out;
+    // buffer stores (soffset = channel plane, voffset = row offset; rows past H get an
+    // out-of-range offset, so no store needs a mask) when the float4 path applies to every
+    // lane of the layer and one image's output fits 2^31 bytes
+    const int64_t plane = (int64_t)e.H * e.W;
+    e.bst = (e.W & 3) == 0 && (int64_t)e.Cout * plane * 4 < (1LL << 31);
+    e.oimg = e.out + (int64_t)e.n * e.Cout * plane;
+    e.obytes = (unsigned)(e.Cout * plane * 4);
+#pragma unroll
+    for (int yy = 0; yy < 4; ++yy)
+      e.voff[yy] = (yy < e.rows && e.gx0 < e.W) ? (unsigned)(((e.gy0 + yy) * e.W + e.gx0) * 4)
+                                               : 0x80000000u;
     e.btab = L->btab;
     e.statp = L->stat_part;
     e.statP = L->stat_P;
@@ -593,37 +619,58 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     // folded AdaIN / WCT: the bias depends on which taps of the zero-padded input were
     // inside the image (border class); interior tiles take the interior entry
     const float* bt = BTAB ? e.btab + ((int64_t)n * e.Cout + (cok ? co : 0)) * 9 : nullptr;
-    if (BTAB) bv = cok ? bt[4] : 0.f;
-    const bool edge = BTAB && (gy0 == 0 || gy0 + 4 >= e.H || gx0 == 0 || gx0 + 4 >= e.W);
+    if (BTAB && e.edge) {
+      // a wave touching the image border: the nine class biases of co in registers, the
+      // row class uniform per output row, the column class per lane
+      float b9[9];
 #pragma unroll
-    for (int yy = 0; yy < 4; ++yy)
+      for (int i = 0; i < 9; ++i) b9[i] = cok ? bt[i] : 0.f;
 #pragma unroll
-      for (int xx = 0; xx < 4; ++xx) {
-        float b = bv;
-        if (BTAB && edge) {
-          const int gy = gy0 + yy, gx = gx0 + xx;
-          const int rc = gy == 0 ? 0 : (gy >= e.H - 1 ? 2 : 1);
-          const int cc = gx == 0 ? 0 : (gx >= e.W - 1 ? 2 : 1);
-          b = cok ? bt[rc * 3 + cc] : 0.f;
+      for (int yy = 0; yy < 4; ++yy) {
+        const int gy = gy0 + yy;
+        const int rc = gy == 0 ? 0 : (gy >= e.H - 1 ? 2 : 1);
+        const float l = rc == 0 ? b9[0] : (rc == 2 ? b9[6] : b9[3]);
+        const float m = rc == 0 ? b9[1] : (rc == 2 ? b9[7] : b9[4]);
+        const float r = rc == 0 ? b9[2] : (rc == 2 ? b9[8] : b9[5]);
+#pragma unroll
+        for (int xx = 0; xx < 4; ++xx) {
+          const int gx = gx0 + xx;
+          Y[yy * 4 + xx] += gx == 0 ? l : (gx >= e.W - 1 ? r : m);
         }
-        Y[yy * 4 + xx] += b;
       }
-    // the activation mode is uniform: one branch per tile, not per element
-    if (e.relu == RPST_ACT_RELU) {
+    } else {
+      if (BTAB) bv = cok ? bt[4] : 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) Y[i] = fmaxf(Y[i], 0.f);
-    } else if (e.relu == RPST_ACT_LRELU) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) Y[i] = Y[i] > 0.f ? Y[i] : Y[i] * 0.2f;
+      for (int i = 0; i < 16; ++i) Y[i] += bv;
     }
+    // activation, branch-free: max(y, slope y) as one v_med3 (fmaxf would add a NaN
+    // canonicalisation per element)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Y[i] = __builtin_amdgcn_fmed3f(Y[i], e.slope * Y[i], __builtin_inff());
     float sum = 0.f;
     if (STATS) {
+      if (e.full) {
 #pragma unroll
-      for (int yy = 0; yy < 4; ++yy)
+        for (int i = 0; i < 16; ++i) sum += Y[i];
+      } else {
 #pragma unroll
-        for (int xx = 0; xx < 4; ++xx) sum += (yy < rows && gx0 + xx < e.W) ? Y[yy * 4 + xx] : 0.f;
+        for (int yy = 0; yy < 4; ++yy)
+#pragma unroll
+          for (int xx = 0; xx < 4; ++xx) sum += (yy < rows && gx0 + xx < e.W) ? Y[yy * 4 + xx] : 0.f;
+      }
     }
-    if (cok) {
+    if (e.bst) {
+      // the channel (per lane: co depends on the lane's k) goes into the per-lane offset;
+      // co >= Cout or a row past H lands in [2^31 - 1, 2^32): out of range, dropped
+      const auto ro = rsrc_or_zero(e.oimg, e.obytes, true);
+      const unsigned cofs = cok ? (unsigned)co * (unsigned)(e.H * e.W) * 4u : 0x7fffffffu;
+#pragma unroll
+      for (int yy = 0; yy < 4; ++yy) {
+        const floatx4 v = {Y[yy * 4], Y[yy * 4 + 1], Y[yy * 4 + 2], Y[yy * 4 + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro,
+                                               (int)(e.voff[yy] + cofs), 0, 0);
+      }
+    } else if (cok) {
       float* o = e.out + (((int64_t)n * e.Cout + co) * e.H + gy0) * e.W + gx0;
 #pragma unroll
       for (int yy = 0; yy < 4; ++yy) {
@@ -640,19 +687,22 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
       }
     }
     if constexpr (STATS) {
-#pragma unroll
-      for (int m = 1; m < 16; m <<= 1) sum += __shfl_xor(sum, m, 64);
+      sum = row16_sum(sum);
       const float mean = sum * e.inv;
       float m2 = 0.f;
+      if (e.full) {
 #pragma unroll
-      for (int yy = 0; yy < 4; ++yy)
+        for (int i = 0; i < 16; ++i) m2 = fmaf(Y[i] - mean, Y[i] - mean, m2);
+      } else {
 #pragma unroll
-        for (int xx = 0; xx < 4; ++xx) {
-          const float dv = Y[yy * 4 + xx] - mean;
-          m2 += (yy < rows && gx0 + xx < e.W) ? dv * dv : 0.f;
-        }
+        for (int yy = 0; yy < 4; ++yy)
 #pragma unroll
-      for (int m = 1; m < 16; m <<= 1) m2 += __shfl_xor(m2, m, 64);
+          for (int xx = 0; xx < 4; ++xx) {
+            const float dv = Y[yy * 4 + xx] - mean;
+            m2 += (yy < rows && gx0 + xx < e.W) ? dv * dv : 0.f;
+          }
+      }
+      m2 = row16_sum(m2);
       if (tn == 0 && cok)
         e.statp[((int64_t)n * e.Cout + co) * e.statP + e.sidx] = make_float2(mean, m2);
     }
@@ -675,7 +725,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     // the four biases this wave applies, loaded once ahead of the passes
     const EpiCtx e = epi_ctx();
     const int co0 = ct * kW4BM + 16 * PH + 4 * k;
-    float bias4[4];
+    float bias4[4] = {0.f, 0.f, 0.f, 0.f};
     if (!BTAB) {
       const float* bias = late_args()->bias;
 #pragma unroll
