@@ -20,15 +20,17 @@
 // n = lane & 15) reads 5 rows of its 6x6 input window from the LDS patch, forms its three
 // rows of V = B^T d B (72 VALU) and issues 36 v_mfma_f32_16x16x4_f32 (18 positions x 2
 // channel halves sharing each V value): A = U (LDS, one ds_read_b128 per 4 MFMAs).
-// Per chunk of 8 channels the next chunk's patch and weight slice stream into LDS by
-// LDS-DMA while this one computes (patch: 19 pieces of 64 floats per channel, per-lane
-// source offsets resolved against the padding once per block; weights: 36 pieces of
-// 1 KiB); one barrier per chunk. One block loops over the co tiles of its spatial tile.
+// Per K step the patch (4 channels x 18 rows x 68) and the weight slice (18 KiB) stream
+// into a 4-stage LDS ring by LDS-DMA three steps ahead (step g + 3 issued inside step g's
+// MFMA stream; per-lane patch offsets resolved against the padding once per block); one
+// counted vmcnt wait and one barrier per step. One block loops over the co tiles of its
+// spatial tile (split over two same-XCD blocks for Cin >= 128: a.cosplit).
 // The output transform splits like the positions: each wave applies A^T . A to its three
 // rows (a partial 4x4 tile), the two waves of a tile row swap the partials of the channel
 // half the other one finishes through LDS, and each adds, biases, activates and stores 16
-// channels. Measured against the alternatives (profiles/r01_wino4_variants.log): a 4-wave
-// one-per-SIMD software-pipelined form and register-staged patches were slower.
+// channels. The fp32 MFMA and the VALU do not co-execute on a SIMD (tools/coexec.hip), so
+// the design minimises VALU per MFMA; measured alternatives and their timings:
+// profiles/r01_wino4_variants.log, profiles/r02_wino4_variants.log.
 #include "rpst_conv.h"
 
 #include <type_traits>
@@ -279,9 +281,10 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int k = lane >> 4, tn = lane & 15;
   const int wr = wave & 3, ph = wave >> 2;  // tile row, transformed-row half
-  // static priority for the second-dispatched half (waves 4-7), the arbitration loser on
-  // every segment (MI355X_MICROARCH.md, two waves per SIMD, item 4); a.persist & 2 = A/B off
-  if (ph && !(a.persist & 2)) __builtin_amdgcn_s_setprio(1);
+  // optional static priority (a.persist & 2: waves 4-7, & 4: waves 0-3; RPST_WINO4_PRIO=1/2):
+  // with the DMA inside the MFMA stream, equal priorities measured fastest (128->256 28.47
+  // vs 28.75 ms with waves 4-7 at priority 1; profiles/r02_wino4_variants.log)
+  if ((ph && (a.persist & 2)) || (!ph && (a.persist & 4))) __builtin_amdgcn_s_setprio(1);
 
   const bool pooled = INOP == RPST_IN_UPSAMPLE2;
   const unsigned in_plane = pooled ? (unsigned)(a.Hs * a.Ws) : (unsigned)(a.H * a.W);
@@ -540,7 +543,9 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
 
   // this wave's partial output tile of channel half mt, accumulator element r:
   // sum over its transformed rows i = 3ph + i' of A^T[:, i] (M[i, :] A); PH = ph
-  auto partial = [&](auto PHc, int mt, int r, float (&Y)[16]) {
+  // b (PH = 0 only): the channel's bias, added to transformed row 1 after the column pass:
+  // column 1 of A^T is (1, 1, 1, 1), so it reaches all four output rows (4 adds, not 16)
+  auto partial = [&](auto PHc, int mt, int r, float (&Y)[16], float b) {
     constexpr int PH = decltype(PHc)::value;
     float P[3][4];
 #pragma unroll
@@ -549,6 +554,10 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int jj = 0; jj < 6; ++jj) m[jj] = acc[6 * i + jj][mt][r];
       at6(m, P[i]);
+    }
+    if constexpr (PH == 0) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) P[1][x] += b;
     }
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
@@ -612,8 +621,8 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     e.sidx = (bty * L->tiles_x + btx) * 4 + wr;
     return e;
   };
-  // bv: the layer's bias of channel co (loaded by the caller ahead of time)
-  auto finish = [&](const EpiCtx& e, int co, float bv, float (&Y)[16]) {
+  // the bias (interior class for BTAB) is already in Y (partial)
+  auto finish = [&](const EpiCtx& e, int co, float (&Y)[16]) {
     const int gy0 = e.gy0, gx0 = e.gx0, rows = e.rows, n = e.n;
     const bool cok = co < e.Cout;
     // folded AdaIN / WCT: the bias depends on which taps of the zero-padded input were
@@ -625,6 +634,9 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
       float b9[9];
 #pragma unroll
       for (int i = 0; i < 9; ++i) b9[i] = cok ? bt[i] : 0.f;
+      const float b4 = b9[4];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) b9[i] -= b4;  // the interior class went in with the partials
 #pragma unroll
       for (int yy = 0; yy < 4; ++yy) {
         const int gy = gy0 + yy;
@@ -638,15 +650,12 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
           Y[yy * 4 + xx] += gx == 0 ? l : (gx >= e.W - 1 ? r : m);
         }
       }
-    } else {
-      if (BTAB) bv = cok ? bt[4] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) Y[i] += bv;
     }
     // activation, branch-free: max(y, slope y) as one v_med3 (fmaxf would add a NaN
     // canonicalisation per element)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) Y[i] = __builtin_amdgcn_fmed3f(Y[i], e.slope * Y[i], __builtin_inff());
+    for (int i = 0; i < 16; ++i)
+      Y[i] = __builtin_amdgcn_fmed3f(Y[i], e.slope * Y[i], __builtin_inff());
     float sum = 0.f;
     if (STATS) {
       if (e.full) {
@@ -722,22 +731,29 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     constexpr int PH = decltype(PHc)::value;
     lds_barrier();  // every wave is done reading the stage
     float* xb = xs + wr * 2048;
-    // the four biases this wave applies, loaded once ahead of the passes
     const EpiCtx e = epi_ctx();
     const int co0 = ct * kW4BM + 16 * PH + 4 * k;
-    float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-    if (!BTAB) {
-      const float* bias = late_args()->bias;
+    // PH = 0 adds the biases of both channel halves (its own and the partner's partial),
+    // loaded once ahead of the passes: [half][r]
+    float bias8[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    if constexpr (PH == 0) {
+      const float* bias = BTAB ? nullptr : late_args()->bias;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bias4[r] = (bias && co0 + r < e.Cout) ? bias[co0 + r] : 0.f;
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = ct * kW4BM + 16 * h + 4 * k + r;
+          if (co < e.Cout)
+            bias8[h][r] = BTAB ? e.btab[((int64_t)e.n * e.Cout + co) * 9 + 4] : (bias ? bias[co] : 0.f);
+        }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float own[16];
       {
         float give[16];
-        partial(PHc, PH, r, own);
-        partial(PHc, 1 - PH, r, give);
+        partial(PHc, PH, r, own, bias8[0][r]);
+        partial(PHc, 1 - PH, r, give, bias8[1][r]);
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4)
           *reinterpret_cast<float4*>(xb + ((PH * 4 + g4) * 64 + lane) * 4) =
@@ -753,7 +769,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         own[4 * g4 + 2] += o4.z;
         own[4 * g4 + 3] += o4.w;
       }
-      finish(e, co0 + r, BTAB ? 0.f : bias4[r], own);
+      finish(e, co0 + r, own);
       if (r < 3) lds_barrier();  // the next pass overwrites the exchange region
     }
   };
@@ -1075,8 +1091,9 @@ int wino4_launch(ConvArgs& a, int in_op, hipStream_t st) {
   a.co_tiles = a.Cout_pad / kW4BM;
   a.stat_P = a.tiles_x * a.tiles_y * 4;
   {
-    const char* e = getenv("RPST_WINO4_NOPRIO");  // A/B switch for the static priority
-    a.persist = 1 | ((e && *e && atoi(e)) ? 2 : 0);
+    const char* e = getenv("RPST_WINO4_PRIO");  // A/B switch for a static priority
+    const int pr = (e && *e) ? atoi(e) : 0;
+    a.persist = 1 | (pr == 1 ? 2 : 0) | (pr == 2 ? 4 : 0);
   }
   RPST_REQUIRE((int64_t)a.co_tiles * a.nchunks * kW4WCH * 4 < (1LL << 31),
                "conv2d: winograd4 weight image exceeds 2 GiB");
