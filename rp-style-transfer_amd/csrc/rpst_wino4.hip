@@ -241,7 +241,7 @@ __device__ __forceinline__ bool resolve_bf(int& v, int n, bool zero_pad) {
 // border-class bias table (a.btab). Both are template arguments so a plain layer's
 // epilogue carries none of their VALU; the two transformed-row halves (ph, waves 0-3 and
 // 4-7) run epilogues specialised for their half.
-template <int INOP, bool STATS, bool BTAB>
+template <int INOP, bool STATS, bool BTAB, bool RELU>
 __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // timing-only experiments (results wrong; tools/build_variants.sh -DRPST_W4DBG=n): 1 no
   // patch DMA, 2 no weight DMA, 8 no input transform, 16 no barriers, 32 no epilogue,
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     // canonicalisation per element)
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      Y[i] = __builtin_amdgcn_fmed3f(Y[i], e.slope * Y[i], __builtin_inff());
+      Y[i] = __builtin_amdgcn_fmed3f(Y[i], RELU ? 0.f : e.slope * Y[i], __builtin_inff());
     float sum = 0.f;
     if (STATS) {
       if (e.full) {
@@ -1112,7 +1112,15 @@ int wino4_launch(ConvArgs& a, int in_op, hipStream_t st) {
   const unsigned nb = (unsigned)blocks;
   const bool stats = a.stat_part != nullptr, btab = a.btab != nullptr;
   RPST_REQUIRE(!btab || in_op == RPST_IN_NONE, "conv2d: winograd4 bias table with a loader op");
-#define RPST_W4_GO(OP, S, B) wino4_mfma_kernel<OP, S, B><<<nb, kW4NTH, 0, st>>>(a)
+  // RELU: the activation as one v_med3 per element (the RP stacks and VGG: every large
+  // layer); other activations run the general max(y, slope y) form
+#define RPST_W4_GO(OP, S, B)                                              \
+  do {                                                                    \
+    if (a.relu == RPST_ACT_RELU)                                          \
+      wino4_mfma_kernel<OP, S, B, true><<<nb, kW4NTH, 0, st>>>(a);        \
+    else                                                                  \
+      wino4_mfma_kernel<OP, S, B, false><<<nb, kW4NTH, 0, st>>>(a);       \
+  } while (0)
   switch (in_op) {
     case RPST_IN_ADAIN:
       if (stats) RPST_W4_GO(RPST_IN_ADAIN, true, false);
