@@ -52,15 +52,6 @@ constexpr int kW4CK = 8;                   // input channels per chunk
 #ifndef RPST_W4_HP
 #define RPST_W4_HP 2
 #endif
-#ifndef RPST_W4_PAIR
-#define RPST_W4_PAIR 0
-#endif
-#ifndef RPST_W4_STAG
-#define RPST_W4_STAG 0
-#endif
-#ifndef RPST_W4_QD
-#define RPST_W4_QD 5
-#endif
 constexpr int kW4BM = 32;                  // output channels per co tile
 constexpr int kW4TH = 16, kW4TW = 64;      // output rows x columns per block
 constexpr int kW4PH = kW4TH + 2;           // patch rows
@@ -446,52 +437,31 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
 
   // one K step of 4 channels from a stage: 72 VALU of input transform + 36 MFMAs
   // hw / hp: called after MFMA pair kHW / kHP (RPST_W4VAR placement experiments)
-  // RPST_W4_STAG: the ph = 1 waves (4-7, SIMD partners of waves 0-3) defer MFMA pairs
-  // q >= kQD of a step to after the next barrier (operands kept in registers), so on every
-  // SIMD one wave's deferred MFMAs run beside its partner's DMA issue, LDS reads and input
-  // transform; per accumulator the K order is unchanged (bit-identical results)
-  constexpr int kQD = RPST_W4_QD, kND = 9 - kQD;
-  float tdef[2 * kND];
-  // prv: the stage of the previous step (its weights stay until the next barrier: with
-  // RPST_W4_STAG the weight DMA runs two steps ahead, the patch DMA three)
-  [[maybe_unused]] auto mma_def = [&](const float* prv) {
-    const float* wq = prv + kW4SPATCH + 9 * 256 + lane * 4;
-    float4 wdef[kND];
+  // input rows ph .. ph + 4 of this lane's 6x6 window of one step
+  auto load_rows = [&](const float* pbuf, float (&d)[5][6]) {
+    const float* pr = pbuf + k * kW4CS + (4 * wr + ph) * kW4PS + 4 * tn;
 #pragma unroll
-    for (int j = 0; j < kND; ++j) wdef[j] = *reinterpret_cast<const float4*>(wq + (kQD + j) * 256);
-#pragma unroll
-    for (int j = 0; j < kND; ++j) {
-      const int p0 = 2 * (kQD + j), p1 = p0 + 1;
-      acc[p0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wdef[j].x, tdef[2 * j], acc[p0][0], 0, 0, 0);
-      acc[p0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wdef[j].y, tdef[2 * j], acc[p0][1], 0, 0, 0);
-      acc[p1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wdef[j].z, tdef[2 * j + 1], acc[p1][0], 0, 0, 0);
-      acc[p1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wdef[j].w, tdef[2 * j + 1], acc[p1][1], 0, 0, 0);
+    for (int r = 0; r < 5; ++r) {
+      const float4 u = *reinterpret_cast<const float4*>(pr + r * kW4PS);
+      const float2 v = *reinterpret_cast<const float2*>(pr + r * kW4PS + 4);
+      d[r][0] = u.x;
+      d[r][1] = u.y;
+      d[r][2] = u.z;
+      d[r][3] = u.w;
+      d[r][4] = v.x;
+      d[r][5] = v.y;
     }
   };
-  auto compute = [&](const float* pbuf, auto&& hw, auto&& hp, auto DEFc) {
-    constexpr bool DEF = decltype(DEFc)::value;
+  // one K step of 4 channels from a stage (its rows already in d): 72 VALU of input
+  // transform + 36 MFMAs; hw / hp run after MFMA pair kHW / kHP (the DMA of step g + 3)
+  auto compute = [&](const float* pbuf, float (&d)[5][6], auto&& hw, auto&& hp) {
     {
       const float* wq = pbuf + kW4SPATCH + ph * 9 * 256 + lane * 4;
       float4 w4[9];
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        if (!(DEF && q >= kQD))
-          w4[q] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
-                             : *reinterpret_cast<const float4*>(wq + q * 256);
-      // input rows ph .. ph + 4 of this lane's 6x6 window
-      const float* pr = pbuf + k * kW4CS + (4 * wr + ph) * kW4PS + 4 * tn;
-      float d[5][6];
-#pragma unroll
-      for (int r = 0; r < 5; ++r) {
-        const float4 u = *reinterpret_cast<const float4*>(pr + r * kW4PS);
-        const float2 v = *reinterpret_cast<const float2*>(pr + r * kW4PS + 4);
-        d[r][0] = u.x;
-        d[r][1] = u.y;
-        d[r][2] = u.z;
-        d[r][3] = u.w;
-        d[r][4] = v.x;
-        d[r][5] = v.y;
-      }
+        w4[q] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
+                           : *reinterpret_cast<const float4*>(wq + q * 256);
       // rows 3ph..3ph+2 of B^T d (d[r] = input row ph + r), then B along each row
       float t[3][6];
       if (DBG & 8) {
@@ -521,16 +491,11 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
         if (!(DBG & 8)) bt6(t[i][0], t[i][1], t[i][2], t[i][3], t[i][4], t[i][5]);
 #pragma unroll
       for (int q = 0; q < 9; ++q) {
-        if (q + 3 < 9 && !(DEF && q + 3 >= kQD))
+        if (q + 3 < 9)
           w4[q + 3] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
                                  : *reinterpret_cast<const float4*>(wq + (q + 3) * 256);
         const int p0 = 2 * q, p1 = 2 * q + 1;
         const float v0 = t[p0 / 6][p0 % 6], v1 = t[p1 / 6][p1 % 6];
-        if (DEF && q >= kQD) {
-          tdef[2 * (q - kQD)] = v0;
-          tdef[2 * (q - kQD) + 1] = v1;
-          continue;
-        }
         acc[p0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].x, v0, acc[p0][0], 0, 0, 0);
         acc[p0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].y, v0, acc[p0][1], 0, 0, 0);
         acc[p1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].z, v1, acc[p1][0], 0, 0, 0);
@@ -788,69 +753,30 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     if (wide) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // 2 x (3 + 3)
     else asm volatile("s_waitcnt vmcnt(26)" ::: "memory");       // 2 x (3 + kSlow)
   };
-  // RPST_W4_STAG: step g - 1 issued [w(g + 1), p(g + 2)], step g - 2 [w(g), p(g + 1)]: the
-  // weights of g have landed once only p(g + 1), w(g + 1), p(g + 2) may be outstanding
-  auto wait_step = [&]() {
-#if RPST_W4_STAG
-    if (DBG & 128) return;
-    if (wide) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");   // 3 + 3 + 3
-    else asm volatile("s_waitcnt vmcnt(23)" ::: "memory");       // kSlow + 3 + kSlow
-#else
-    wait_ahead2();
-#endif
-  };
-#if RPST_W4_STAG
-  // groups [w(g + 2), p(g + 3)] from step g on; the prologue issues the same shape:
-  // [w(-1) (out of range, zeros into stage 3's weights: w(3) follows at step 1), p(0)],
-  // [w(0), p(1)], [w(1), p(2)], so every counted wait is one constant
-  issue_w(0, false, smem3);
-  issue_p(0, true, smem0);
-  issue_w(0, true, smem0);
-  issue_p(1 % K4, G > 1, smem1);
-  issue_w(1, G > 1, smem1);
-  issue_p(2 % K4, G > 2, smem2);
-#else
   issue(0, 0, true, smem0);
   issue(1, 1 % K4, G > 1, smem1);
-#if !RPST_W4_PAIR
   issue(2, 2 % K4, G > 2, smem2);
-#endif
-#endif
   int ks3 = 3 % K4;          // chunk step of g + 3
   int ks = 0, ct = ct0;      // chunk step and co tile of g
   if constexpr (kAff) {  // step 0's affine (published by the first step's barrier)
-#if RPST_W4_PAIR
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    fix_own(0, smem0);
-    fix_own(1, smem1);
-#else
     wait_ahead2();
     fix_own(0, smem0);
-#endif
   }
   // K step g from stage `cur`; step g + 3's DMA into `nx3` (the stage step g - 1 used);
-  // ADAIN: step g + 1's affine on this wave's own pieces in `nx1`, after the MFMAs
-  auto step = [&](int g, float* cur, float* nx1, float* nx2, float* nx3) {
-    (void)nx2;
-    wait_step();
+  // ADAIN: step g + 1's affine on this wave's own pieces in `nx1`, after the MFMAs.
+  // (Reading the next step's rows one step ahead, under the MFMAs, needs 30 more VGPRs
+  // across the step: 650-1800 spills.)
+  auto step = [&](int g, float* cur, float* nx1, float* nx3) {
+    wait_ahead2();
     lds_barrier();  // step g's stage is complete; nx3 is free
+    float d[5][6];
+    load_rows(cur, d);
     const bool live3 = g + 3 < G;
-#if RPST_W4_STAG
-    if (ph && ks != 0) mma_def(nx3);  // step g - 1's deferred pairs (none after an epilogue)
-    issue_w(g + 2, g + 2 < G, nx2);
-    issue_p(ks3, live3, nx3);
-#else
     if constexpr (kHW < 0) issue_w(g + 3, live3, nx3);
     if constexpr (kHP < 0) issue_p(ks3, live3, nx3);
-#endif
     auto hw = [&]() { if constexpr (kHW >= 0) issue_w(g + 3, live3, nx3); };
     auto hp = [&]() { if constexpr (kHP >= 0) issue_p(ks3, live3, nx3); };
-#if RPST_W4_STAG
-    if (ph && ks != K4 - 1) compute(cur, hw, hp, std::true_type{});
-    else compute(cur, hw, hp, std::false_type{});
-#else
-    compute(cur, hw, hp, std::false_type{});
-#endif
+    compute(cur, d, hw, hp);
     ks3 = ks3 + 1 == K4 ? 0 : ks3 + 1;
     if (ks == K4 - 1) {
       if (!(DBG & 32)) epilogue(ct, cur);
@@ -866,47 +792,12 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     ct += ks == K4 - 1 ? 1 : 0;
     ks = ks == K4 - 1 ? 0 : ks + 1;
   };
-#if RPST_W4_PAIR
-  // one barrier per PAIR of K steps (G is even: K4 = 2 nch): the barrier before step g
-  // (even) publishes steps g and g + 1 and frees the stages of g - 2, g - 1, which then take
-  // the DMA of g + 2, g + 3 (one pair ahead, so the wait drains everything: vmcnt(0))
-  (void)step;
-  auto pair = [&](int g, float* c0, float* c1, float* n0, float* n1) {
-    if (!(DBG & 128)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    issue(g + 2, ks3 == 0 ? K4 - 1 : ks3 - 1, g + 2 < G, n0);
-    issue(g + 3, ks3, g + 3 < G, n1);
-    ks3 = ks3 + 2 >= K4 ? ks3 + 2 - K4 : ks3 + 2;
-    compute(c0, [] {}, [] {}, std::false_type{});
-    ks += 1;  // g even, K4 even: never the last step of a co tile
-    compute(c1, [] {}, [] {}, std::false_type{});
-    if (ks == K4 - 1) {
-      if (!(DBG & 32)) epilogue(ct, c1);
-#pragma unroll
-      for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
-    if constexpr (kAff) {
-      if (g + 2 < G) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        fix_own(g + 2, n0);
-        fix_own(g + 3, n1);
-      }
-    }
-    ct += ks == K4 - 1 ? 1 : 0;
-    ks = ks == K4 - 1 ? 0 : ks + 1;
-  };
   for (int g = 0; g < G; g += kW4STG) {
-    pair(g, smem0, smem1, smem2, smem3);
-    if (g + 2 < G) pair(g + 2, smem2, smem3, smem0, smem1);
+    step(g, smem0, smem1, smem3);
+    if (g + 1 < G) step(g + 1, smem1, smem2, smem0);
+    if (g + 2 < G) step(g + 2, smem2, smem3, smem1);
+    if (g + 3 < G) step(g + 3, smem3, smem0, smem2);
   }
-#else
-  for (int g = 0; g < G; g += kW4STG) {
-    step(g, smem0, smem1, smem2, smem3);
-    if (g + 1 < G) step(g + 1, smem1, smem2, smem3, smem0);
-    if (g + 2 < G) step(g + 2, smem2, smem3, smem0, smem1);
-    if (g + 3 < G) step(g + 3, smem3, smem0, smem1, smem2);
-  }
-#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the padding DMA has landed too
 }
 
