@@ -87,3 +87,15 @@ def checksum(arrs: Dict[str, np.ndarray]) -> Tuple[float, float]:
         s += float(a.sum())
         s2 += float((a * a).sum())
     return s, s2
+
+
+def conditioned_features(seed: int, C: int, HW: int, decades: float = 3.0) -> np.ndarray:
+    """(C, HW) float64 ReLU features conditioned like encoder activations: channel scales
+    spanning 10^-decades .. 1, neighbouring channels mixed, so the covariance's eigenvalues
+    spread over ~2 * decades decades (WCT goldens at C = 256 / 512). Elementwise only:
+    bit-identical on every machine."""
+    z = (2.0 * uniform01(seed, "wctfeat", C * HW).reshape(C, HW) - 1.0) * np.sqrt(3.0)
+    scale = 10.0 ** (-decades * np.arange(C, dtype=np.float64) / max(C - 1, 1))
+    x = scale[:, None] * (z + 0.3)
+    x[:-1] += 0.5 * x[1:]
+    return np.maximum(x, 0.0)

@@ -187,6 +187,32 @@ def gen_wct(net):
                         nnet=ncase, **out)
 
 
+def gen_wct_large(net):
+    """The WCT matrix functions and whiten_and_color at the widths WCTRPNet runs at
+    (C = 256: the RP encoder's output; 512: VGG relu4_1) on features conditioned like real
+    activations (synth.conditioned_features: the style covariance spans ~6 decades before
+    the reference's +1e-4). Outputs are stored as products with fixed +-1 probe matrices
+    (and the first 32 columns of the fused feature), which pins them without storing
+    C x C / C x HW fp64 arrays; the inputs are regenerated from the seeds."""
+    from network.wct_rp import matrix_inv_sqrt, matrix_sqrt
+    m = net.WCTRPNet(rp_config(2), copy.deepcopy(net.vgg))
+    out = {}
+    cases = [(256, 4096, 900), (512, 2048, 901)]
+    for i, (cdim, hw, seed) in enumerate(cases):
+        cf = synth.conditioned_features(seed, cdim, hw, 1.5)
+        sf = synth.conditioned_features(seed + 50, cdim, hw, 3.0)
+        sm = sf - sf.mean(1, keepdims=True)
+        a = sm @ sm.T / (hw - 1)  # the reference's style covariance (wct_rp.py:92-94)
+        pm = 2.0 * synth.uniform01(seed, "probe", cdim * 8).reshape(cdim, 8) - 1.0
+        ph = 2.0 * synth.uniform01(seed, "hwprobe", hw * 4).reshape(hw, 4) - 1.0
+        wc = m.whiten_and_color(t(cf), t(sf)).numpy()
+        out.update({f"C{i}": cdim, f"HW{i}": hw, f"seed{i}": seed,
+                    f"sqrtP{i}": matrix_sqrt(t(a)).numpy() @ pm,
+                    f"isqrtP{i}": matrix_inv_sqrt(t(a)).numpy() @ pm,
+                    f"wcP{i}": wc @ ph, f"wcCols{i}": wc[:, :32].copy()})
+    np.savez_compressed(os.path.join(HERE, "wct_large.npz"), ncase=len(cases), **out)
+
+
 def gen_sanet(net):
     from network.sanet import SANet, Transform, mean_variance_norm
     out = {}
@@ -459,7 +485,7 @@ GENERATORS = {"keys": gen_keys, "stats": gen_stats, "adain_rp": gen_adain_rp,
               "forward": gen_forward, "wct": gen_wct, "sanet": gen_sanet, "vgg": gen_vgg,
               "multiscale": gen_multiscale, "sourcenet": gen_sourcenet,
               "adaptive": gen_adaptive, "deeper": gen_deeper, "grads": gen_grads,
-              "grads_wct": gen_grads_wct}
+              "grads_wct": gen_grads_wct, "wct_large": gen_wct_large}
 
 
 def main():

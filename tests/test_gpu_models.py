@@ -122,6 +122,24 @@ def test_whiten_and_color_golden(cuda, golden):
         assert rel_l2(out, g[f"wc{i}"]) < 1e-10, (i, rel_l2(out, g[f"wc{i}"]))
 
 
+def test_wct_large_golden(cuda, golden):
+    """C = 256 / 512 on conditioned features (style covariance spanning ~6 decades): the
+    GPU Newton-Schulz powers and whiten_and_color against the reference's SVD-based
+    outputs (probe products, tests/golden/wct_large.npz)."""
+    import network as net
+    from test_oracle_golden import _wct_large_inputs
+    g = golden("wct_large")
+    m = net.WCTRPNet(rp_config(2), copy.deepcopy(net.vgg))
+    for i in range(int(g["ncase"])):
+        cf, sf, a, pm, ph = _wct_large_inputs(g, i)
+        ad = t(a).to(cuda)
+        assert rel_l2(net.matrix_sqrt(ad).cpu().numpy() @ pm, g[f"sqrtP{i}"]) < 1e-10, i
+        assert rel_l2(net.matrix_inv_sqrt(ad).cpu().numpy() @ pm, g[f"isqrtP{i}"]) < 1e-10, i
+        wc = m.whiten_and_color(t(cf).to(cuda), t(sf).to(cuda)).cpu().numpy()
+        assert rel_l2(wc @ ph, g[f"wcP{i}"]) < 1e-10, i
+        assert rel_l2(wc[:, :32], g[f"wcCols{i}"]) < 1e-10, i
+
+
 def test_wct_rp_test_golden(cuda, golden):
     import network as net
     g = golden("wct")

@@ -94,6 +94,32 @@ def test_wct_whiten_and_color(golden):
         assert rel_l2(out, g[f"wc{i}"]) < 1e-12
 
 
+def _wct_large_inputs(g, i):
+    from rpst import synth
+    c, hw, seed = int(g[f"C{i}"]), int(g[f"HW{i}"]), int(g[f"seed{i}"])
+    cf = synth.conditioned_features(seed, c, hw, 1.5)
+    sf = synth.conditioned_features(seed + 50, c, hw, 3.0)
+    sm = sf - sf.mean(1, keepdims=True)
+    a = sm @ sm.T / (hw - 1)
+    pm = 2.0 * synth.uniform01(seed, "probe", c * 8).reshape(c, 8) - 1.0
+    ph = 2.0 * synth.uniform01(seed, "hwprobe", hw * 4).reshape(hw, 4) - 1.0
+    return cf, sf, a, pm, ph
+
+
+def test_wct_large_reference(golden):
+    """C = 256 / 512 on conditioned features (reference outputs as probe products,
+    gen_golden.gen_wct_large): matrix functions of the style covariance and the fused
+    feature of whiten_and_color."""
+    g = golden("wct_large")
+    for i in range(int(g["ncase"])):
+        cf, sf, a, pm, ph = _wct_large_inputs(g, i)
+        assert rel_l2(R.matrix_sqrt(t(a)).numpy() @ pm, g[f"sqrtP{i}"]) < 1e-11, i
+        assert rel_l2(R.matrix_inv_sqrt(t(a)).numpy() @ pm, g[f"isqrtP{i}"]) < 1e-11, i
+        wc = R.whiten_and_color(t(cf), t(sf)).numpy()
+        assert rel_l2(wc @ ph, g[f"wcP{i}"]) < 1e-11, i
+        assert rel_l2(wc[:, :32], g[f"wcCols{i}"]) < 1e-11, i
+
+
 def test_wct_rp_test(golden):
     import network as net
     g = golden("wct")
