@@ -706,7 +706,9 @@ static int ns_power(const double* A, double add, double* sqrt_out, double* isqrt
   if (isqrt_out)
     ns_final_kernel<<<blocks, 256, 0, st>>>(buf0[1], buf1[1], isqrt_out, svec, stop, -0.5,
                                             (int64_t)n * n, batch);
-  if (res_out) hipMemcpyAsync(res_out, res, sizeof(double) * batch, hipMemcpyDeviceToDevice, st);
+  if (res_out)
+    RPST_REQUIRE(hipMemcpyAsync(res_out, res, sizeof(double) * batch, hipMemcpyDeviceToDevice,
+                                st) == hipSuccess, "newton-schulz: residual copy failed");
   return launch_status("newton-schulz");
 }
 
@@ -949,7 +951,8 @@ extern "C" int rpst_wct_params(const float* content, const float* style, const f
   const WctLayout L = wct_layout(n, C, HW);
   double* ws = static_cast<double*>(workspace);
   if (int e = wct_matrices<SRC_F32C>(content, style, means, n, C, HW, L, ws, residual, st)) return e;
-  hipMemcpyAsync(T, ws + L.tm, sizeof(double) * n * C * C, hipMemcpyDeviceToDevice, st);
+  RPST_REQUIRE(hipMemcpyAsync(T, ws + L.tm, sizeof(double) * n * C * C, hipMemcpyDeviceToDevice,
+                              st) == hipSuccess, "wct_params: copy of T failed");
   const int64_t nc = (int64_t)n * C;
   wct_offset_kernel<<<(unsigned)((nc + 255) / 256), 256, 0, st>>>(ws + L.tm, ws + L.mu_c,
                                                                   ws + L.mu_s, offset, n, C);
