@@ -271,6 +271,27 @@ int rpst_adain_backward(const float* g, const float* c, const float* s, const fl
 int rpst_style_content_loss_grad(const float* F, const float* Fc, const float* stats,
                                  const float* weights, float* out, int planes, int64_t HW,
                                  int accumulate, rpst_stream_t stream);
+/* ---- SAModel training (network/sanet.py:248-275): the extra backward pieces --------
+ * 1-pixel pad of `planes` H x W planes to (H+2) x (W+2): reflect = 1 ReflectionPad2d(1)
+ * (H, W >= 2), 0 zeros. A reflect-padded conv's weight gradient is rpst_conv_wgrad of the
+ * padded input against the zero-padded output gradient. */
+int rpst_pad1(const float* x, float* out, int64_t planes, int H, int W, int reflect,
+              rpst_stream_t stream);
+/* nn.Upsample(scale_factor=2, mode='nearest') backward: g (planes, 2H, 2W) -> dx (planes,
+ * H, W), each dx the sum of its 2x2 block of g (sanet.py:145,166,179,186). */
+int rpst_upsample_nearest2x_backward(const float* g, float* dx, int64_t planes, int H, int W,
+                                     rpst_stream_t stream);
+/* mean_variance_norm backward (sanet.py:20-24): y the normalised output, dy its gradient,
+ * std (planes) = sqrt(var_unbiased + eps) -> dx = (dy - mean(dy) - y sum(dy y)/(HW-1))/std
+ * (accumulate = 1 adds into dx). */
+int rpst_mean_variance_norm_backward(const float* y, const float* dy, const float* std,
+                                     float* dx, int64_t planes, int64_t HW, int accumulate,
+                                     rpst_stream_t stream);
+/* Row softmax (sanet.py:92-93, dim=-1) and its backward dS = P (dP - rowsum(dP P)), for
+ * `rows` rows of `cols` contiguous floats (dS may alias dP). */
+int rpst_softmax_rows(const float* S, float* P, int64_t rows, int cols, rpst_stream_t stream);
+int rpst_softmax_rows_backward(const float* P, const float* dP, float* dS, int64_t rows,
+                               int cols, rpst_stream_t stream);
 /* *out = scale * sum (a - b)^2 over n elements (fp64 accumulation, fixed order).
  * Workspace: rpst_sq_diff_workspace_size(). */
 size_t rpst_sq_diff_workspace_size(void);

@@ -327,6 +327,48 @@ def samodel_test(content: Tensor, style: Tensor, sd: SD) -> Tensor:
         return decoder(fusion, sd, "decoder.")
 
 
+def samodel_losses(content, style, sd, cfg):
+    """SAModel.forward (sanet.py:248-275): the loss dict, differentiable w.r.t. the entries
+    of sd (the CPU gradient oracle of the SAModel training step). cfg: content_weight,
+    style_weight, l_identity1_weight, l_identity2_weight."""
+    mse = F.mse_loss
+    sfeat = encode_with_intermediate(style, sd, 5)
+    cfeat = encode_with_intermediate(content, sd, 5)
+    stylized = transform(cfeat[3], sfeat[3], cfeat[4], sfeat[4], sd, "transform.")
+    gt = encode_with_intermediate(decoder(stylized, sd, "decoder."), sd, 5)
+    lc = (mse(mean_variance_norm(gt[3]), mean_variance_norm(cfeat[3])) +
+          mse(mean_variance_norm(gt[4]), mean_variance_norm(cfeat[4])))
+    ls = style_loss(gt[0], sfeat[0])
+    for i in range(1, 5):
+        ls = ls + style_loss(gt[i], sfeat[i])
+    icc = decoder(transform(cfeat[3], cfeat[3], cfeat[4], cfeat[4], sd, "transform."), sd,
+                  "decoder.")
+    iss = decoder(transform(sfeat[3], sfeat[3], sfeat[4], sfeat[4], sd, "transform."), sd,
+                  "decoder.")
+    l1 = mse(icc, content) + mse(iss, style)
+    fcc = encode_with_intermediate(icc, sd, 5)
+    fss = encode_with_intermediate(iss, sd, 5)
+    l2 = mse(fcc[0], cfeat[0]) + mse(fss[0], sfeat[0])
+    for i in range(1, 5):
+        l2 = l2 + mse(fcc[i], cfeat[i]) + mse(fss[i], sfeat[i])
+    tot = (cfg["content_weight"] * lc + cfg["style_weight"] * ls +
+           cfg["l_identity1_weight"] * l1 + cfg["l_identity2_weight"] * l2)
+    return {"style_loss": ls, "content_loss": lc, "l_identity1_loss": l1,
+            "l_identity2_loss": l2, "total_loss": tot}
+
+
+def samodel_grads(content, style, sd, cfg):
+    """(loss dict, {name: d total_loss / d param}) for the transform and decoder (the
+    encoder is frozen, sanet.py:213-216)."""
+    sd = {k: (v.detach().clone().requires_grad_(k.startswith(("transform.", "decoder.")))
+              if v.is_floating_point() else v) for k, v in sd.items()}
+    with torch.enable_grad():
+        losses = samodel_losses(content, style, sd, cfg)
+        names = [k for k, v in sd.items() if v.requires_grad]
+        grads = torch.autograd.grad(losses["total_loss"], [sd[k] for k in names])
+    return ({k: v.detach() for k, v in losses.items()}, dict(zip(names, grads)))
+
+
 # ---- f3: AdaptiveSANet (sanet.py:12-18, 26-71, 100-160, 278-345) -----------------
 def cal_affinity_matrix(content: Tensor, style: Tensor) -> Tensor:
     """sanet.py:12-18: cosine similarity of positions over channels, (B, HW, HW)."""

@@ -219,7 +219,14 @@ class SAModel(nn.Module):
             return stylized
 
     def forward(self, content, style):
-        """Loss dict of sanet.py:248-275 (inference kernels: call under no_grad)."""
+        """Loss dict of sanet.py:248-275. With autograd enabled and a trainable transform /
+        decoder the losses come from rpst.autograd (forward + backward kernels), so
+        total_loss.backward() trains them as train.py does; under no_grad op by op."""
+        if type(self) is SAModel and torch.is_grad_enabled() and any(
+                p.requires_grad for p in list(self.transform.parameters()) +
+                list(self.decoder.parameters())):
+            from rpst.autograd import samodel_losses
+            return samodel_losses(self, content, style)
         style_feats = self.encode_with_intermediate(style)
         content_feats = self.encode_with_intermediate(content)
         stylized = self.transform(content_feats[3], style_feats[3], content_feats[4], style_feats[4])

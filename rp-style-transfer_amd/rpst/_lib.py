@@ -58,6 +58,11 @@ SIGNATURES = {
     "rpst_style_content_loss_grad": (_I, [_P, _P, _P, _P, _P, _I, _I64, _I, _P]),
     "rpst_sq_diff_workspace_size": (_SZ, []),
     "rpst_sq_diff_sum": (_I, [_P, _P, _I64, _D, _P, _P, _SZ, _P]),
+    "rpst_pad1": (_I, [_P, _P, _I64, _I, _I, _I, _P]),
+    "rpst_upsample_nearest2x_backward": (_I, [_P, _P, _I64, _I, _I, _P]),
+    "rpst_mean_variance_norm_backward": (_I, [_P, _P, _P, _P, _I64, _I64, _I, _P]),
+    "rpst_softmax_rows": (_I, [_P, _P, _I64, _I, _P]),
+    "rpst_softmax_rows_backward": (_I, [_P, _P, _P, _I64, _I, _P]),
     "rpst_u8hwc_to_f32nchw": (_I, [_P, _P, _I, _I, _I, _P]),
     "rpst_f32nchw_to_u8_tile": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_cosine_affinity_workspace_size": (_SZ, [_I, _I, _I]),

@@ -317,3 +317,310 @@ def wct_rp_losses(model, content: torch.Tensor, style: torch.Tensor
     total, ls, lc = _WCTRPStep.apply(content.detach().contiguous(), style.detach().contiguous(),
                                      model, cw, sw, *params)
     return {'style_loss': ls, 'content_loss': lc, 'total_loss': total}, total
+
+
+# ---- SAModel (sanet.py:248-275) ----------------------------------------------------------
+# The transform (two SANet modules + merge conv) and the VGG-style decoder train; the VGG
+# encoder is frozen and the transform's inputs are its (constant) features. Three branches
+# share the transform and decoder: g_t = decoder(transform(c, s)) with style (relu1..5_1)
+# and mean_variance_norm content (relu4_1, relu5_1) losses, and the identity reconstructions
+# Icc / Iss with l_identity1 (image MSE) and l_identity2 (feature MSE at relu1..5_1). The
+# backward walks each branch: loss seeds -> VGG dgrad -> decoder (reflect-pad wgrad via
+# rpst_pad1, upsample backward) -> merge conv -> SANet (1x1 convs, attention: S and dP
+# GEMMs on rocBLAS, row-softmax backward kernel). Parameter gradients add over branches.
+
+def _pad1(x: torch.Tensor, reflect: bool) -> torch.Tensor:
+    n, c, h, w = x.shape
+    out = torch.empty((n, c, h + 2, w + 2), device=x.device, dtype=torch.float32)
+    _lib.call("rpst_pad1", x.data_ptr(), out.data_ptr(), n * c, h, w, int(reflect), _stream(x))
+    return out
+
+
+def _upsample_backward(g: torch.Tensor) -> torch.Tensor:
+    n, c, h2, w2 = g.shape
+    dx = torch.empty((n, c, h2 // 2, w2 // 2), device=g.device, dtype=torch.float32)
+    _lib.call("rpst_upsample_nearest2x_backward", g.data_ptr(), dx.data_ptr(), n * c, h2 // 2,
+              w2 // 2, _stream(g))
+    return dx
+
+
+def _wgrad_reflect(x: torch.Tensor, g: torch.Tensor, conv: nn.Conv2d):
+    """ReflectionPad2d(1) + conv3x3 weight / bias gradient: the zero-pad wgrad of the
+    reflect-padded input against the zero-padded output gradient."""
+    return conv_wgrad(_pad1(x, True), _pad1(g, False), conv)
+
+
+def _acc(grads: Dict[int, torch.Tensor], p: torch.Tensor, g: torch.Tensor) -> None:
+    if g is None:
+        return
+    k = id(p)
+    if k in grads:
+        grads[k].add_(g)
+    else:
+        grads[k] = g
+
+
+def _stats(F: torch.Tensor, T: torch.Tensor) -> torch.Tensor:
+    """[mean(F) | std(F) | mean(T) | std(T)] (planes each): the loss-seed kernel's stats."""
+    mu, sd = ops.calc_mean_std(F)
+    mt, st = ops.calc_mean_std(T)
+    return torch.cat([mu.reshape(-1), sd.reshape(-1), mt.reshape(-1), st.reshape(-1)])
+
+
+def _seed(F, target, stats, wts, out, acc: bool):
+    """wts[0] * d calc_style_loss(F, target) + wts[1] * d mse(F, target) (target = None: no
+    MSE term) into out (acc: added)."""
+    planes = F.shape[0] * F.shape[1]
+    hw = F.shape[2] * F.shape[3]
+    _lib.call("rpst_style_content_loss_grad", F.data_ptr(),
+              None if target is None else target.data_ptr(), stats.data_ptr(), wts.data_ptr(),
+              out.data_ptr(), planes, hw, int(acc), _stream(F))
+
+
+def _vgg_saving(model, x, levels=5):
+    steps, saved, taps = [], [], []
+    for i in range(levels):
+        st = plan.compile_layers(getattr(model, f"enc_{i + 1}").children())
+        x, sv = _run_steps_saving(st, x)
+        steps += st
+        saved += sv
+        taps.append(len(steps) - 1)
+    return steps, saved, taps
+
+
+def _vgg_backward(steps, saved, taps, seed_fn):
+    """d input from seeds at the taps: seed_fn(level, F, g) returns the tap gradient with
+    the level's loss terms added into g (g None: a fresh tensor)."""
+    g = None
+    for k in range(len(steps) - 1, -1, -1):
+        x_in, y = saved[k]
+        if k in taps:
+            g = seed_fn(taps.index(k), y, g)
+        if g is None:
+            continue
+        s = steps[k]
+        if s.relu:
+            g = relu_backward(g, y)
+        g = conv_dgrad(g, s)
+        if s.in_op == ops.IN_MAXPOOL2:
+            g = maxpool_backward(x_in, g, relu_mask=False)
+        elif s.in_op != ops.IN_NONE:
+            raise NotImplementedError("rpst autograd: VGG input operator")
+    return g
+
+
+def _decoder_backward(steps, saved, g, grads):
+    """Decoder (sanet.py:162-192: reflect-pad conv3x3 + ReLU, nearest x2 upsample fused
+    into the next conv's loader): parameter gradients into grads, returns d input."""
+    for k in range(len(steps) - 1, -1, -1):
+        s = steps[k]
+        x_in, y = saved[k]
+        if s.relu:
+            g = relu_backward(g, y)
+        up = s.in_op == ops.IN_UPSAMPLE2
+        if not up and s.in_op != ops.IN_NONE:
+            raise NotImplementedError("rpst autograd: decoder input operator")
+        xc = ops.upsample_nearest2x(x_in) if up else x_in
+        dw, db = _wgrad_reflect(xc, g, s.conv)
+        _acc(grads, s.conv.weight, dw)
+        _acc(grads, s.conv.bias, db)
+        g = conv_dgrad(g, s)
+        if up:
+            g = _upsample_backward(g)
+    return g
+
+
+def _conv1x1(conv, x, residual=None):
+    return ops.conv2d(x, plan.packed_weight(conv), conv.bias, conv.out_channels, 1,
+                      residual=residual)
+
+
+def _sanet_forward(m, c, s):
+    Fn = ops.mean_variance_norm(c)
+    Gn = ops.mean_variance_norm(s)
+    F = _conv1x1(m.f, Fn)
+    G = _conv1x1(m.g, Gn)
+    H = _conv1x1(m.h, s)
+    O = ops.sanet_attention(F, G, H)
+    return _conv1x1(m.out_conv, O, residual=c), (Fn, Gn, s, F, G, H, O)
+
+
+def _lin_grads(dY, X):
+    """1x1 conv weight / bias gradient over a batch: sum_n dY_n X_n^T (rocBLAS GEMM)."""
+    b, co = dY.shape[:2]
+    ci = X.shape[1]
+    dw = torch.bmm(dY.reshape(b, co, -1), X.reshape(b, ci, -1).transpose(1, 2)).sum(0)
+    return dw.reshape(co, ci, 1, 1), dY.sum((0, 2, 3))
+
+
+def _sanet_backward(m, saved, d_out, grads):
+    """SANet parameter gradients from d_out (sanet.py:82-99; the residual's content and
+    both inputs are constants of the step)."""
+    Fn, Gn, s, F, G, H, O = saved
+    b, c, hc, wc = F.shape
+    hwc, hws = hc * wc, G.shape[2] * G.shape[3]
+    dw, db = _lin_grads(d_out, O)
+    _acc(grads, m.out_conv.weight, dw)
+    _acc(grads, m.out_conv.bias, db)
+    dO = ops.conv2d(d_out, flip_packed_weight(m.out_conv), None, c, 1).reshape(b, c, hwc)
+    Fv, Gv, Hv = F.reshape(b, c, hwc), G.reshape(b, c, hws), H.reshape(b, c, hws)
+    S = torch.bmm(Fv.transpose(1, 2), Gv)
+    P = torch.empty_like(S)
+    _lib.call("rpst_softmax_rows", S.data_ptr(), P.data_ptr(), b * hwc, hws, _stream(S))
+    dH = torch.bmm(dO, P)
+    dP = torch.bmm(dO.transpose(1, 2), Hv)
+    _lib.call("rpst_softmax_rows_backward", P.data_ptr(), dP.data_ptr(), dP.data_ptr(),
+              b * hwc, hws, _stream(dP))
+    dF = torch.bmm(Gv, dP.transpose(1, 2))
+    dG = torch.bmm(Fv, dP)
+    for conv, dY, X in ((m.f, dF, Fn), (m.g, dG, Gn), (m.h, dH, s)):
+        dw, db = _lin_grads(dY.reshape(X.shape[0], c, *X.shape[2:]), X)
+        _acc(grads, conv.weight, dw)
+        _acc(grads, conv.bias, db)
+
+
+def _transform_forward(tr, c4, s4, c5, s5):
+    a, sa = _sanet_forward(tr.sanet4_1, c4, s4)
+    b, sb = _sanet_forward(tr.sanet5_1, c5, s5)
+    c = tr.merge_conv
+    out = ops.conv2d(a, plan.packed_weight(c), c.bias, c.out_channels, 3, pad=ops.PAD_REFLECT,
+                     in_op=ops.IN_ADD_UPSAMPLE2, aux=b)
+    z = a + ops.upsample_nearest2x(b)  # merge conv input, for its weight gradient
+    return out, (sa, sb, z)
+
+
+def _transform_backward(tr, saved, g, grads):
+    sa, sb, z = saved
+    c = tr.merge_conv
+    dw, db = _wgrad_reflect(z, g, c)
+    _acc(grads, c.weight, dw)
+    _acc(grads, c.bias, db)
+    dz = conv_dgrad(g, plan.ConvStep(conv=c, pad=ops.PAD_REFLECT, in_op=ops.IN_NONE, relu=0))
+    _sanet_backward(tr.sanet4_1, sa, dz, grads)
+    _sanet_backward(tr.sanet5_1, sb, _upsample_backward(dz), grads)
+
+
+class _SAModelStep(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, content, style, model, cfg, *params):
+        with ops.precise_convs():
+            return _SAModelStep._forward(ctx, content, style, model, cfg, *params)
+
+    @staticmethod
+    def backward(ctx, g_total, g_ls, g_lc, g_l1, g_l2):
+        with ops.precise_convs():
+            return _SAModelStep._backward(ctx, g_total, g_ls, g_lc, g_l1, g_l2)
+
+    @staticmethod
+    def _forward(ctx, content, style, model, cfg, *params):
+        n = content.shape[0]
+        feats = model.encode_with_intermediate(torch.cat([style, content], dim=0))
+        sf = [f[:n].contiguous() for f in feats]
+        cf = [f[n:].contiguous() for f in feats]
+        dec_steps = plan.compile_layers(model.decoder.children())
+        tr = model.transform
+        br = {}
+        for name, (a4, b4, a5, b5) in (("gt", (cf[3], sf[3], cf[4], sf[4])),
+                                       ("cc", (cf[3], cf[3], cf[4], cf[4])),
+                                       ("ss", (sf[3], sf[3], sf[4], sf[4]))):
+            t, tsv = _transform_forward(tr, a4, b4, a5, b5)
+            img, dsv = _run_steps_saving(dec_steps, t)
+            vs, vsv, taps = _vgg_saving(model, img)
+            br[name] = (tsv, dsv, (vs, vsv, taps), img)
+        gtf = [br["gt"][2][1][k][1] for k in br["gt"][2][2]]
+        ls = None
+        sstats = []
+        for i in range(5):
+            st = _stats(gtf[i], sf[i])
+            sstats.append(st)
+            mu, sd = ops.calc_mean_std(gtf[i])
+            mt, stt = ops.calc_mean_std(sf[i])
+            term = sq_diff_mean(mu, mt) + sq_diff_mean(sd, stt)
+            ls = term if ls is None else ls + term
+        mvn = {}
+        lc = None
+        for i in (3, 4):
+            y = ops.mean_variance_norm(gtf[i])
+            yt = ops.mean_variance_norm(cf[i])
+            mvn[i] = (y, yt, ops.calc_mean_std(gtf[i])[1].reshape(-1).contiguous(), _stats(y, yt))
+            term = sq_diff_mean(y, yt)
+            lc = term if lc is None else lc + term
+        icc, iss = br["cc"][3], br["ss"][3]
+        l1 = sq_diff_mean(icc, content) + sq_diff_mean(iss, style)
+        fcc = [br["cc"][2][1][k][1] for k in br["cc"][2][2]]
+        fss = [br["ss"][2][1][k][1] for k in br["ss"][2][2]]
+        l2 = None
+        for i in range(5):
+            term = sq_diff_mean(fcc[i], cf[i]) + sq_diff_mean(fss[i], sf[i])
+            l2 = term if l2 is None else l2 + term
+        total = (cfg[0] * lc + cfg[1] * ls + cfg[2] * l1 + cfg[3] * l2)
+        ctx.save = (model, dec_steps, br, sf, cf, sstats, mvn, content, style, cfg, params)
+        return total, ls, lc, l1, l2
+
+    @staticmethod
+    def _backward(ctx, g_total, g_ls, g_lc, g_l1, g_l2):
+        model, dec_steps, br, sf, cf, sstats, mvn, content, style, cfg, params = ctx.save
+        dev = content.device
+        zero = torch.zeros((), device=dev)
+
+        def w(g_part, k):
+            gt = zero if g_total is None else g_total
+            return gt * cfg[k] + (zero if g_part is None else g_part)
+
+        w_c, w_s, w_1, w_2 = w(g_lc, 0), w(g_ls, 1), w(g_l1, 2), w(g_l2, 3)
+        wt = lambda a, b: torch.stack([a, b]).to(torch.float32).contiguous()  # noqa: E731
+        w_style, w_mse_c, w_mse_2, w_mse_1 = wt(w_s, zero), wt(zero, w_c), wt(zero, w_2), wt(zero, w_1)
+        grads: Dict[int, torch.Tensor] = {}
+        tr = model.transform
+
+        def gt_seed(i, F, g):
+            fresh = g is None
+            if fresh:
+                g = torch.empty_like(F)
+            if i in mvn:  # content loss: mse(mvn(F), mvn(Fc)) -> through mean_variance_norm
+                y, yt, sd, st = mvn[i]
+                dy = torch.empty_like(y)
+                _seed(y, yt, st, w_mse_c, dy, False)
+                _lib.call("rpst_mean_variance_norm_backward", y.data_ptr(), dy.data_ptr(),
+                          sd.data_ptr(), g.data_ptr(), F.shape[0] * F.shape[1],
+                          F.shape[2] * F.shape[3], int(not fresh), _stream(F))
+                fresh = False
+            _seed(F, None, sstats[i], w_style, g, not fresh)
+            return g
+
+        def id_seed(targets):
+            def fn(i, F, g):
+                st = _stats(F, targets[i])
+                if g is None:
+                    g = torch.empty_like(F)
+                    _seed(F, targets[i], st, w_mse_2, g, False)
+                else:
+                    _seed(F, targets[i], st, w_mse_2, g, True)
+                return g
+            return fn
+
+        for name, seed_fn, img_target in (("gt", gt_seed, None), ("cc", id_seed(cf), content),
+                                          ("ss", id_seed(sf), style)):
+            tsv, dsv, (vs, vsv, taps), img = br[name]
+            g = _vgg_backward(vs, vsv, taps, seed_fn)
+            if img_target is not None:  # l_identity1 on the reconstructed image
+                _seed(img, img_target, _stats(img, img_target), w_mse_1, g, True)
+            g = _decoder_backward(dec_steps, dsv, g, grads)
+            _transform_backward(tr, tsv, g, grads)
+        ctx.save = None
+        return (None, None, None, None, *[grads.get(id(p)) for p in params])
+
+
+def samodel_losses(model, content: torch.Tensor, style: torch.Tensor
+                   ) -> Tuple[Dict[str, torch.Tensor], torch.Tensor]:
+    """SAModel.forward with autograd: the loss dict of sanet.py:248-275 and total_loss,
+    differentiable w.r.t. the transform and decoder parameters."""
+    ops._check(content, style)
+    params: List[torch.Tensor] = list(model.transform.parameters()) + list(model.decoder.parameters())
+    c = model.config
+    cfg = (float(c['content_weight']), float(c['style_weight']), float(c['l_identity1_weight']),
+           float(c['l_identity2_weight']))
+    total, ls, lc, l1, l2 = _SAModelStep.apply(content.detach().contiguous(),
+                                               style.detach().contiguous(), model, cfg, *params)
+    return {'style_loss': ls, 'content_loss': lc, 'l_identity1_loss': l1,
+            'l_identity2_loss': l2, 'total_loss': total}, total

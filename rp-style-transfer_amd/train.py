@@ -18,9 +18,10 @@ WORLD_SIZE > 1 every rank draws its own batches and the gradients are averaged b
 all-reduce of a flat buffer per step (rpst.shard.GradientAllReduce; RCCL over xGMI).
 Scalars go to <output>/logs/train.jsonl (tensorboardX is not available offline); the
 reference's per-iteration try/except that swallows errors is not reproduced.
-Networks with backward kernels: 'adain' (AdaINRPNet: RP encoder + decoder) and 'wct'
-(WCTRPNet: RP decoder; its fuse() detaches the encoder features, wct_rp.py:161-162); the
-others raise.
+Networks with backward kernels: 'adain' (AdaINRPNet: RP encoder + decoder), 'wct'
+(WCTRPNet: RP decoder; its fuse() detaches the encoder features, wct_rp.py:161-162) and
+'sanet' (SAModel: transform + decoder, sanet.py:248-275; checkpoints {'decoder',
+'transform'}); the others raise.
 """
 from __future__ import annotations
 
@@ -41,7 +42,24 @@ logging.basicConfig(level=logging.INFO,
                     format="%(asctime)s - %(name)s - %(levelname)s - %(message)s")
 logger = logging.getLogger("train")
 
-TRAINABLE = {"adain", "wct"}  # networks with backward kernels (rpst.autograd)
+TRAINABLE = {"adain", "wct", "sanet"}  # networks with backward kernels (rpst.autograd)
+
+
+def _begin(network) -> int:
+    """network.begin (BaseNet, base.py:536); the reference's SAModel has none (its train.py
+    would fail there), so SAModel starts at 0 like the others."""
+    return getattr(network, "begin", 0)
+
+
+def _save(network, path, iterations) -> None:
+    """network.save (adain_rp.py:103-108); SAModel, which has no save(), is checkpointed like
+    AdaptiveSAModel.save (sanet.py:323-328): {'decoder', 'transform'}."""
+    if hasattr(network, "save"):
+        network.save(path, iterations=iterations)
+    else:
+        import torch
+        torch.save({"decoder": network.decoder.state_dict(),
+                    "transform": network.transform.state_dict()}, path)
 
 
 def adjust_learning_rate(opt, optimizer, iteration_count):
@@ -176,11 +194,11 @@ def main(argv=None) -> int:
             continue
         scalars = {k: float(v.detach()) for k, v in loss_dict.items()}
         elapsed = round(time.time() - start, 2)
-        log.write(json.dumps({"iteration": network.begin + i, "elapsed": elapsed,
+        log.write(json.dumps({"iteration": _begin(network) + i, "elapsed": elapsed,
                               **scalars}) + "\n")
         log.flush()
         if test_set is not None and i % opt["test_iter"] == 0:
-            out = test_dir / f"{network.begin + i}"
+            out = test_dir / f"{_begin(network) + i}"
 
             def stylize_fn(c, s):
                 return network.test(c, s, iterations=i)
@@ -189,9 +207,9 @@ def main(argv=None) -> int:
                      opt.get("num_workers", 4)).run(test_set, str(out), log=logger.info)
         if i % opt["log_iter"] == 0:
             loss_str = "".join(f", {k} {v}" for k, v in scalars.items())
-            logger.info(f"Iterations {network.begin + i}, elapsed time: {elapsed} {loss_str}")
+            logger.info(f"Iterations {_begin(network) + i}, elapsed time: {elapsed} {loss_str}")
         if i % opt["snapshot_save_iter"] == 0 or (i + 1) == opt["max_iter"]:
-            network.save(ckpt_dir / f"{network.begin + i}", iterations=i)
+            _save(network, ckpt_dir / f"{_begin(network) + i}", i)
     if log:
         log.close()
     if world > 1:

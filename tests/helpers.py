@@ -57,3 +57,21 @@ def deeper_config(hidden, blocks=5, inception=3):
     cfg = multiscale_config(hidden, blocks, inception)
     cfg["enc_stack_way"] = "deeper"
     return cfg
+
+
+def grad_probe(key, g):
+    """(sum, sum of squares, dot with a fixed uniform probe) of one gradient tensor
+    (tests/golden/gen_golden.gen_grads_sam stores these instead of ~8M SAModel gradients)."""
+    from rpst import synth
+    g = np.asarray(torch.as_tensor(g).detach().double().cpu(), dtype=np.float64).reshape(-1)
+    pr = 2.0 * synth.uniform01(0, "gprobe:" + key, g.size) - 1.0
+    return np.array([g.sum(), (g * g).sum(), (g * pr).sum()])
+
+
+def probe_err(ours, ref, n):
+    """Largest of the three probe differences, each scaled like a rel-L2 error by the
+    reference gradient's norm (sum and probe dot: by norm * sqrt(n) and norm * sqrt(n/3))."""
+    nrm = max(np.sqrt(ref[1]), 1e-300)
+    return max(abs(ours[0] - ref[0]) / (nrm * np.sqrt(n)),
+               abs(np.sqrt(max(ours[1], 0.0)) - nrm) / nrm,
+               abs(ours[2] - ref[2]) / (nrm * np.sqrt(n / 3.0)))

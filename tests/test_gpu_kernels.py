@@ -306,9 +306,9 @@ def test_adain_rp_vs_oracle_hidden16(cuda):
 
 def test_grad_enabled_raises(cuda):
     """Models without backward kernels raise under autograd instead of running ATen
-    (AdaINRPNet and WCTRPNet train through rpst.autograd: tests/test_gpu_train.py)."""
+    (AdaINRPNet, WCTRPNet and SAModel train through rpst.autograd: tests/test_gpu_train.py)."""
     import network as net
-    m = net.SAModel({}, copy.deepcopy(net.vgg), 0, 32).to(cuda)
+    m = net.SourceNet({}, copy.deepcopy(net.vgg)).to(cuda)
     x = torch.rand(1, 3, 32, 32, device=cuda)
     with pytest.raises(NotImplementedError):
         m(x, x)

@@ -222,6 +222,30 @@ def test_reference_wct_training_gradients(golden):
             assert rel_l2(grads[name], g[f"grad{i}:{name}"]) < 1e-5, (i, name)
 
 
+def test_reference_samodel_training_gradients(golden):
+    """R.samodel_grads against the reference's SAModel.forward + backward
+    (sanet.py:248-275): the five losses and probes of every transform / decoder gradient."""
+    import network as net
+    from helpers import grad_probe, probe_err
+    g = golden("grads_sam")
+    cfg = {"content_weight": 1.0, "style_weight": 3.0, "l_identity1_weight": 50.0,
+           "l_identity2_weight": 1.0}
+    for i in range(int(g["n"])):
+        shp = g[f"content{i}"].shape
+        m = net.SAModel(dict(cfg), copy.deepcopy(net.vgg), 0, shp[-1])
+        np.testing.assert_allclose(synth_(m, int(g[f"seed{i}"])), g[f"checksum{i}"], rtol=1e-12)
+        losses, grads = R.samodel_grads(t(g[f"content{i}"]), t(g[f"style{i}"]),
+                                        state_dict_of(m), cfg)
+        for k in ("style_loss", "content_loss", "l_identity1_loss", "l_identity2_loss",
+                  "total_loss"):
+            np.testing.assert_allclose(losses[k].numpy(), g[f"{k}{i}"], rtol=1e-5)
+        names = [str(n) for n in g[f"names{i}"]]
+        assert sorted(names) == sorted(grads)
+        for name in names:
+            e = probe_err(grad_probe(name, grads[name]), g[f"gprobe{i}:{name}"], grads[name].numel())
+            assert e < 1e-5, (i, name, e)
+
+
 def test_sourcenet_test(golden):
     """SourceNet.test (classic AdaIN) against the reference."""
     import network as net
