@@ -77,6 +77,8 @@ def build_model(kind, dev):
         m = net.AdaINRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
     elif kind == "train_wct":
         m = net.WCTRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
+    elif kind == "train_sanet":
+        m = net.SAModel(dict(SANET_TRAIN_CONFIG), copy.deepcopy(net.vgg), 0, 512)
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, 512)
     synth.synth_module_(m, 0)
@@ -93,6 +95,10 @@ SOURCE_CONFIG = {"use_mask": False, "content_weight": 1.0, "style_weight": 10.0}
 # config/rl/train_dynamic_sanet.yaml: ada_module 'relu' (AEALReluModule)
 ADAPTIVE_CONFIG = {"ada_module": "relu", "content_weight": 1.0, "style_weight": 3.0,
                    "l_identity1_weight": 50.0, "l_identity2_weight": 1.0}
+# config/rl/train_static_sanet.yaml loss weights
+SANET_TRAIN_CONFIG = {"content_weight": 1.0, "style_weight": 3.0, "l_identity1_weight": 50.0,
+                      "l_identity2_weight": 1.0}
+TRAIN_KINDS = ("train", "train_wct", "train_sanet")
 
 
 WORKLOADS = {
@@ -110,12 +116,16 @@ WORKLOADS = {
     "train_wct": "WCTRPNet training iteration: forward() losses + total_loss.backward() + Adam "
                  "step (RP decoder; fuse() detaches the encoder features), rp_blocks=5 "
                  "hidden_dim=16 (SURVEY 8(f) rank 2)",
+    "train_sanet": "SAModel training iteration: forward() losses (g_t style/content, identity "
+                   "1/2 over Icc, Iss) + total_loss.backward() + Adam step on the transform and "
+                   "decoder, config/rl/train_static_sanet.yaml weights (SURVEY 8(f) rank 2)",
     "selftest": "CPU stand-in per-image function (launcher / timing / gather test only)",
 }
 DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32, "multiscale": 32, "source": 32,
-                 "adaptive": 32, "train": 8, "train_wct": 8, "selftest": 4}
+                 "adaptive": 32, "train": 8, "train_wct": 8, "train_sanet": 8,
+                 "selftest": 4}
 # CPU-baseline sample per workload (BASELINE.md plan: B=2 at 512^2, B=1 for WCT)
-CPU_SAMPLE_BATCH = {"wct": 1, "train": 1, "train_wct": 1}
+CPU_SAMPLE_BATCH = {"wct": 1, "train": 1, "train_wct": 1, "train_sanet": 1}
 
 
 def cpu_info():
@@ -164,6 +174,9 @@ def cpu_baseline(kind, size, reps=3):
     elif kind == "train_wct":
         m = net.WCTRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
         fn = lambda c, s, sd: R.wct_rp_grads(c, s, sd, 5, 1.0, 1.0)  # noqa: E731
+    elif kind == "train_sanet":
+        m = net.SAModel(dict(SANET_TRAIN_CONFIG), copy.deepcopy(net.vgg), 0, size)
+        fn = lambda c, s, sd: R.samodel_grads(c, s, sd, SANET_TRAIN_CONFIG)  # noqa: E731
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, size)
         fn = R.samodel_test
@@ -431,7 +444,7 @@ def main():
     content = torch.from_numpy(synth.image_range(1000, (total, 3, size, size), start, end)).to(dev)
     style = torch.from_numpy(synth.image_range(2000, (total, 3, size, size), start, end)).to(dev)
 
-    if model_kind in ("train", "train_wct"):
+    if model_kind in TRAIN_KINDS:
         from rpst.shard import GradientAllReduce
         trained = model.rp_decoder if model_kind == "train_wct" else model
         params = [p for p in trained.parameters() if p.requires_grad]
@@ -454,7 +467,7 @@ def main():
     # the D2H gather of chunk i runs on a copy stream while chunk i + 1 computes
     copy_stream = torch.cuda.Stream(dev) if (cuda and host is not None) else None
 
-    if model_kind not in ("train", "train_wct"):
+    if model_kind not in TRAIN_KINDS:
         def step():
             out = None
             for s0 in range(0, B, mb):
