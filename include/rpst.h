@@ -258,6 +258,12 @@ size_t rpst_conv_wgrad_workspace_size(int N, int Cin, int H, int W, int Cout);
 int rpst_conv_wgrad(const float* x, const float* dy, float* dw, float* db, int N, int Cin,
                     int H, int W, int Cout, void* workspace, size_t workspace_bytes,
                     rpst_stream_t stream);
+/* the same with the conv's padding: RPST_PAD_ZERO, or RPST_PAD_REFLECT (ReflectionPad2d(1) +
+ * conv3x3 pad 0, the decoders of sanet.py:162-192 / base.py Conv2dBlock 'reflect'; H, W >= 2),
+ * read in the loader (no padded copy). Same workspace. */
+int rpst_conv_wgrad_pad(const float* x, const float* dy, float* dw, float* db, int N, int Cin,
+                        int H, int W, int Cout, int pad, void* workspace,
+                        size_t workspace_bytes, rpst_stream_t stream);
 /* adaptive_instance_normalization backward (base.py:410-418): g the gradient at the AdaIN
  * output, c / s the content / style features (planes x HW), stats = [mean_c | std_c |
  * mean_s | std_s] (planes each) -> dc, ds. Workspace: 2*planes floats. */

@@ -227,6 +227,9 @@ __global__ __launch_bounds__(256) void reflect_fold_kernel(
 }
 
 // ---- conv weight gradient (3x3, stride 1, zero pad 1) ---------------------------------------
+// reflect != 0: ReflectionPad2d(1) instead (the decoders of sanet.py:162-192): rows -1 / H and
+// columns -1 / W of X read rows / columns 1 / H - 2 (only column W inside a segment needs a
+// fix-up: columns past it multiply a zero dY).
 // Block: 256 threads (2 x 2 waves), tile 64 co x 64 ci, all 9 taps (9 accumulators per wave).
 // K = pixels, walked in row segments of 64 columns: LDS holds dY[px][co] (64 x 65) and
 // X[row][col][ci] (3 x 66 x 65, rows y-1..y+1, columns x0-1..x0+64, zero outside the image);
@@ -245,7 +248,8 @@ typedef unsigned wg_u32x4 __attribute__((ext_vector_type(4)));
 template <bool VEC>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(
     const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part,
-    float* __restrict__ bpart, int N, int Cin, int H, int W, int Cout, int64_t segs_per_split) {
+    float* __restrict__ bpart, int N, int Cin, int H, int W, int Cout, int64_t segs_per_split,
+    int reflect) {
   __shared__ float Ys[kWgPx * kWgLd];
   __shared__ float Xs[3 * kWgCols * kWgLd];
   const int tilesCi = (Cin + kWgTile - 1) / kWgTile;
@@ -301,7 +305,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(
     }
 #pragma unroll
     for (int row = 0; row < 3; ++row) {
-      const int yy = y - 1 + row;
+      int yy = y - 1 + row;
+      if (reflect) yy = reflect1(yy, H);
       const bool rok = live && ci_ok && yy >= 0 && yy < H;
       const unsigned rbase = ((unsigned)(ci0 + c) * HW + (unsigned)(rok ? yy : 0) * W) * 4u;
 #pragma unroll
@@ -311,17 +316,23 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(
         if (VEC) {
           rx[row][k] = __builtin_amdgcn_raw_buffer_load_b128(
               rxx, (int)(ok ? rbase + 4u * xx : kWgOOB), 0, 0);
+          // reflect: column W (first element of a group past the image) is column W - 2
+          if (reflect && xx == W)
+            rx[row][k][0] = __builtin_amdgcn_raw_buffer_load_b32(
+                rxx, (int)(rok ? rbase + 4u * (W - 2) : kWgOOB), 0, 0);
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const bool oe = ok && xx + e < W;
+            const int xe = reflect && xx + e == W ? W - 2 : xx + e;
+            const bool oe = ok && xe < W;
             rx[row][k][e] = __builtin_amdgcn_raw_buffer_load_b32(
-                rxx, (int)(oe ? rbase + 4u * (xx + e) : kWgOOB), 0, 0);
+                rxx, (int)(oe ? rbase + 4u * xe : kWgOOB), 0, 0);
           }
         }
       }
       // halo: column x0 - 1 (q == 0) or x0 + 64 (q == 3)
-      const int hx = q == 0 ? x0 - 1 : x0 + kWgPx;
+      int hx = q == 0 ? x0 - 1 : x0 + kWgPx;
+      if (reflect && hx <= W) hx = reflect1(hx, W);
       const bool hok = rok && (q == 0 || q == 3) && hx >= 0 && hx < W;
       rh[row] = __uint_as_float(
           __builtin_amdgcn_raw_buffer_load_b32(rxx, (int)(hok ? rbase + 4u * hx : kWgOOB), 0, 0));
@@ -587,11 +598,16 @@ extern "C" size_t rpst_conv_wgrad_workspace_size(int N, int Cin, int H, int W, i
   return sizeof(float) * (size_t)splits * Cout * ((size_t)Cin * 9 + 1);
 }
 
-extern "C" int rpst_conv_wgrad(const float* x, const float* dy, float* dw, float* db, int N,
-                               int Cin, int H, int W, int Cout, void* workspace,
-                               size_t workspace_bytes, rpst_stream_t stream) {
+extern "C" int rpst_conv_wgrad_pad(const float* x, const float* dy, float* dw, float* db,
+                                   int N, int Cin, int H, int W, int Cout, int pad,
+                                   void* workspace, size_t workspace_bytes,
+                                   rpst_stream_t stream) {
   RPST_REQUIRE(x && dy && dw && N > 0 && Cin > 0 && H > 0 && W > 0 && Cout > 0,
                "conv_wgrad: bad args");
+  RPST_REQUIRE(pad == RPST_PAD_ZERO || pad == RPST_PAD_REFLECT, "conv_wgrad: bad pad mode");
+  RPST_REQUIRE(pad != RPST_PAD_REFLECT || (H >= 2 && W >= 2),
+               "conv_wgrad: reflect padding needs H, W >= 2");
+  const int reflect = pad == RPST_PAD_REFLECT;
   if (!workspace || workspace_bytes < rpst_conv_wgrad_workspace_size(N, Cin, H, W, Cout)) {
     set_error("conv_wgrad: workspace too small");
     return RPST_EWORKSPACE;
@@ -608,10 +624,10 @@ extern "C" int rpst_conv_wgrad(const float* x, const float* dy, float* dw, float
   const bool vec = (W % 4) == 0;
   if (vec)
     conv_wgrad_kernel<true><<<dim3(tiles, splits), 256, 0, st>>>(
-        x, dy, part, db ? bpart : nullptr, N, Cin, H, W, Cout, sps);
+        x, dy, part, db ? bpart : nullptr, N, Cin, H, W, Cout, sps, reflect);
   else
     conv_wgrad_kernel<false><<<dim3(tiles, splits), 256, 0, st>>>(
-        x, dy, part, db ? bpart : nullptr, N, Cin, H, W, Cout, sps);
+        x, dy, part, db ? bpart : nullptr, N, Cin, H, W, Cout, sps, reflect);
   if (int e = launch_status("conv_wgrad_kernel")) return e;
   const int64_t n = (int64_t)Cout * Cin * 9;
   wgrad_reduce_kernel<<<blocks_for(n), 256, 0, st>>>(part, dw, n, splits);
@@ -621,6 +637,13 @@ extern "C" int rpst_conv_wgrad(const float* x, const float* dy, float* dw, float
     return launch_status("wgrad_reduce_kernel(bias)");
   }
   return RPST_OK;
+}
+
+extern "C" int rpst_conv_wgrad(const float* x, const float* dy, float* dw, float* db, int N,
+                               int Cin, int H, int W, int Cout, void* workspace,
+                               size_t workspace_bytes, rpst_stream_t stream) {
+  return rpst_conv_wgrad_pad(x, dy, dw, db, N, Cin, H, W, Cout, RPST_PAD_ZERO, workspace,
+                             workspace_bytes, stream);
 }
 
 extern "C" int rpst_adain_backward(const float* g, const float* c, const float* s,

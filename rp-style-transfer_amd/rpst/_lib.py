@@ -54,6 +54,7 @@ SIGNATURES = {
     "rpst_reflect_pad_border_grad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     "rpst_conv_wgrad_workspace_size": (_SZ, [_I, _I, _I, _I, _I]),
     "rpst_conv_wgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
+    "rpst_conv_wgrad_pad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     "rpst_adain_backward": (_I, [_P, _P, _P, _P, _P, _P, _I, _I64, _P, _SZ, _P]),
     "rpst_style_content_loss_grad": (_I, [_P, _P, _P, _P, _P, _I, _I64, _I, _P]),
     "rpst_sq_diff_workspace_size": (_SZ, []),

@@ -87,7 +87,9 @@ def maxpool_backward(x: torch.Tensor, g: torch.Tensor, relu_mask: bool) -> torch
     return dx
 
 
-def conv_wgrad(x: torch.Tensor, g: torch.Tensor, conv: nn.Conv2d):
+def conv_wgrad(x: torch.Tensor, g: torch.Tensor, conv: nn.Conv2d, pad: int = ops.PAD_ZERO):
+    """3x3 conv weight / bias gradient; pad = ops.PAD_REFLECT for ReflectionPad2d(1) + conv
+    (the reflection is read in the kernel's loader)."""
     n, cin, h, w = x.shape
     cout = conv.out_channels
     assert conv.kernel_size == (3, 3) and tuple(g.shape) == (n, cout, h, w)
@@ -95,11 +97,11 @@ def conv_wgrad(x: torch.Tensor, g: torch.Tensor, conv: nn.Conv2d):
     db = torch.empty_like(conv.bias) if conv.bias is not None else None
     nbytes = _lib.load().rpst_conv_wgrad_workspace_size(n, cin, h, w, cout)
     ws = _ws(nbytes, x)
-    with ops._traced(f"wgrad3x3 {cin}->{cout} {h}x{w} N{n} op0",
+    with ops._traced(f"wgrad3x3 {cin}->{cout} {h}x{w} N{n} op0{' reflect' if pad else ''}",
                      2.0 * n * cout * cin * 9 * h * w, 4.0 * (x.numel() + g.numel())):
-        _lib.call("rpst_conv_wgrad", x.data_ptr(), g.data_ptr(), dw.data_ptr(),
-                  None if db is None else db.data_ptr(), n, cin, h, w, cout, ws.data_ptr(),
-                  nbytes, _stream(x))
+        _lib.call("rpst_conv_wgrad_pad", x.data_ptr(), g.data_ptr(), dw.data_ptr(),
+                  None if db is None else db.data_ptr(), n, cin, h, w, cout, int(pad),
+                  ws.data_ptr(), nbytes, _stream(x))
     return dw, db
 
 
@@ -345,9 +347,9 @@ def _upsample_backward(g: torch.Tensor) -> torch.Tensor:
 
 
 def _wgrad_reflect(x: torch.Tensor, g: torch.Tensor, conv: nn.Conv2d):
-    """ReflectionPad2d(1) + conv3x3 weight / bias gradient: the zero-pad wgrad of the
-    reflect-padded input against the zero-padded output gradient."""
-    return conv_wgrad(_pad1(x, True), _pad1(g, False), conv)
+    """ReflectionPad2d(1) + conv3x3 weight / bias gradient (the reflection in the wgrad
+    kernel's loader; equal to the zero-pad wgrad of _pad1(x, True) against _pad1(g, False))."""
+    return conv_wgrad(x, g, conv, ops.PAD_REFLECT)
 
 
 def _acc(grads: Dict[int, torch.Tensor], p: torch.Tensor, g: torch.Tensor) -> None:

@@ -62,6 +62,31 @@ def test_conv_wgrad(cuda, shape):
     assert rel_l2(db, bd.grad) < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(2, 16, 12, 20, 32), (1, 3, 9, 7, 16), (2, 64, 33, 70, 40),
+                                   (1, 8, 2, 2, 8), (1, 32, 16, 64, 24), (1, 16, 5, 132, 16)])
+def test_conv_wgrad_reflect(cuda, shape):
+    """ReflectionPad2d(1) + conv3x3 weight / bias gradient (rpst_conv_wgrad_pad, reflection in
+    the loader): against float64 autograd, and equal to the zero-pad wgrad of the
+    rpst_pad1-padded tensors (W = 64 and W % 64 != 0, odd widths: the column-W fix-up)."""
+    from rpst import autograd as A
+    from rpst import ops
+    n, cin, h, w, cout = shape
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=0).to(cuda)
+    x = gen(14, (n, cin, h, w))
+    g = gen(15, (n, cout, h, w))
+    wd = conv.weight.detach().cpu().double().requires_grad_()
+    bd = conv.bias.detach().cpu().double().requires_grad_()
+    Fn.conv2d(Fn.pad(x.double(), (1, 1, 1, 1), mode="reflect"), wd, bd).backward(g.double())
+    dw, db = A.conv_wgrad(x.to(cuda), g.to(cuda), conv, ops.PAD_REFLECT)
+    assert rel_l2(dw, wd.grad) < 1e-5
+    assert rel_l2(db, bd.grad) < 1e-5
+    xp, gp = A._pad1(x.to(cuda), True), A._pad1(g.to(cuda), False)
+    assert torch.equal(xp.cpu(), Fn.pad(x, (1, 1, 1, 1), mode="reflect"))
+    assert torch.equal(gp.cpu(), Fn.pad(g, (1, 1, 1, 1)))
+    dw2, db2 = A.conv_wgrad(xp, gp, conv)
+    assert rel_l2(dw2, wd.grad) < 1e-5 and rel_l2(db2, bd.grad) < 1e-5
+
+
 @pytest.mark.parametrize("shape", [(2, 5, 8, 8), (1, 3, 7, 9), (2, 4, 1, 5)])
 def test_maxpool_relu_backward(cuda, shape):
     from rpst import autograd as A
