@@ -127,19 +127,26 @@ __global__ __launch_bounds__(256) void reflect_ring_kernel(
   const int64_t HW = (int64_t)H * W;
   const float* dyn = dy + (int64_t)n * Cout * HW;
   float acc[4][4] = {};
-  for (int c0 = 0; c0 < Cout; c0 += CC) {
-    // line[co][t'] = line value at t = u0 - 2 + t' (0 outside [0, L))
-    for (int e = tid; e < CC * 66; e += 256) {
+  // the next co chunk's line and tap values are loaded into registers while the current
+  // chunk computes (the loads are latency-bound: column lines stride W, taps stride 9)
+  constexpr int kLn = (CC * 66 + 255) / 256, kTp = CC * 3 * 64 / 256;
+  float lv[kLn], tv[kTp];
+  auto gload = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < kLn; ++i) {
+      const int e = tid + 256 * i;
       const int cc = e / 66, tt = e - cc * 66, t = u0 - 2 + tt, co = c0 + cc;
       float v = 0.f;
-      if (co < Cout && t >= 0 && t < L) {
+      if (e < CC * 66 && co < Cout && t >= 0 && t < L) {
         const int64_t off = row ? (int64_t)(side == 0 ? 0 : H - 1) * W + t
                                 : (int64_t)t * W + (side == 2 ? 0 : W - 1);
         v = dyn[co * HW + off];
       }
-      line[cc][tt] = v;
+      lv[i] = v;
     }
-    for (int e = tid; e < CC * 3 * 64; e += 256) {
+#pragma unroll
+    for (int i = 0; i < kTp; ++i) {
+      const int e = tid + 256 * i;
       const int cc = e / 192, r = e - cc * 192, k = r / 64, c = r - k * 64;
       const int co = c0 + cc, ci = ci0 + c;
       float v = 0.f;
@@ -147,9 +154,23 @@ __global__ __launch_bounds__(256) void reflect_ring_kernel(
         const int kh = row ? (side == 0 ? 0 : 2) : k, kw = row ? k : (side == 2 ? 0 : 2);
         v = w[((int64_t)co * Cin + ci) * 9 + kh * 3 + kw];
       }
-      taps[cc][k][c] = v;
+      tv[i] = v;
+    }
+  };
+  gload(0);
+  for (int c0 = 0; c0 < Cout; c0 += CC) {
+#pragma unroll
+    for (int i = 0; i < kLn; ++i) {
+      const int e = tid + 256 * i;
+      if (e < CC * 66) line[e / 66][e % 66] = lv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < kTp; ++i) {
+      const int e = tid + 256 * i;
+      taps[e / 192][(e % 192) / 64][e % 64] = tv[i];
     }
     __syncthreads();
+    if (c0 + CC < Cout) gload(c0 + CC);
 #pragma unroll 4
     for (int cc = 0; cc < CC; ++cc) {
 #pragma unroll
