@@ -238,6 +238,10 @@ int rpst_conv_weight_flip(const float* w, float* wt, int Cout, int Cin, int ksiz
 /* ReLU backward: out = y > 0 ? g : 0 (y = the ReLU output), n elements. */
 int rpst_relu_backward(const float* g, const float* y, float* out, int64_t n,
                        rpst_stream_t stream);
+/* LeakyReLU(slope) backward (Conv2dBlock's activation, base.py:147; slope > 0):
+ * out = y > 0 ? g : slope * g (y = the activation output, same sign as its input). */
+int rpst_leaky_relu_backward(const float* g, const float* y, float* out, int64_t n, float slope,
+                             rpst_stream_t stream);
 /* MaxPool2d(2, 2, ceil_mode=True) backward: x (N,C,H,W) the pool input, g the gradient at
  * its output -> dx (N,C,H,W) (argmax as ATen: first max in window order, NaN wins);
  * relu_mask = 1 also applies ReLU backward with y = x (x is a ReLU output). */

@@ -210,6 +210,59 @@ def adain_rp_grads(content, style, sd, rp_blocks, content_weight, style_weight):
     return ({k: v.detach() for k, v in losses.items()}, dict(zip(names, grads)))
 
 
+def _vgg_losses(stylized, style, content_target, sd, content_weight, style_weight):
+    """calc_style_loss at relu1_1..relu4_1 against the style + calc_content_loss of the
+    stylized relu4_1 against content_target (adain_rp.py:130-138, base.py:634-642)."""
+    ds = encode_with_intermediate(stylized, sd)
+    dt = encode_with_intermediate(style, sd)
+    ls = style_loss(ds[0], dt[0])
+    for i in range(1, 4):
+        ls = ls + style_loss(ds[i], dt[i])
+    lc = F.mse_loss(ds[-1], content_target)
+    tot = content_weight * lc + style_weight * ls
+    return {"style_loss": ls, "content_loss": lc, "total_loss": tot}
+
+
+def sourcenet_losses(content, style, sd, content_weight, style_weight):
+    """SourceNet.forward loss dict (base.py:624-649): content target = t = AdaIN of the
+    relu4_1 features (not the content's relu4_1)."""
+    with torch.no_grad():
+        t = adain(encode_with_intermediate(content, sd)[-1], encode_with_intermediate(style, sd)[-1])
+    return _vgg_losses(decoder(t, sd, "decoder."), style, t, sd, content_weight, style_weight)
+
+
+def multiscale_losses(content, style, sd, rp_blocks, inception_num, content_weight,
+                      style_weight):
+    """MultiScaleAdaINRPNet.forward loss dict (adain_rp.py:321-345); the encoder blocks
+    carry inception_num 1x1 convs, the decoder blocks none (rp_constant / rp_shallower
+    decoders, adain_rp.py:152-170)."""
+    def enc(x):
+        feats = []
+        for i in range(rp_blocks):
+            x = conv2d_block(x, sd, f"rp_shared_encoder.{i}.", inception_num)
+            feats.append(x)
+        return feats
+    cfs, sfs = enc(content), enc(style)
+    y = conv2d_block(adain(cfs[-1], sfs[-1]), sd, "rp_decoder.0.")
+    for i, (cf, sf) in enumerate(list(zip(cfs[:-1], sfs[:-1]))[::-1]):
+        y = conv2d_block(y + adain(cf, sf), sd, f"rp_decoder.{i + 1}.")
+    with torch.no_grad():
+        c4 = encode_with_intermediate(content, sd)[-1]
+    return _vgg_losses(y, style, c4, sd, content_weight, style_weight)
+
+
+def grads_of(loss_fn, sd: SD, trainable: Tuple[str, ...], *args):
+    """(loss dict, {name: d total_loss / d param}) by CPU autograd over the sd entries whose
+    names start with one of `trainable` (the VGG stays frozen)."""
+    sd = {k: (v.detach().clone().requires_grad_(k.startswith(trainable))
+              if v.is_floating_point() else v) for k, v in sd.items()}
+    with torch.enable_grad():
+        losses = loss_fn(*args[:2], sd, *args[2:])
+        names = [k for k, v in sd.items() if v.requires_grad]
+        grads = torch.autograd.grad(losses["total_loss"], [sd[k] for k in names])
+    return ({k: v.detach() for k, v in losses.items()}, dict(zip(names, grads)))
+
+
 # ---- a7/a8/a9: WCT ----------------------------------------------------------------
 def _psd_power(A: Tensor, p: float) -> Tensor:
     """matrix_sqrt / matrix_inv_sqrt body (wct_rp.py:7-40): +1e-4 on the diagonal,

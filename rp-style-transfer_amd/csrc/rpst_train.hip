@@ -33,21 +33,25 @@ __global__ __launch_bounds__(256) void conv_flip_kernel(const float* __restrict_
 }
 
 // ---- ReLU backward: threshold_backward(grad, output, 0) -----------------------------------
+// slope = 0: ReLU (threshold_backward: g where y > 0, else 0); slope > 0: LeakyReLU
+// (Conv2dBlock base.py:147; leaky_relu_backward on the result: g where y > 0, else slope g)
 __global__ __launch_bounds__(256) void relu_backward_kernel(const float* __restrict__ g,
                                                             const float* __restrict__ y,
-                                                            float* __restrict__ out, int64_t n) {
+                                                            float* __restrict__ out, int64_t n,
+                                                            float slope) {
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  auto f = [slope](float gv, float yv) { return yv > 0.f ? gv : (slope == 0.f ? 0.f : gv * slope); };
   if (i + 3 < n) {
     const float4 gv = *reinterpret_cast<const float4*>(g + i);
     const float4 yv = *reinterpret_cast<const float4*>(y + i);
     float4 o;
-    o.x = yv.x > 0.f ? gv.x : 0.f;
-    o.y = yv.y > 0.f ? gv.y : 0.f;
-    o.z = yv.z > 0.f ? gv.z : 0.f;
-    o.w = yv.w > 0.f ? gv.w : 0.f;
+    o.x = f(gv.x, yv.x);
+    o.y = f(gv.y, yv.y);
+    o.z = f(gv.z, yv.z);
+    o.w = f(gv.w, yv.w);
     *reinterpret_cast<float4*>(out + i) = o;
   } else {
-    for (int64_t j = i; j < n; ++j) out[j] = y[j] > 0.f ? g[j] : 0.f;
+    for (int64_t j = i; j < n; ++j) out[j] = f(g[j], y[j]);
   }
 }
 
@@ -556,7 +560,15 @@ extern "C" int rpst_conv_weight_flip(const float* w, float* wt, int Cout, int Ci
 extern "C" int rpst_relu_backward(const float* g, const float* y, float* out, int64_t n,
                                   rpst_stream_t stream) {
   RPST_REQUIRE(g && y && out && n > 0, "relu_backward: bad args");
-  relu_backward_kernel<<<blocks_for((n + 3) / 4), 256, 0, as_stream(stream)>>>(g, y, out, n);
+  relu_backward_kernel<<<blocks_for((n + 3) / 4), 256, 0, as_stream(stream)>>>(g, y, out, n, 0.f);
+  return launch_status("relu_backward_kernel");
+}
+
+extern "C" int rpst_leaky_relu_backward(const float* g, const float* y, float* out, int64_t n,
+                                        float slope, rpst_stream_t stream) {
+  RPST_REQUIRE(g && y && out && n > 0 && slope > 0.f, "leaky_relu_backward: bad args");
+  relu_backward_kernel<<<blocks_for((n + 3) / 4), 256, 0, as_stream(stream)>>>(g, y, out, n,
+                                                                               slope);
   return launch_status("relu_backward_kernel");
 }
 

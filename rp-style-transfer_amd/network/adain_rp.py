@@ -233,8 +233,15 @@ class MultiScaleAdaINRPNet(AdaINRPNet):
         return stylized
 
     def forward(self, content, style, alpha=1.0):
-        """Loss dict of adain_rp.py:322-345 (inference kernels: call under torch.no_grad())."""
+        """Loss dict of adain_rp.py:322-345. With autograd enabled and trainable RP
+        parameters the losses come from rpst.autograd._MultiScaleStep (forward and backward
+        kernels; total_loss.backward() fills the RP encoder / decoder gradients); under
+        no_grad it is evaluated op by op."""
         assert 0 <= alpha <= 1
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            self._kernel_path_check(self.config['use_mask'])
+            from rpst.autograd import multiscale_losses
+            return multiscale_losses(self, content, style)
         content_feats = self.encode_rp_intermediate(content)
         style_feats = self.encode_rp_intermediate(style)
         stylized = self.decode(content_feats, style_feats)

@@ -312,8 +312,14 @@ class SourceNet(BaseNet):
         return mse(input_mean, target_mean) + mse(input_std, target_std)
 
     def forward(self, content, style, alpha=1.0):
-        """Loss dict of base.py:624-649 (inference kernels: call under torch.no_grad())."""
+        """Loss dict of base.py:624-649. With autograd enabled and a trainable decoder the
+        losses come from rpst.autograd._SourceNetStep (forward and backward kernels;
+        total_loss.backward() fills the decoder gradients); under no_grad it is evaluated
+        op by op."""
         assert 0 <= alpha <= 1
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            from rpst.autograd import sourcenet_losses
+            return sourcenet_losses(self, content, style)
         content_feats = self.encode_with_intermediate(content)
         style_feats = self.encode_with_intermediate(style)
         t = adaptive_instance_normalization(content_feats[-1], style_feats[-1])

@@ -49,6 +49,7 @@ SIGNATURES = {
     "rpst_sanet_attention": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
     "rpst_conv_weight_flip": (_I, [_P, _P, _I, _I, _I, _P]),
     "rpst_relu_backward": (_I, [_P, _P, _P, _I64, _P]),
+    "rpst_leaky_relu_backward": (_I, [_P, _P, _P, _I64, _F, _P]),
     "rpst_maxpool2x2_ceil_backward": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "rpst_reflect_pad_border_grad_workspace_size": (_SZ, [_I, _I, _I, _I]),
     "rpst_reflect_pad_border_grad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),

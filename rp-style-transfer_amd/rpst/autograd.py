@@ -148,7 +148,11 @@ class _VGGLoss:
     and content batches: forward keeps what the backward needs, backward returns
     d total / d stylized through the frozen VGG."""
 
-    def __init__(self, model, stylized, content, style, cw, sw):
+    def __init__(self, model, stylized, content, style, cw, sw, targets=None,
+                 content_target=None):
+        """targets: the VGG relu1_1..relu4_1 features of [style; content] when the caller
+        already has them; content_target: the relu4_1 target of the content loss (default
+        the content's relu4_1; SourceNet's is the AdaIN feature t, base.py:636)."""
         n = stylized.shape[0]
         vgg_steps, vgg_saved, taps, x = [], [], [], stylized
         for i in range(4):
@@ -157,11 +161,12 @@ class _VGGLoss:
             vgg_steps += st
             vgg_saved += sv
             taps.append(len(vgg_steps) - 1)
-        ref = torch.cat([style, content], dim=0)
-        targets = []
-        for i in range(4):
-            ref = getattr(model, f"enc_{i + 1}")(ref)
-            targets.append(ref)
+        if targets is None:
+            ref = torch.cat([style, content], dim=0)
+            targets = []
+            for i in range(4):
+                ref = getattr(model, f"enc_{i + 1}")(ref)
+                targets.append(ref)
         stats, loss_s = [], []
         for i, k in enumerate(taps):
             F = vgg_saved[k][1]
@@ -171,7 +176,7 @@ class _VGGLoss:
                                     sdt.reshape(-1)]))
             loss_s.append(sq_diff_mean(mu, mut) + sq_diff_mean(sd, sdt))
         self.ls = loss_s[0] + loss_s[1] + loss_s[2] + loss_s[3]
-        self.content4 = targets[3][n:].contiguous()
+        self.content4 = (targets[3][n:] if content_target is None else content_target).contiguous()
         self.lc = sq_diff_mean(vgg_saved[taps[3]][1], self.content4)
         self.total = cw * self.lc + sw * self.ls
         self.cw, self.sw = cw, sw
@@ -411,7 +416,7 @@ def _vgg_backward(steps, saved, taps, seed_fn):
     return g
 
 
-def _decoder_backward(steps, saved, g, grads):
+def _decoder_backward(steps, saved, g, grads, need_input_grad: bool = True):
     """Decoder (sanet.py:162-192: reflect-pad conv3x3 + ReLU, nearest x2 upsample fused
     into the next conv's loader): parameter gradients into grads, returns d input."""
     for k in range(len(steps) - 1, -1, -1):
@@ -426,6 +431,8 @@ def _decoder_backward(steps, saved, g, grads):
         dw, db = _wgrad_reflect(xc, g, s.conv)
         _acc(grads, s.conv.weight, dw)
         _acc(grads, s.conv.bias, db)
+        if k == 0 and not need_input_grad:
+            return None
         g = conv_dgrad(g, s)
         if up:
             g = _upsample_backward(g)
@@ -626,3 +633,184 @@ def samodel_losses(model, content: torch.Tensor, style: torch.Tensor
                                                style.detach().contiguous(), model, cfg, *params)
     return {'style_loss': ls, 'content_loss': lc, 'l_identity1_loss': l1,
             'l_identity2_loss': l2, 'total_loss': total}, total
+
+
+# ---- SourceNet (base.py:624-649) and MultiScaleAdaINRPNet (adain_rp.py:321-345) -----------
+def act_backward(g: torch.Tensor, y: torch.Tensor, act: int) -> torch.Tensor:
+    """Backward of a conv epilogue activation from its output y (ops.ACT_*)."""
+    if act == ops.ACT_RELU:
+        return relu_backward(g, y)
+    if act == ops.ACT_LRELU:
+        out = torch.empty_like(g)
+        _lib.call("rpst_leaky_relu_backward", g.data_ptr(), y.data_ptr(), out.data_ptr(),
+                  g.numel(), 0.2, _stream(g))
+        return out
+    return g
+
+
+def _conv_steps_backward(steps, saved, g, grads, need_input_grad: bool):
+    """Backward through compiled conv steps without input operators: 3x3 convs with zero or
+    reflect padding (wgrad kernel, the reflection read in its loader; dgrad + reflect border
+    fold) and 1x1 convs (Conv2dBlock's inception convs, base.py:166-171: weight gradient as
+    a batched GEMM), each with its ReLU / LeakyReLU(0.2) epilogue. Parameter gradients add
+    into grads; returns d input (None when not needed)."""
+    for k in range(len(steps) - 1, -1, -1):
+        s = steps[k]
+        x_in, y = saved[k]
+        if s.in_op != ops.IN_NONE:
+            raise NotImplementedError("rpst autograd: conv block input operator")
+        g = act_backward(g, y, s.relu)
+        if s.conv.kernel_size[0] == 3:
+            dw, db = conv_wgrad(x_in, g, s.conv, s.pad)
+        else:
+            dw, db = _lin_grads(g, x_in)
+            db = db if s.conv.bias is not None else None
+        _acc(grads, s.conv.weight, dw)
+        if s.conv.bias is not None:
+            _acc(grads, s.conv.bias, db)
+        if k > 0 or need_input_grad:
+            g = conv_dgrad(g, s)
+    return g if need_input_grad else None
+
+
+def _adain_state(cf: torch.Tensor, sf: torch.Tensor):
+    mc, sc = ops.calc_mean_std(cf)
+    ms, ss = ops.calc_mean_std(sf)
+    return cf, sf, torch.cat([mc.reshape(-1), sc.reshape(-1), ms.reshape(-1), ss.reshape(-1)])
+
+
+def _adain_backward(g: torch.Tensor, state) -> torch.Tensor:
+    """d AdaIN(cf, sf) -> [d cf; d sf] stacked along the batch (the shared encoder's
+    [content; style] layout)."""
+    cf, sf, st = state
+    n = cf.shape[0]
+    d = torch.empty((2 * n,) + tuple(cf.shape[1:]), device=g.device, dtype=torch.float32)
+    planes = cf.shape[0] * cf.shape[1]
+    hw = cf.shape[2] * cf.shape[3]
+    ws = torch.empty(2 * planes, device=g.device, dtype=torch.float32)
+    _lib.call("rpst_adain_backward", g.data_ptr(), cf.data_ptr(), sf.data_ptr(), st.data_ptr(),
+              d[:n].data_ptr(), d[n:].data_ptr(), planes, hw, ws.data_ptr(), ws.numel() * 4,
+              _stream(g))
+    return d
+
+
+class _SourceNetStep(torch.autograd.Function):
+    """SourceNet.forward (base.py:624-649): VGG relu1_1..relu4_1 of content and style (frozen,
+    constants of the step), t = AdaIN(c4, s4), g_t = decoder(t); style loss at the four taps,
+    content loss of g_t's relu4_1 against t. Only the decoder trains."""
+
+    @staticmethod
+    def forward(ctx, content, style, model, cw, sw, *params):
+        with ops.precise_convs():
+            n = content.shape[0]
+            ref, targets = torch.cat([style, content], dim=0), []
+            for i in range(4):
+                ref = getattr(model, f"enc_{i + 1}")(ref)
+                targets.append(ref)
+            t = ops.adaptive_instance_normalization(targets[3][n:], targets[3][:n])
+            dec_steps = plan.compile_layers(model.decoder.children())
+            stylized, dec_saved = _run_steps_saving(dec_steps, t)
+            loss = _VGGLoss(model, stylized, content, style, cw, sw, targets=targets,
+                            content_target=t)
+        ctx.loss, ctx.dec_steps, ctx.dec_saved, ctx.params = loss, dec_steps, dec_saved, params
+        return loss.total, loss.ls, loss.lc
+
+    @staticmethod
+    def backward(ctx, g_total, g_ls, g_lc):
+        with ops.precise_convs():
+            g = ctx.loss.backward(g_total, g_ls, g_lc)
+            grads: Dict[int, torch.Tensor] = {}
+            _decoder_backward(ctx.dec_steps, ctx.dec_saved, g, grads, need_input_grad=False)
+        ctx.dec_saved = None
+        return (None, None, None, None, None, *[grads.get(id(p)) for p in ctx.params])
+
+
+class _MultiScaleStep(torch.autograd.Function):
+    """MultiScaleAdaINRPNet.forward (adain_rp.py:321-345) for the constant / deeper stacks.
+
+    Forward: the shared encoder over [content; style] block by block (every block output is
+    a level, every conv's input / output kept); decoder block 0 on AdaIN(level L-1), block k
+    on y_{k-1} + AdaIN(level L-1-k) (adain_rp.py:291-302; the sums and AdaIN outputs are
+    materialised, they are the blocks' wgrad inputs); VGG losses on the stylized batch.
+    Backward: VGG dgrad -> decoder blocks (LeakyReLU, 1x1 / reflect 3x3 wgrad + dgrad); the
+    gradient at each block input passes unchanged to the previous block's output and through
+    AdaIN backward to the level's content and style features; the encoder walks back with
+    each level's [d content; d style] added at its block output."""
+
+    @staticmethod
+    def forward(ctx, content, style, model, cw, sw, *params):
+        with ops.precise_convs():
+            n = content.shape[0]
+            x, enc, levels = torch.cat([content, style], dim=0), [], []
+            for blk in model.rp_shared_encoder:
+                st = plan.compile_layers(plan.block_layers(blk))
+                x, sv = _run_steps_saving(st, x)
+                enc.append((st, sv))
+                levels.append(x)
+            L = len(levels)
+            dec, states = [], []
+            y = None
+            for k, blk in enumerate(model.rp_decoder):
+                lv = levels[L - 1 - k]
+                state = _adain_state(lv[:n], lv[n:])
+                z = ops.adaptive_instance_normalization(lv[:n], lv[n:])
+                if y is not None:
+                    z.add_(y)
+                st = plan.compile_layers(plan.block_layers(blk))
+                y, sv = _run_steps_saving(st, z)
+                dec.append((st, sv))
+                states.append(state)
+                if k == L - 1:
+                    break
+            loss = _VGGLoss(model, y, content, style, cw, sw)
+        ctx.loss, ctx.enc, ctx.dec, ctx.states, ctx.params = loss, enc, dec, states, params
+        return loss.total, loss.ls, loss.lc
+
+    @staticmethod
+    def backward(ctx, g_total, g_ls, g_lc):
+        with ops.precise_convs():
+            g = ctx.loss.backward(g_total, g_ls, g_lc)
+            grads: Dict[int, torch.Tensor] = {}
+            L = len(ctx.enc)
+            dlev = [None] * L
+            for k in range(len(ctx.dec) - 1, -1, -1):
+                st, sv = ctx.dec[k]
+                g = _conv_steps_backward(st, sv, g, grads, need_input_grad=True)
+                dlev[L - 1 - k] = _adain_backward(g, ctx.states[k])
+            ge = None
+            for i in range(L - 1, -1, -1):
+                if dlev[i] is not None:
+                    ge = dlev[i] if ge is None else ge.add_(dlev[i])
+                if ge is None:
+                    continue
+                st, sv = ctx.enc[i]
+                ge = _conv_steps_backward(st, sv, ge, grads, need_input_grad=i > 0)
+        ctx.enc = ctx.dec = ctx.states = None
+        return (None, None, None, None, None, *[grads.get(id(p)) for p in ctx.params])
+
+
+def sourcenet_losses(model, content: torch.Tensor, style: torch.Tensor
+                     ) -> Tuple[Dict[str, torch.Tensor], torch.Tensor]:
+    """SourceNet.forward with autograd: the loss dict and total_loss, differentiable w.r.t.
+    the decoder parameters."""
+    ops._check(content, style)
+    params: List[torch.Tensor] = list(model.decoder.parameters())
+    cw = float(model.config['content_weight'])
+    sw = float(model.config['style_weight'])
+    total, ls, lc = _SourceNetStep.apply(content.detach().contiguous(),
+                                         style.detach().contiguous(), model, cw, sw, *params)
+    return {'style_loss': ls, 'content_loss': lc, 'total_loss': total}, total
+
+
+def multiscale_losses(model, content: torch.Tensor, style: torch.Tensor
+                      ) -> Tuple[Dict[str, torch.Tensor], torch.Tensor]:
+    """MultiScaleAdaINRPNet.forward with autograd: the loss dict and total_loss,
+    differentiable w.r.t. the RP encoder / decoder parameters."""
+    ops._check(content, style)
+    params: List[torch.Tensor] = (list(model.rp_shared_encoder.parameters()) +
+                                  list(model.rp_decoder.parameters()))
+    cw = float(model.config['content_weight'])
+    sw = float(model.config['style_weight'])
+    total, ls, lc = _MultiScaleStep.apply(content.detach().contiguous(),
+                                          style.detach().contiguous(), model, cw, sw, *params)
+    return {'style_loss': ls, 'content_loss': lc, 'total_loss': total}, total

@@ -46,7 +46,9 @@ def build_network(opt, synthetic_seed=None):
         vgg.load_state_dict(torch.load(opt["vgg"], weights_only=True))
     vgg_relu4_1 = nn.Sequential(*list(vgg.children())[:31])
     kind = opt["network"]
-    if kind == "adain":
+    if kind == "src":  # train.py:93-94
+        m = net.SourceNet(opt, vgg_relu4_1)
+    elif kind == "adain":
         m = net.AdaINRPNet(opt, vgg_relu4_1)
     elif kind == "multi_adain":
         m = net.MultiScaleAdaINRPNet(opt, vgg_relu4_1)

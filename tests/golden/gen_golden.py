@@ -492,6 +492,66 @@ def gen_sourcenet(net):
     np.savez_compressed(os.path.join(HERE, "sourcenet.npz"), n=len(cases), **out)
 
 
+def gen_grads_src(net):
+    """Reference SourceNet.forward + total_loss.backward() (base.py:624-649; only the
+    decoder trains): the losses and probes of every decoder gradient."""
+    out = {}
+    cases = [((1, 3, 32, 32), 53, 1.0, 10.0), ((2, 3, 40, 48), 54, 1.0, 1.0)]
+    for i, (shp, seed, cw, sw) in enumerate(cases):
+        m = net.SourceNet({"use_mask": False, "content_weight": cw, "style_weight": sw},
+                          copy.deepcopy(net.vgg))
+        m.decoder = copy.deepcopy(m.decoder)  # the module-level decoder is shared
+        ck = synth_model_(m, seed)
+        c = synth.image(5300 + i, shp)
+        s = synth.image(5400 + i, shp)
+        m.zero_grad()
+        d, tot = m.forward(t(c), t(s))
+        tot.backward()
+        out.update({f"seed{i}": seed, f"checksum{i}": ck, f"cw{i}": cw, f"sw{i}": sw,
+                    f"content{i}": c, f"style{i}": s})
+        for k, v in d.items():
+            out[f"{k}{i}"] = v.detach().numpy()
+        names = []
+        for name, p in m.named_parameters():
+            if p.grad is not None:
+                out[f"gprobe{i}:{name}"] = helpers.grad_probe(name, p.grad.numpy())
+                names.append(name)
+        out[f"names{i}"] = np.array(names)
+    np.savez_compressed(os.path.join(HERE, "grads_src.npz"), n=len(cases), **out)
+
+
+def gen_grads_ms(net):
+    """Reference MultiScaleAdaINRPNet.forward + total_loss.backward() (adain_rp.py:321-345):
+    the constant stack with one inception conv per encoder block, and the 'deeper' stack of
+    config/rl/train_deeper_multiscale_rp_adain.yaml (3 inception convs): the losses and every
+    RP encoder / decoder gradient."""
+    out = {}
+    cases = [(8, 5, 1, "constant", (2, 3, 32, 32), 55, 1.0, 10.0),
+             (4, 5, 3, "deeper", (1, 3, 48, 40), 56, 1.0, 1.0)]
+    for i, (hid, blocks, inc, way, shp, seed, cw, sw) in enumerate(cases):
+        cfg = multiscale_config(hid, blocks, inc)
+        cfg.update(enc_stack_way=way, content_weight=cw, style_weight=sw)
+        m = net.MultiScaleAdaINRPNet(cfg, copy.deepcopy(net.vgg))
+        ck = synth_model_(m, seed)
+        c = synth.image(5500 + i, shp)
+        s = synth.image(5600 + i, shp)
+        m.zero_grad()
+        d, tot = m.forward(t(c), t(s))
+        tot.backward()
+        out.update({f"hidden{i}": hid, f"blocks{i}": blocks, f"inception{i}": inc,
+                    f"way{i}": way, f"seed{i}": seed, f"checksum{i}": ck, f"cw{i}": cw,
+                    f"sw{i}": sw, f"content{i}": c, f"style{i}": s})
+        for k, v in d.items():
+            out[f"{k}{i}"] = v.detach().numpy()
+        names = []
+        for name, p in m.named_parameters():
+            if p.grad is not None:
+                out[f"grad{i}:{name}"] = p.grad.numpy()
+                names.append(name)
+        out[f"names{i}"] = np.array(names)
+    np.savez_compressed(os.path.join(HERE, "grads_ms.npz"), n=len(cases), **out)
+
+
 def gen_keys(net):
     """state_dict key/shape lists of the reference models (checkpoint compatibility)."""
     import json
@@ -519,7 +579,8 @@ GENERATORS = {"keys": gen_keys, "stats": gen_stats, "adain_rp": gen_adain_rp,
               "multiscale": gen_multiscale, "sourcenet": gen_sourcenet,
               "adaptive": gen_adaptive, "deeper": gen_deeper, "grads": gen_grads,
               "grads_wct": gen_grads_wct, "wct_large": gen_wct_large,
-              "grads_sam": gen_grads_sam}
+              "grads_sam": gen_grads_sam, "grads_src": gen_grads_src,
+              "grads_ms": gen_grads_ms}
 
 
 def main():

@@ -59,6 +59,19 @@ def deeper_config(hidden, blocks=5, inception=3):
     return cfg
 
 
+def ms_grads_config(g, i):
+    """The MultiScaleAdaINRPNet config of case i of tests/golden/grads_ms.npz."""
+    cfg = multiscale_config(int(g[f"hidden{i}"]), int(g[f"blocks{i}"]), int(g[f"inception{i}"]))
+    cfg.update(enc_stack_way=str(g[f"way{i}"]), content_weight=float(g[f"cw{i}"]),
+               style_weight=float(g[f"sw{i}"]))
+    return cfg
+
+
+def src_grads_config(g, i):
+    """The SourceNet config of case i of tests/golden/grads_src.npz."""
+    return dict(SOURCE_CONFIG, content_weight=float(g[f"cw{i}"]), style_weight=float(g[f"sw{i}"]))
+
+
 def grad_probe(key, g):
     """(sum, sum of squares, dot with a fixed uniform probe) of one gradient tensor
     (tests/golden/gen_golden.gen_grads_sam stores these instead of ~8M SAModel gradients)."""

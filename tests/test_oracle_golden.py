@@ -246,6 +246,52 @@ def test_reference_samodel_training_gradients(golden):
             assert e < 1e-5, (i, name, e)
 
 
+def test_reference_sourcenet_training_gradients(golden):
+    """R.sourcenet_losses under CPU autograd against the reference's SourceNet.forward +
+    backward (base.py:624-649): the losses and probes of every decoder gradient."""
+    import network as net
+    from helpers import grad_probe, probe_err, src_grads_config
+    g = golden("grads_src")
+    for i in range(int(g["n"])):
+        cfg = src_grads_config(g, i)
+        m = net.SourceNet(cfg, copy.deepcopy(net.vgg))
+        m.decoder = copy.deepcopy(m.decoder)
+        np.testing.assert_allclose(synth_(m, int(g[f"seed{i}"])), g[f"checksum{i}"], rtol=1e-12)
+        losses, grads = R.grads_of(R.sourcenet_losses, state_dict_of(m), ("decoder.",),
+                                   t(g[f"content{i}"]), t(g[f"style{i}"]),
+                                   cfg["content_weight"], cfg["style_weight"])
+        for k in ("style_loss", "content_loss", "total_loss"):
+            np.testing.assert_allclose(losses[k].numpy(), g[f"{k}{i}"], rtol=1e-5)
+        names = [str(n) for n in g[f"names{i}"]]
+        assert sorted(names) == sorted(grads)
+        for name in names:
+            e = probe_err(grad_probe(name, grads[name]), g[f"gprobe{i}:{name}"], grads[name].numel())
+            assert e < 1e-5, (i, name, e)
+
+
+def test_reference_multiscale_training_gradients(golden):
+    """R.multiscale_losses under CPU autograd against the reference's
+    MultiScaleAdaINRPNet.forward + backward (adain_rp.py:321-345): constant stack with an
+    inception conv, and the 'deeper' stack; every RP encoder / decoder gradient."""
+    import network as net
+    from helpers import ms_grads_config
+    g = golden("grads_ms")
+    for i in range(int(g["n"])):
+        cfg = ms_grads_config(g, i)
+        m = net.MultiScaleAdaINRPNet(cfg, copy.deepcopy(net.vgg))
+        np.testing.assert_allclose(synth_(m, int(g[f"seed{i}"])), g[f"checksum{i}"], rtol=1e-12)
+        losses, grads = R.grads_of(R.multiscale_losses, state_dict_of(m),
+                                   ("rp_shared_encoder.", "rp_decoder."), t(g[f"content{i}"]),
+                                   t(g[f"style{i}"]), cfg["rp_blocks"], cfg["inception_num"],
+                                   cfg["content_weight"], cfg["style_weight"])
+        for k in ("style_loss", "content_loss", "total_loss"):
+            np.testing.assert_allclose(losses[k].numpy(), g[f"{k}{i}"], rtol=1e-5)
+        names = [str(n) for n in g[f"names{i}"]]
+        assert sorted(names) == sorted(grads)
+        for name in names:
+            assert rel_l2(grads[name], g[f"grad{i}:{name}"]) < 1e-5, (i, name)
+
+
 def test_sourcenet_test(golden):
     """SourceNet.test (classic AdaIN) against the reference."""
     import network as net
