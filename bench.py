@@ -79,6 +79,12 @@ def build_model(kind, dev):
         m = net.WCTRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
     elif kind == "train_sanet":
         m = net.SAModel(dict(SANET_TRAIN_CONFIG), copy.deepcopy(net.vgg), 0, 512)
+    elif kind == "train_multiscale":
+        m = net.MultiScaleAdaINRPNet(dict(MULTISCALE_CONFIG, style_weight=1.0),
+                                     copy.deepcopy(net.vgg))
+    elif kind == "train_source":
+        m = net.SourceNet(dict(SOURCE_CONFIG), copy.deepcopy(net.vgg))
+        m.decoder = copy.deepcopy(m.decoder)  # the module-level decoder is shared
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, 512)
     synth.synth_module_(m, 0)
@@ -98,7 +104,7 @@ ADAPTIVE_CONFIG = {"ada_module": "relu", "content_weight": 1.0, "style_weight": 
 # config/rl/train_static_sanet.yaml loss weights
 SANET_TRAIN_CONFIG = {"content_weight": 1.0, "style_weight": 3.0, "l_identity1_weight": 50.0,
                       "l_identity2_weight": 1.0}
-TRAIN_KINDS = ("train", "train_wct", "train_sanet")
+TRAIN_KINDS = ("train", "train_wct", "train_sanet", "train_multiscale", "train_source")
 
 
 WORKLOADS = {
@@ -119,13 +125,20 @@ WORKLOADS = {
     "train_sanet": "SAModel training iteration: forward() losses (g_t style/content, identity "
                    "1/2 over Icc, Iss) + total_loss.backward() + Adam step on the transform and "
                    "decoder, config/rl/train_static_sanet.yaml weights (SURVEY 8(f) rank 2)",
+    "train_multiscale": "MultiScaleAdaINRPNet training iteration: forward() losses + "
+                        "total_loss.backward() + Adam step, constant stack hidden 32 x 5 "
+                        "(SURVEY 8(f) ranks 1-2)",
+    "train_source": "SourceNet training iteration: forward() losses + total_loss.backward() + "
+                    "Adam step on the decoder (SURVEY 8(f) ranks 2-3)",
     "selftest": "CPU stand-in per-image function (launcher / timing / gather test only)",
 }
 DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32, "multiscale": 32, "source": 32,
                  "adaptive": 32, "train": 8, "train_wct": 8, "train_sanet": 8,
+                 "train_multiscale": 8, "train_source": 8,
                  "selftest": 4}
 # CPU-baseline sample per workload (BASELINE.md plan: B=2 at 512^2, B=1 for WCT)
-CPU_SAMPLE_BATCH = {"wct": 1, "train": 1, "train_wct": 1, "train_sanet": 1}
+CPU_SAMPLE_BATCH = {"wct": 1, "train": 1, "train_wct": 1, "train_sanet": 1,
+                    "train_multiscale": 1, "train_source": 1}
 
 
 def cpu_info():
@@ -177,6 +190,15 @@ def cpu_baseline(kind, size, reps=3):
     elif kind == "train_sanet":
         m = net.SAModel(dict(SANET_TRAIN_CONFIG), copy.deepcopy(net.vgg), 0, size)
         fn = lambda c, s, sd: R.samodel_grads(c, s, sd, SANET_TRAIN_CONFIG)  # noqa: E731
+    elif kind == "train_multiscale":
+        m = net.MultiScaleAdaINRPNet(dict(MULTISCALE_CONFIG, style_weight=1.0),
+                                     copy.deepcopy(net.vgg))
+        fn = lambda c, s, sd: R.grads_of(  # noqa: E731
+            R.multiscale_losses, sd, ("rp_shared_encoder.", "rp_decoder."), c, s, 5, 0, 1.0, 1.0)
+    elif kind == "train_source":
+        m = net.SourceNet(dict(SOURCE_CONFIG), copy.deepcopy(net.vgg))
+        fn = lambda c, s, sd: R.grads_of(  # noqa: E731
+            R.sourcenet_losses, sd, ("decoder.",), c, s, 1.0, 10.0)
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, size)
         fn = R.samodel_test

@@ -541,14 +541,14 @@ def test_multiscale_and_sourcenet_training_deterministic(cuda):
             gs.append([p.grad.clone() for p in m.parameters() if p.grad is not None])
         assert len(gs[0]) == sum(1 for p in m.parameters() if p.requires_grad)
         assert all(torch.equal(a, b) for a, b in zip(*gs))
-        opt = torch.optim.Adam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
+        opt = torch.optim.Adam([p for p in m.parameters() if p.requires_grad], lr=1e-4)
         totals = []
         for _ in range(5):
             opt.zero_grad()
             _, total = m(c, s)
             total.backward()
             opt.step()
-            totals.append(float(total))
+            totals.append(float(total.detach()))
         assert totals[-1] < totals[0], totals
 
 
