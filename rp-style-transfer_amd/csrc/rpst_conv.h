@@ -224,7 +224,7 @@ constexpr int kWinoNTH = 256;  // threads per block
 // tile shape in use: output channels (BM) x rows (TH, x kTW columns) per block
 int wino_bm();
 int wino_th();
-int wino_persist(int in_op);  // 1: grid over spatial tiles only, each block loops over co tiles
+int wino_persist(int in_op, int64_t spatial_blocks);  // 1: grid over spatial tiles only, each block loops over co tiles
 // floats of the Winograd weight image (stored after the direct image for 3x3 convs)
 size_t wino_packed_floats(int Cout, int Cin);
 int wino_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);

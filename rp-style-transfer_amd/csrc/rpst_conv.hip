@@ -644,7 +644,7 @@ static ConvGeom conv_geom(int N, int Cin, int Hs, int Ws, int Cout, int ksize, i
   if (g.algo == RPST_CONV_WINOGRAD) {
     const int th = wino_th(), bm = wino_bm();
     const int ty = (H + th - 1) / th;
-    g.blocks = (int64_t)g.tiles_x * ty * N * (wino_persist(in_op) ? 1 : (Cout + bm - 1) / bm);
+    g.blocks = (int64_t)g.tiles_x * ty * N * (wino_persist(in_op, (int64_t)g.tiles_x * ty * N) ? 1 : (Cout + bm - 1) / bm);
     g.nth = kWinoNTH;
     g.stat_P = g.tiles_x * ty;
     g.stat_nt = th;

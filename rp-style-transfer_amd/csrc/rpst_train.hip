@@ -15,6 +15,8 @@
 //   losses            loss_seed_kernel (d/dF of calc_style_loss + calc_content_loss) and
 //                       sq_diff_sum_kernel (the loss values)
 // All reductions are fixed-order (no float atomics): results are deterministic.
+#include <cstdlib>
+
 #include "rpst_common.h"
 
 namespace rpst {
@@ -255,41 +257,47 @@ __global__ __launch_bounds__(256) void reflect_fold_kernel(
 // reflect != 0: ReflectionPad2d(1) instead (the decoders of sanet.py:162-192): rows -1 / H and
 // columns -1 / W of X read rows / columns 1 / H - 2 (only column W inside a segment needs a
 // fix-up: columns past it multiply a zero dY).
-// Block: 256 threads (2 x 2 waves), tile 64 co x 64 ci, all 9 taps (9 accumulators per wave).
-// K = pixels, walked in row segments of 64 columns: LDS holds dY[px][co] (64 x 65) and
-// X[row][col][ci] (3 x 66 x 65, rows y-1..y+1, columns x0-1..x0+64, zero outside the image);
+// Block: 256 threads (4 waves), all 9 taps (9 accumulators per wave). TC = 64: tile 64 co x
+// 64 ci split 2 x 2 over the waves, K = pixels walked in row segments of PX = 64 columns.
+// TC = 32 (Cin, Cout <= 32: the RP stacks' 3..32-channel layers, where a 64-wide tile would
+// be 3/4 padding): tile 32 co x 32 ci, segments of PX = 128 columns, and the four waves
+// split the segment's pixels (32 each) as four split-K partials of their own (the reduce
+// kernel sums 4 x splits partials). LDS holds dY[px][co] (PX x (TC+1)) and X[row][col][ci]
+// (3 x (PX+2) x (TC+1), rows y-1..y+1, columns x0-1..x0+PX, zero outside the image);
 // v_mfma_f32_32x32x2_f32 with A = dY (co x px) and B = X shifted by the tap (px x ci).
-// Staging: thread -> (channel c = tid / 4, quarter q = tid % 4 of the 64 columns); the next
-// segment's 16-B buffer loads (dY 4, X 12, X halo 3 per thread) are issued into registers
-// before the current segment's MFMAs and written to LDS after them (one load latency per
-// segment, hidden behind 288 MFMAs per wave). Rows / channels outside the image read the
-// out-of-range offset (0), columns at or past W are masked. Blocks of the first ci tile also
-// reduce the bias gradient (sum of dY over their pixels) from the staged dY tile.
-constexpr int kWgTile = 64, kWgPx = 64, kWgLd = 65, kWgCols = kWgPx + 2;
+// Staging: thread -> (channel c = tid / (256/TC), 16-column group q of the PX columns); the
+// next segment's 16-B buffer loads (dY 4, X 12, X halo 3 per thread) are issued into
+// registers before the current segment's MFMAs and written to LDS after them (one load
+// latency per segment, hidden behind 288 (TC 64) / 144 (TC 32) MFMAs per wave). Rows /
+// channels outside the image read the out-of-range offset (0), columns at or past W are
+// masked. Blocks of the first ci tile also reduce the bias gradient (sum of dY over their
+// pixels) from the staged dY tile.
 constexpr unsigned kWgOOB = 0x80000000u;
 
 typedef unsigned wg_u32x4 __attribute__((ext_vector_type(4)));
 
-template <bool VEC>
+template <bool VEC, int TC>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(
     const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ part,
     float* __restrict__ bpart, int N, int Cin, int H, int W, int Cout, int64_t segs_per_split,
     int reflect) {
-  __shared__ float Ys[kWgPx * kWgLd];
-  __shared__ float Xs[3 * kWgCols * kWgLd];
-  const int tilesCi = (Cin + kWgTile - 1) / kWgTile;
+  constexpr int PX = 4096 / TC, LD = TC + 1, COLS = PX + 2, QN = PX / 16;
+  constexpr int KSPL = TC == 32 ? 4 : 1;  // per-wave pixel split (partials per split)
+  __shared__ float Ys[PX * LD];
+  __shared__ float Xs[3 * COLS * LD];
+  const int tilesCi = (Cin + TC - 1) / TC;
   const int tile = blockIdx.x, split = blockIdx.y;
-  const int co0 = (tile / tilesCi) * kWgTile, ci0 = (tile % tilesCi) * kWgTile;
+  const int co0 = (tile / tilesCi) * TC, ci0 = (tile % tilesCi) * TC;
   const bool bias_tile = bpart != nullptr && (tile % tilesCi) == 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = KSPL > 1 ? 0 : wave >> 1, wn = KSPL > 1 ? 0 : wave & 1;
   const int h = lane >> 5, j = lane & 31;
-  const int segW = (W + kWgPx - 1) / kWgPx;
+  const int segW = (W + PX - 1) / PX;
   const int64_t segs = (int64_t)N * H * segW;
   const int64_t s0 = (int64_t)split * segs_per_split;
   const int64_t s1 = s0 + segs_per_split < segs ? s0 + segs_per_split : segs;
   const unsigned HW = (unsigned)(H * W);
-  const int c = tid >> 2, q = tid & 3;
+  const int c = tid / QN, q = tid % QN;
   const bool co_ok = co0 + c < Cout, ci_ok = ci0 + c < Cin;
 
   floatx16 acc[9];
@@ -308,7 +316,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(
     const int xs = (int)(sgc % segW);
     const int64_t ry_ = sgc / segW;
     const int y = (int)(ry_ % H), n = (int)(ry_ / H);
-    const int x0 = xs * kWgPx;
+    const int x0 = xs * PX;
     const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(dy + (int64_t)n * Cout * HW), (short)0, (int)(Cout * HW * 4u), 0x00020000);
     const __amdgpu_buffer_rsrc_t rxx = __builtin_amdgcn_make_buffer_rsrc(
@@ -355,10 +363,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(
           }
         }
       }
-      // halo: column x0 - 1 (q == 0) or x0 + 64 (q == 3)
-      int hx = q == 0 ? x0 - 1 : x0 + kWgPx;
+      // halo: column x0 - 1 (q == 0) or x0 + PX (q == QN - 1)
+      int hx = q == 0 ? x0 - 1 : x0 + PX;
       if (reflect && hx <= W) hx = reflect1(hx, W);
-      const bool hok = rok && (q == 0 || q == 3) && hx >= 0 && hx < W;
+      const bool hok = rok && (q == 0 || q == QN - 1) && hx >= 0 && hx < W;
       rh[row] = __uint_as_float(
           __builtin_amdgcn_raw_buffer_load_b32(rxx, (int)(hok ? rbase + 4u * hx : kWgOOB), 0, 0));
     }
@@ -368,53 +376,57 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Ys[(q * 16 + 4 * k + e) * kWgLd + c] = __uint_as_float(ry[k][e]);
+      for (int e = 0; e < 4; ++e) Ys[(q * 16 + 4 * k + e) * LD + c] = __uint_as_float(ry[k][e]);
 #pragma unroll
     for (int row = 0; row < 3; ++row) {
 #pragma unroll
       for (int k = 0; k < 4; ++k)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          Xs[(row * kWgCols + 1 + q * 16 + 4 * k + e) * kWgLd + c] = __uint_as_float(rx[row][k][e]);
-      if (q == 0) Xs[(row * kWgCols) * kWgLd + c] = rh[row];
-      if (q == 3) Xs[(row * kWgCols + kWgCols - 1) * kWgLd + c] = rh[row];
+          Xs[(row * COLS + 1 + q * 16 + 4 * k + e) * LD + c] = __uint_as_float(rx[row][k][e]);
+      if (q == 0) Xs[(row * COLS) * LD + c] = rh[row];
+      if (q == QN - 1) Xs[(row * COLS + COLS - 1) * LD + c] = rh[row];
     }
   };
 
+  // pixel pairs of this wave: all PX / 2 (TC 64) or its quarter of them (TC 32)
+  constexpr int KK = PX / 2 / KSPL;
+  const int kk0 = KSPL > 1 ? wave * KK : 0;
   load(s0);
   for (int64_t sg = s0; sg < s1; ++sg) {
     store();
     __syncthreads();
     load(sg + 1);  // in flight during this segment's MFMAs
-    if (bias_tile && wave == 0) {
+    if (bias_tile && wave == 0 && lane < TC) {
       float t = 0.f;
-      for (int px = 0; px < kWgPx; ++px) t += Ys[px * kWgLd + lane];
+      for (int px = 0; px < PX; ++px) t += Ys[px * LD + lane];
       bacc += t;
     }
 #pragma unroll 4
-    for (int kk = 0; kk < kWgPx / 2; ++kk) {
+    for (int kk = kk0; kk < kk0 + KK; ++kk) {
       const int px = 2 * kk + h;
-      const float av = Ys[px * kWgLd + wm * 32 + j];
+      const float av = Ys[px * LD + wm * 32 + j];
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int dyy = t / 3, dxx = t % 3;
-        const float bv = Xs[(dyy * kWgCols + px + dxx) * kWgLd + wn * 32 + j];
+        const float bv = Xs[(dyy * COLS + px + dxx) * LD + wn * 32 + j];
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
       }
     }
     __syncthreads();
   }
-  if (bias_tile && wave == 0 && co0 + lane < Cout)
+  if (bias_tile && wave == 0 && lane < TC && co0 + lane < Cout)
     bpart[(int64_t)split * Cout + co0 + lane] = bacc;
-  // partial[split][co][ci][9]; accumulator element r of lane: row (co) = (r&3) + 8(r>>2) +
-  // 4h, column (ci) = j
+  // partial[split * KSPL + wave part][co][ci][9]; accumulator element r of lane: row (co) =
+  // (r&3) + 8(r>>2) + 4h, column (ci) = j
   const int ci = ci0 + wn * 32 + j;
-  if (ci >= Cin) return;
+  if (ci >= Cin || (KSPL == 1 && wn * 32 + j >= TC)) return;
+  const int64_t ps = (int64_t)split * KSPL + (KSPL > 1 ? wave : 0);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
     if (co >= Cout) continue;
-    float* o = part + (((int64_t)split * Cout + co) * Cin + ci) * 9;
+    float* o = part + ((ps * Cout + co) * Cin + ci) * 9;
 #pragma unroll
     for (int t = 0; t < 9; ++t) o[t] = acc[t][r];
   }
@@ -611,10 +623,21 @@ extern "C" int rpst_reflect_pad_border_grad(const float* dy, const float* w, flo
   return launch_status("reflect_fold_kernel");
 }
 
+// channel tile of the wgrad kernel: 32 when both channel counts fit one (no padded waves)
+static int wgrad_tc(int Cin, int Cout) {
+  static const int force = [] {
+    const char* e = std::getenv("RPST_WGRAD_TC");  // A/B switch: 64 forces the wide tiles
+    return e ? std::atoi(e) : 0;
+  }();
+  if (force == 64) return 64;
+  return (Cin <= 32 && Cout <= 32) ? 32 : 64;
+}
+
 static void wgrad_geometry(int N, int Cin, int H, int W, int Cout, int* splits,
                            int64_t* segs_per_split) {
-  const int tiles = ((Cout + kWgTile - 1) / kWgTile) * ((Cin + kWgTile - 1) / kWgTile);
-  const int64_t segs = (int64_t)N * H * ((W + kWgPx - 1) / kWgPx);
+  const int tc = wgrad_tc(Cin, Cout), px = 4096 / tc;
+  const int tiles = ((Cout + tc - 1) / tc) * ((Cin + tc - 1) / tc);
+  const int64_t segs = (int64_t)N * H * ((W + px - 1) / px);
   // ~1024 workgroups in all, at least 4 segments each
   int64_t s = (1024 + tiles - 1) / tiles;
   if (s > segs / 4) s = segs / 4;
@@ -628,7 +651,8 @@ extern "C" size_t rpst_conv_wgrad_workspace_size(int N, int Cin, int H, int W, i
   int splits;
   int64_t sps;
   wgrad_geometry(N, Cin, H, W, Cout, &splits, &sps);
-  return sizeof(float) * (size_t)splits * Cout * ((size_t)Cin * 9 + 1);
+  const size_t kspl = wgrad_tc(Cin, Cout) == 32 ? 4 : 1;
+  return sizeof(float) * (size_t)splits * Cout * (kspl * Cin * 9 + 1);
 }
 
 extern "C" int rpst_conv_wgrad_pad(const float* x, const float* dy, float* dw, float* db,
@@ -649,21 +673,26 @@ extern "C" int rpst_conv_wgrad_pad(const float* x, const float* dy, float* dw, f
   int splits;
   int64_t sps;
   wgrad_geometry(N, Cin, H, W, Cout, &splits, &sps);
-  const int tiles = ((Cout + kWgTile - 1) / kWgTile) * ((Cin + kWgTile - 1) / kWgTile);
+  const int tc = wgrad_tc(Cin, Cout), kspl = tc == 32 ? 4 : 1;
+  const int tiles = ((Cout + tc - 1) / tc) * ((Cin + tc - 1) / tc);
+  RPST_REQUIRE(tiles <= 65535 * 64 && splits <= 65535, "conv_wgrad: grid too large");
   float* part = static_cast<float*>(workspace);
-  float* bpart = part + (size_t)splits * Cout * Cin * 9;
+  float* bpart = part + (size_t)splits * kspl * Cout * Cin * 9;
   RPST_REQUIRE((int64_t)(Cout > Cin ? Cout : Cin) * H * W * 4 < (1LL << 31),
                "conv_wgrad: one image's tensor exceeds 2 GiB");
   const bool vec = (W % 4) == 0;
-  if (vec)
-    conv_wgrad_kernel<true><<<dim3(tiles, splits), 256, 0, st>>>(
-        x, dy, part, db ? bpart : nullptr, N, Cin, H, W, Cout, sps, reflect);
-  else
-    conv_wgrad_kernel<false><<<dim3(tiles, splits), 256, 0, st>>>(
-        x, dy, part, db ? bpart : nullptr, N, Cin, H, W, Cout, sps, reflect);
+  const dim3 grid(tiles, splits);
+  float* bp = db ? bpart : nullptr;
+  if (tc == 32) {
+    if (vec) conv_wgrad_kernel<true, 32><<<grid, 256, 0, st>>>(x, dy, part, bp, N, Cin, H, W, Cout, sps, reflect);
+    else conv_wgrad_kernel<false, 32><<<grid, 256, 0, st>>>(x, dy, part, bp, N, Cin, H, W, Cout, sps, reflect);
+  } else {
+    if (vec) conv_wgrad_kernel<true, 64><<<grid, 256, 0, st>>>(x, dy, part, bp, N, Cin, H, W, Cout, sps, reflect);
+    else conv_wgrad_kernel<false, 64><<<grid, 256, 0, st>>>(x, dy, part, bp, N, Cin, H, W, Cout, sps, reflect);
+  }
   if (int e = launch_status("conv_wgrad_kernel")) return e;
   const int64_t n = (int64_t)Cout * Cin * 9;
-  wgrad_reduce_kernel<<<blocks_for(n), 256, 0, st>>>(part, dw, n, splits);
+  wgrad_reduce_kernel<<<blocks_for(n), 256, 0, st>>>(part, dw, n, splits * kspl);
   if (int e = launch_status("wgrad_reduce_kernel")) return e;
   if (db) {
     wgrad_reduce_kernel<<<blocks_for(Cout), 256, 0, st>>>(bpart, db, Cout, splits);

@@ -88,11 +88,14 @@ static size_t wino_image_floats(int MT, int Cout, int Cin) {
 constexpr int kWMT = 1;
 int wino_bm() { return 32 * kWMT; }
 int wino_th() { return 4 * (2 / kWMT); }
-int wino_persist(int in_op) {
+// spatial_blocks = tiles_x * tiles_y * N: a persistent grid of fewer than 512 blocks (two
+// per CU) leaves CUs idle (the 64x64 relu4_1 / relu5_1 layers of SAModel training at B = 8:
+// 128 blocks), so such layers take one co tile per block
+int wino_persist(int in_op, int64_t spatial_blocks) {
   const char* e = getenv("RPST_WINO_PERSIST");  // A/B switch for the one-load loaders
   if (in_op == RPST_IN_MAXPOOL2 || in_op == RPST_IN_ADD_UPSAMPLE2 || in_op == RPST_IN_ADD_ADAIN)
     return 0;
-  return (e && *e) ? atoi(e) != 0 : 1;
+  return (e && *e) ? atoi(e) != 0 : spatial_blocks >= 512;
 }
 
 size_t wino_packed_floats(int Cout, int Cin) { return wino_image_floats(kWMT, Cout, Cin); }
@@ -466,7 +469,7 @@ int wino_launch(ConvArgs& a, int in_op, hipStream_t st) {
   a.tiles_y = (a.H + TH - 1) / TH;
   a.co_tiles = a.Cout_pad / BM;
   a.stat_P = a.tiles_x * a.tiles_y;
-  a.persist = wino_persist(in_op);
+  a.persist = wino_persist(in_op, (int64_t)a.tiles_x * a.tiles_y * a.N);
   const int64_t blocks = (int64_t)a.tiles_x * a.tiles_y * a.N * (a.persist ? 1 : a.co_tiles);
   RPST_REQUIRE(blocks <= 0x7fffffffLL, "conv2d: grid too large");
   const unsigned nb = (unsigned)blocks;

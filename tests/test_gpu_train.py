@@ -47,8 +47,11 @@ def test_conv_dgrad(cuda, pad, shape):
 
 
 @pytest.mark.parametrize("shape", [(2, 16, 12, 20, 32), (1, 3, 9, 7, 16), (2, 64, 33, 70, 40),
-                                   (1, 128, 16, 130, 256)])
+                                   (1, 128, 16, 130, 256), (2, 32, 6, 260, 32), (1, 3, 4, 200, 32),
+                                   (1, 33, 5, 64, 16)])
 def test_conv_wgrad(cuda, shape):
+    """3x3 weight / bias gradient vs float64 autograd: 64-channel tiles, and 32-channel tiles
+    with the per-wave pixel split (Cin, Cout <= 32; 128-column segments, ragged widths)."""
     from rpst import autograd as A
     n, cin, h, w, cout = shape
     conv = torch.nn.Conv2d(cin, cout, 3, padding=1).to(cuda)
@@ -63,7 +66,8 @@ def test_conv_wgrad(cuda, shape):
 
 
 @pytest.mark.parametrize("shape", [(2, 16, 12, 20, 32), (1, 3, 9, 7, 16), (2, 64, 33, 70, 40),
-                                   (1, 8, 2, 2, 8), (1, 32, 16, 64, 24), (1, 16, 5, 132, 16)])
+                                   (1, 8, 2, 2, 8), (1, 32, 16, 64, 24), (1, 16, 5, 132, 16),
+                                   (1, 32, 5, 129, 3), (2, 32, 3, 256, 32)])
 def test_conv_wgrad_reflect(cuda, shape):
     """ReflectionPad2d(1) + conv3x3 weight / bias gradient (rpst_conv_wgrad_pad, reflection in
     the loader): against float64 autograd, and equal to the zero-pad wgrad of the
