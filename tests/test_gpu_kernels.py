@@ -305,11 +305,14 @@ def test_adain_rp_vs_oracle_hidden16(cuda):
 
 
 def test_grad_enabled_raises(cuda):
-    """Models without backward kernels raise under autograd instead of running ATen
-    (AdaINRPNet, WCTRPNet and SAModel train through rpst.autograd: tests/test_gpu_train.py)."""
+    """Models without backward kernels (the AdaptiveSAModel family) raise under autograd
+    instead of running ATen (AdaINRPNet, WCTRPNet, SAModel, MultiScaleAdaINRPNet and
+    SourceNet train through rpst.autograd: tests/test_gpu_train.py)."""
     import network as net
-    m = net.SourceNet({}, copy.deepcopy(net.vgg)).to(cuda)
-    x = torch.rand(1, 3, 32, 32, device=cuda)
+    cfg = {"ada_module": "relu", "content_weight": 1.0, "style_weight": 3.0,
+           "l_identity1_weight": 50.0, "l_identity2_weight": 1.0}
+    m = net.AdaptiveSAModel(cfg, copy.deepcopy(net.vgg), 0, 64).to(cuda)
+    x = torch.rand(1, 3, 64, 64, device=cuda)
     with pytest.raises(NotImplementedError):
         m(x, x)
 

@@ -407,7 +407,7 @@ def test_samodel_training_deterministic_and_descends(cuda):
         _, total = m(c, s)
         total.backward()
         opt.step()
-        totals.append(float(total))
+        totals.append(float(total.detach()))
     assert totals[-1] < totals[0], totals
 
 
