@@ -127,9 +127,18 @@ __device__ __forceinline__ void g_load(float (&reg)[16], const float* __restrict
   }
 }
 
+// LDS row stride of a staged operand: RK tiles are written transposed (4 k of one row per
+// thread), so their stride is odd (129: 2-way bank conflicts on those scalar stores instead
+// of 4-way at 132); KR tiles keep 132 for their 16-B stores. (Measured: S = F^T G + O at
+// B = 32, C = 512, HW = 4096: 10.54 -> 10.33 ms, tools/bench_attn.py; a 64-deep k tile
+// (11.2 ms) and double-buffered LDS with the exp applied at the LDS store (11.2 ms) were
+// slower.)
+template <int LAY>
+constexpr int g_ld() { return LAY == LAY_RK ? 128 + 1 : 128 + kGPad; }
+
 template <int LAY>
 __device__ __forceinline__ void g_store(float* __restrict__ Xs, const float (&reg)[16], int tid) {
-  constexpr int LD = 128 + kGPad;
+  constexpr int LD = g_ld<LAY>();
   if (LAY == LAY_KR) {
     const int kk = tid >> 5, r4 = (tid & 31) * 4;
 #pragma unroll
@@ -147,9 +156,9 @@ __device__ __forceinline__ void g_store(float* __restrict__ Xs, const float (&re
 
 template <int ALAY, int BLAY, int BX, bool VECA, bool VECB>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
-  constexpr int LD = 128 + kGPad;
-  __shared__ float As[kGBK * LD];
-  __shared__ float Bs[kGBK * LD];
+  constexpr int LDA = g_ld<ALAY>(), LDB = g_ld<BLAY>();
+  __shared__ float As[kGBK * LDA];
+  __shared__ float Bs[kGBK * LDB];
   const int b = blockIdx.z;
   const int m0 = blockIdx.y * kGBM, n0 = blockIdx.x * kGBN;
   const float* A = g.A + b * g.sA;
@@ -186,9 +195,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     for (int kk = 0; kk < kGBK / 2; ++kk) {
       float av[2], bv[2];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) av[mt] = As[(2 * kk + h) * LD + wm * 64 + mt * 32 + j];
+      for (int mt = 0; mt < 2; ++mt) av[mt] = As[(2 * kk + h) * LDA + wm * 64 + mt * 32 + j];
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) bv[nt] = Bs[(2 * kk + h) * LD + wn * 64 + nt * 32 + j];
+      for (int nt = 0; nt < 2; ++nt) bv[nt] = Bs[(2 * kk + h) * LDB + wn * 64 + nt * 32 + j];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
