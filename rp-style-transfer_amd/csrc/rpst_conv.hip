@@ -398,7 +398,7 @@ template <int CO, int RPT>  // RPT output rows per thread: block = 4 RPT rows x 
 __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
   constexpr int CK = ConvK<3>::CK, kNrTH = 4 * RPT, kNrPS = (kNrTH + 2) * kNrPW;
   __shared__ float patch[kNrPS];
-  __shared__ float wl[kNrWl];  // Cin * 9 * CO <= 576 (narrow_shape)
+  __shared__ __attribute__((aligned(8))) float wl[kNrWl];  // Cin * 9 * CO <= 576 (narrow_shape)
   const int x0 = blockIdx.x * kNrTW, y0 = blockIdx.y * kNrTH, n = blockIdx.z;
   const int tid = threadIdx.x, col = tid & 63, rg = tid >> 6;  // output rows RPT rg ..
   // direct-packed weights [ci / CK][tap][ci % CK][Cout_pad] (zero beyond Cout)
@@ -406,37 +406,69 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
     const int co = i % CO, t = (i / CO) % 9, ci = i / (9 * CO);
     wl[i] = a.wpk[((int64_t)(ci / CK) * 9 + t) * CK * a.Cout_pad + (ci % CK) * a.Cout_pad + co];
   }
-  float acc[RPT][CO];
+  // accumulators in channel pairs: one v_pk_fma_f32 per two output channels
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 acc2[RPT][CO / 2];
 #pragma unroll
   for (int r = 0; r < RPT; ++r)
 #pragma unroll
-    for (int co = 0; co < CO; ++co) acc[r][co] = 0.f;
+    for (int c2 = 0; c2 < CO / 2; ++c2) acc2[r][c2] = f2{0.f, 0.f};
   const int64_t plane = (int64_t)a.H * a.W;
   const float* in = a.in + (int64_t)n * a.Cin * plane;
+  // this thread's patch elements (slot s: element tid + 256 s), their in-plane offsets
+  // resolved against the padding once (-1: zero padding / outside the patch); channel ci + 1
+  // is loaded into registers while channel ci is computed (the load latency hides under
+  // the FMAs instead of stalling every channel)
+  constexpr int kSl = (kNrPS + 255) / 256;
+  int off[kSl];
+#pragma unroll
+  for (int sl = 0; sl < kSl; ++sl) {
+    const int i = tid + 256 * sl;
+    const int r = i / kNrPW, c = i - r * kNrPW;
+    int y = y0 - 1 + r, x = x0 - 1 + c;
+    const bool oky = resolve(y, a.H, a.pad, true), okx = resolve(x, a.W, a.pad, true);
+    off[sl] = (i < kNrPS && oky && okx) ? y * a.W + x : -1;
+  }
+  float pre[kSl];
+  auto fetch = [&](int ci) {
+    const float* src = in + (int64_t)ci * plane;
+#pragma unroll
+    for (int sl = 0; sl < kSl; ++sl) pre[sl] = off[sl] >= 0 ? src[off[sl]] : 0.f;
+  };
+  fetch(0);
   for (int ci = 0; ci < a.Cin; ++ci) {
     __syncthreads();  // the previous channel's patch is consumed (first pass: weights)
-    for (int i = tid; i < kNrPS; i += 256) {
-      const int r = i / kNrPW, c = i - r * kNrPW;
-      int y = y0 - 1 + r, x = x0 - 1 + c;
-      const bool oky = resolve(y, a.H, a.pad, true), okx = resolve(x, a.W, a.pad, true);
-      patch[i] = oky && okx ? in[ci * plane + (int64_t)y * a.W + x] : 0.f;
-    }
+#pragma unroll
+    for (int sl = 0; sl < kSl; ++sl)
+      if (tid + 256 * sl < kNrPS) patch[tid + 256 * sl] = pre[sl];
     __syncthreads();
+    if (ci + 1 < a.Cin) fetch(ci + 1);
     float win[RPT + 2][3];
 #pragma unroll
     for (int r = 0; r < RPT + 2; ++r)
 #pragma unroll
       for (int c = 0; c < 3; ++c) win[r][c] = patch[(RPT * rg + r) * kNrPW + col + c];
-    const float* w = wl + ci * 9 * CO;
+    const f2* w = reinterpret_cast<const f2*>(wl + ci * 9 * CO);
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
-      for (int co = 0; co < CO; ++co) {
-        const float wv = w[t * CO + co];
+      for (int c2 = 0; c2 < CO / 2; ++c2) {
+        const f2 wv = w[t * (CO / 2) + c2];
 #pragma unroll
-        for (int r = 0; r < RPT; ++r) acc[r][co] = fmaf(win[t / 3 + r][t % 3], wv, acc[r][co]);
+        for (int r = 0; r < RPT; ++r) {
+          const float xv = win[t / 3 + r][t % 3];
+          acc2[r][c2] = __builtin_elementwise_fma(f2{xv, xv}, wv, acc2[r][c2]);
+        }
       }
   }
+  float acc[RPT][CO];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r)
+#pragma unroll
+    for (int c2 = 0; c2 < CO / 2; ++c2) {
+      acc[r][2 * c2] = acc2[r][c2].x;
+      acc[r][2 * c2 + 1] = acc2[r][c2].y;
+    }
   const int x = x0 + col;
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
