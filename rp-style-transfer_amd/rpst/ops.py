@@ -9,6 +9,8 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import os
+
 import torch
 
 from . import _lib
@@ -190,7 +192,9 @@ class precise_convs:
     include/rpst.h) — used by the training step, whose gradients pass ~30 convolutions."""
 
     def __enter__(self):
-        self._old = _lib.load().rpst_conv2d_set_precise(1)
+        # RPST_TRAIN_PRECISE=0: leave F(4x4) on (A/B of the gradient accuracy)
+        on = os.environ.get("RPST_TRAIN_PRECISE", "1") != "0"
+        self._old = _lib.load().rpst_conv2d_set_precise(int(on))
         return self
 
     def __exit__(self, *exc):

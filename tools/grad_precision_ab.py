@@ -1,0 +1,38 @@
+"""Gradient accuracy of the training steps against the reference goldens with and without
+precise mode (F(2x2) instead of F(4x4) in training): RPST_TRAIN_PRECISE=0 python
+tools/grad_precision_ab.py prints the worst per-tensor error per golden case."""
+import copy, os, sys, json
+sys.path.insert(0, "tests"); sys.path.insert(0, "rp-style-transfer_amd"); sys.path.insert(0, ".")
+import numpy as np, torch
+import network as net
+from helpers import rp_config, synth_, rel_l2, ms_grads_config, src_grads_config, grad_probe, probe_err
+cuda = torch.device("cuda:0")
+def load(n): return np.load(f"tests/golden/{n}.npz")
+out = {}
+g = load("grads")
+for i in range(int(g["n"])):
+    cfg = dict(rp_config(int(g[f"hidden{i}"])), content_weight=float(g[f"cw{i}"]), style_weight=float(g[f"sw{i}"]))
+    m = net.AdaINRPNet(cfg, copy.deepcopy(net.vgg)); synth_(m, int(g[f"seed{i}"])); m = m.to(cuda)
+    m.zero_grad(); _, t = m(torch.from_numpy(g[f"content{i}"]).to(cuda), torch.from_numpy(g[f"style{i}"]).to(cuda)); t.backward()
+    nm = dict(m.named_parameters())
+    out[f"adain{i}"] = max(rel_l2(nm[str(k)].grad, g[f"grad{i}:{k}"]) for k in g[f"names{i}"])
+g = load("grads_ms")
+for i in range(int(g["n"])):
+    m = net.MultiScaleAdaINRPNet(ms_grads_config(g, i), copy.deepcopy(net.vgg)); synth_(m, int(g[f"seed{i}"])); m = m.to(cuda)
+    m.zero_grad(); _, t = m(torch.from_numpy(g[f"content{i}"]).to(cuda), torch.from_numpy(g[f"style{i}"]).to(cuda)); t.backward()
+    nm = dict(m.named_parameters())
+    out[f"ms{i}"] = max(rel_l2(nm[str(k)].grad, g[f"grad{i}:{k}"]) for k in g[f"names{i}"])
+g = load("grads_src")
+for i in range(int(g["n"])):
+    m = net.SourceNet(src_grads_config(g, i), copy.deepcopy(net.vgg)); m.decoder = copy.deepcopy(m.decoder); synth_(m, int(g[f"seed{i}"])); m = m.to(cuda)
+    m.zero_grad(); _, t = m(torch.from_numpy(g[f"content{i}"]).to(cuda), torch.from_numpy(g[f"style{i}"]).to(cuda)); t.backward()
+    nm = dict(m.named_parameters())
+    out[f"src{i}"] = max(probe_err(grad_probe(str(k), nm[str(k)].grad), g[f"gprobe{i}:{k}"], nm[str(k)].grad.numel()) for k in g[f"names{i}"])
+g = load("grads_wct")
+for i in range(int(g["n"])):
+    cfg = dict(rp_config(int(g[f"hidden{i}"])), content_weight=float(g[f"cw{i}"]), style_weight=float(g[f"sw{i}"]))
+    m = net.WCTRPNet(cfg, copy.deepcopy(net.vgg)); synth_(m, int(g[f"seed{i}"])); m = m.to(cuda)
+    m.zero_grad(); _, t = m(torch.from_numpy(g[f"content{i}"]).to(cuda), torch.from_numpy(g[f"style{i}"]).to(cuda)); t.backward()
+    nm = dict(m.named_parameters())
+    out[f"wct{i}"] = max(rel_l2(nm[str(k)].grad, g[f"grad{i}:{k}"]) for k in g[f"names{i}"])
+print(os.environ.get("RPST_TRAIN_PRECISE", "1"), json.dumps({k: float("%.3g" % v) for k, v in out.items()}))
