@@ -52,6 +52,9 @@ constexpr int kW4CK = 8;                   // input channels per chunk
 #ifndef RPST_W4_HP
 #define RPST_W4_HP 2
 #endif
+#ifndef RPST_W4_ORDER  // spatial block order (w4_tile)
+#define RPST_W4_ORDER 0
+#endif
 constexpr int kW4BM = 32;                  // output channels per co tile
 constexpr int kW4TH = 16, kW4TW = 64;      // output rows x columns per block
 constexpr int kW4PH = kW4TH + 2;           // patch rows
@@ -228,6 +231,33 @@ __device__ __forceinline__ bool resolve_bf(int& v, int n, bool zero_pad) {
   return in || !zero_pad;
 }
 
+// spatial tile of logical block b (after the co-split digit): order 0 = column tile fastest,
+// then row tile, then image; 1 = image fastest, then column, row; 2 = column, image, row
+// (RPST_W4_ORDER at build time: which tiles the resident blocks share). tools/ab_variants.sh,
+// two rounds (ms, order 0 / 1 / 2): 128->256 N64 28.46 / 28.86 / 28.37, 64->128 8.00 /
+// 8.47 / 7.83, 256->128 N32 13.81 / 14.17 / 13.76, 32->64 2.54 / 2.69 / 2.57; in bench.py
+// (with the statistics epilogue) order 2 measured 29.30 ms for 128->256 vs 29.09 for order 0
+// and the same AdaIN-RP rate within noise (521.5 vs 520.2 img/s): order 0 stays.
+__device__ __forceinline__ void w4_tile(int b, int order, int tiles_x, int tiles_y, int N,
+                                        int& tx, int& ty, int& n) {
+  if (order == 1) {
+    n = b % N;
+    b /= N;
+    tx = b % tiles_x;
+    ty = b / tiles_x;
+  } else if (order == 2) {
+    tx = b % tiles_x;
+    b /= tiles_x;
+    n = b % N;
+    ty = b / N;
+  } else {
+    tx = b % tiles_x;
+    b /= tiles_x;
+    ty = b % tiles_y;
+    n = b / tiles_y;
+  }
+}
+
 // STATS: the calc_mean_std partials epilogue (a.stat_part); BTAB: the folded per-(n, co)
 // border-class bias table (a.btab). Both are template arguments so a plain layer's
 // epilogue carries none of their VALU; the two transformed-row halves (ph, waves 0-3 and
@@ -261,10 +291,8 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   bid /= a.cosplit;
   const int nct = a.co_tiles / a.cosplit;
   const int ct0 = cog * nct;
-  const int tx = bid % a.tiles_x;
-  bid /= a.tiles_x;
-  const int ty = bid % a.tiles_y;
-  const int n = bid / a.tiles_y;
+  int tx, ty, n;
+  w4_tile(bid, RPST_W4_ORDER, a.tiles_x, a.tiles_y, a.N, tx, ty, n);
   const int nch = a.nchunks, K4 = 2 * nch, G = nct * K4;  // K steps per co tile / in total
   const int y0 = ty * kW4TH, x0 = tx * kW4TW;
 
@@ -553,11 +581,9 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     e.H = L->H;
     e.Cout = L->Cout;
     e.slope = L->relu == RPST_ACT_RELU ? 0.f : (L->relu == RPST_ACT_LRELU ? 0.2f : 1.f);
-    int b = xcd_swizzle(blockIdx.x, (int)gridDim.x) / L->cosplit;
-    const int btx = b % L->tiles_x;
-    b /= L->tiles_x;
-    const int bty = b % L->tiles_y;
-    e.n = b / L->tiles_y;
+    int btx, bty;
+    w4_tile(xcd_swizzle(blockIdx.x, (int)gridDim.x) / L->cosplit, RPST_W4_ORDER,
+            L->tiles_x, L->tiles_y, L->N, btx, bty, e.n);
     const int bx0 = btx * kW4TW;
     e.gy0 = bty * kW4TH + 4 * wr;
     e.gx0 = bx0 + 4 * tn;
