@@ -377,8 +377,10 @@ static int pad_cout(int Cout) {
 static int ck_of(int ksize) { return ksize == 3 ? ConvK<3>::CK : ConvK<1>::CK; }
 
 // ---- narrow 3x3 layers on the VALU ------------------------------------------------------
-// Cout <= 4 with Cin <= 16, or Cout <= 16 with Cin <= 4 (narrow_shape; the RP stacks'
-// 3->16 input and 16->3 output convs, base.py:363-396 encoder / decoder ends): an MFMA tile
+// Cout <= 4 with Cin <= 32, or Cout <= 16 with Cin <= 4 (narrow_shape; the RP stacks'
+// 3->16 input and 16->3 output convs, base.py:363-396 encoder / decoder ends, and the
+// MultiScale decoder's last block 32->3, whose loader forms stylized + AdaIN(c) per element:
+// INOP = RPST_IN_ADD_ADAIN, adain_rp.py:301): an MFMA tile
 // pads such a layer to 32 output channels (16->3: 10x the work) or 8 input channels, so
 // these run as plain FMAs instead (algorithm RPST_CONV_NARROW). Block = 4 RPT rows x 64
 // columns, 256 threads (column, RPT rows); per input channel the (4 RPT+2) x 66 patch is
@@ -386,7 +388,7 @@ static int ck_of(int ksize) { return ksize == 3 ? ConvK<3>::CK : ConvK<1>::CK; }
 // whole block. Same epilogue as the direct kernel: bias, activation, residual. Images go
 // on grid.z: batches above 65535 images (or 65535 row tiles) take the MFMA direct path.
 constexpr int kNrTW = 64, kNrPW = kNrTW + 2;
-constexpr int kNrMaxCin = 16, kNrMaxCo = 16, kNrWl = 64 * 9;  // weight floats in LDS
+constexpr int kNrMaxCin = 32, kNrMaxCo = 16, kNrWl = 128 * 9;  // weight floats in LDS
 
 static bool narrow_shape(int Cin, int Cout) {
   return (Cout <= 4 && Cin <= kNrMaxCin) || (Cout <= kNrMaxCo && Cin <= 4);
@@ -394,11 +396,13 @@ static bool narrow_shape(int Cin, int Cout) {
 // the largest Cin * CO an instantiation can meet must fit the LDS weight array
 static_assert(kNrMaxCin * 9 * 4 <= kNrWl && 4 * 9 * kNrMaxCo <= kNrWl, "narrow weights fit LDS");
 
-template <int CO, int RPT>  // RPT output rows per thread: block = 4 RPT rows x 64 columns
+template <int CO, int RPT, int INOP = RPST_IN_NONE>  // block = 4 RPT rows x 64 columns
 __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
+  static_assert(INOP == RPST_IN_NONE || INOP == RPST_IN_ADD_ADAIN, "narrow loaders");
+  constexpr bool kSkip = INOP == RPST_IN_ADD_ADAIN;
   constexpr int CK = ConvK<3>::CK, kNrTH = 4 * RPT, kNrPS = (kNrTH + 2) * kNrPW;
   __shared__ float patch[kNrPS];
-  __shared__ __attribute__((aligned(8))) float wl[kNrWl];  // Cin * 9 * CO <= 576 (narrow_shape)
+  __shared__ __attribute__((aligned(8))) float wl[kNrWl];  // Cin * 9 * CO <= 1152 (narrow_shape)
   const int x0 = blockIdx.x * kNrTW, y0 = blockIdx.y * kNrTH, n = blockIdx.z;
   const int tid = threadIdx.x, col = tid & 63, rg = tid >> 6;  // output rows RPT rg ..
   // direct-packed weights [ci / CK][tap][ci % CK][Cout_pad] (zero beyond Cout)
@@ -429,18 +433,34 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
     const bool oky = resolve(y, a.H, a.pad, true), okx = resolve(x, a.W, a.pad, true);
     off[sl] = (i < kNrPS && oky && okx) ? y * a.W + x : -1;
   }
-  float pre[kSl];
+  // ADD_ADAIN: the skip feature c (aux2) of the same shape; the element is
+  // stylized + ((c - mean_c) / std_c) * std_s + mean_s (0 at zero padding)
+  const float* cin = kSkip ? a.aux2 + (int64_t)n * a.Cin * plane : nullptr;
+  float pre[kSl], prc[kSkip ? kSl : 1];
   auto fetch = [&](int ci) {
     const float* src = in + (int64_t)ci * plane;
 #pragma unroll
     for (int sl = 0; sl < kSl; ++sl) pre[sl] = off[sl] >= 0 ? src[off[sl]] : 0.f;
+    if constexpr (kSkip) {
+      const float* cs = cin + (int64_t)ci * plane;
+#pragma unroll
+      for (int sl = 0; sl < kSl; ++sl) prc[sl] = off[sl] >= 0 ? cs[off[sl]] : 0.f;
+    }
   };
   fetch(0);
   for (int ci = 0; ci < a.Cin; ++ci) {
     __syncthreads();  // the previous channel's patch is consumed (first pass: weights)
+    if constexpr (kSkip) {
+      const AdainP pa = adain_params(a.aux, n, ci, a);
 #pragma unroll
-    for (int sl = 0; sl < kSl; ++sl)
-      if (tid + 256 * sl < kNrPS) patch[tid + 256 * sl] = pre[sl];
+      for (int sl = 0; sl < kSl; ++sl)
+        if (tid + 256 * sl < kNrPS)
+          patch[tid + 256 * sl] = off[sl] >= 0 ? pre[sl] + fmaf(prc[sl] - pa.mc, pa.scale, pa.ms) : 0.f;
+    } else {
+#pragma unroll
+      for (int sl = 0; sl < kSl; ++sl)
+        if (tid + 256 * sl < kNrPS) patch[tid + 256 * sl] = pre[sl];
+    }
     __syncthreads();
     if (ci + 1 < a.Cin) fetch(ci + 1);
     float win[RPT + 2][3];
@@ -592,7 +612,8 @@ static thread_local int t_conv_precise = 0;
 static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
   if (ksize != 3) return RPST_CONV_DIRECT;
   const bool w4 = wino4_supports(in_op) && wino4_fits(1, Cin, Hs, Ws, in_op);
-  const bool nr = in_op == RPST_IN_NONE && narrow_shape(Cin, Cout) && narrow_enabled();
+  const bool nr = (in_op == RPST_IN_NONE || (in_op == RPST_IN_ADD_ADAIN && Cout <= 4)) &&
+                  narrow_shape(Cin, Cout) && narrow_enabled();
   const char* e = getenv("RPST_CONV_ALGO");
   if (e && *e) {
     if (e[0] == 'd') return nr ? RPST_CONV_NARROW : RPST_CONV_DIRECT;
@@ -865,7 +886,11 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
     const int rpt = narrow_rpt(Cout);
     RPST_REQUIRE(Cin * 9 * (Cout <= 4 ? 4 : 16) <= kNrWl, "conv2d: narrow weights exceed LDS");
     dim3 grid((unsigned)((a.W + kNrTW - 1) / kNrTW), (unsigned)((a.H + 4 * rpt - 1) / (4 * rpt)), N);
-    if (Cout <= 4) {
+    if (in_op == RPST_IN_ADD_ADAIN) {
+      RPST_REQUIRE(Cout <= 4, "conv2d: narrow skip-AdaIN conv needs Cout <= 4");
+      if (rpt == 4) conv3x3_narrow_kernel<4, 4, RPST_IN_ADD_ADAIN><<<grid, 256, 0, st>>>(a);
+      else conv3x3_narrow_kernel<4, 2, RPST_IN_ADD_ADAIN><<<grid, 256, 0, st>>>(a);
+    } else if (Cout <= 4) {
       if (rpt == 4) conv3x3_narrow_kernel<4, 4><<<grid, 256, 0, st>>>(a);
       else conv3x3_narrow_kernel<4, 2><<<grid, 256, 0, st>>>(a);
     } else {

@@ -51,8 +51,11 @@ def test_conv2d_leaky_relu(cuda, conv_algo, shape):
     assert (out.cpu() < 0).any()  # the negative branch is exercised
 
 
-@pytest.mark.parametrize("shape", [(2, 32, 24, 40, 32), (1, 8, 9, 13, 3), (3, 16, 16, 16, 64)])
+@pytest.mark.parametrize("shape", [(2, 32, 24, 40, 32), (1, 8, 9, 13, 3), (3, 16, 16, 16, 64),
+                                   (2, 32, 20, 130, 3)])
 def test_conv2d_skip_adain(cuda, conv_algo, shape):
+    """stylized + AdaIN(c) formed in the conv's loader (MultiScale decoder blocks): MFMA
+    paths, and the narrow VALU kernel for Cout <= 4 (the 32->3 / 8->3 last blocks)."""
     from rpst import ops
     n, cin, h, w, cout = shape
     x = gen(80, (n, cin, h, w))
