@@ -496,7 +496,7 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
     if (y >= a.H || x >= a.W) continue;
 #pragma unroll
     for (int co = 0; co < CO; ++co) {
-      if (co >= a.Cout) break;
+      if (co >= a.Cout) continue;  // (not break: the loop stays fully unrolled)
       const int64_t o = ((int64_t)n * a.Cout + co) * plane + (int64_t)y * a.W + x;
       float v = activate(acc[r][co] + (a.bias ? a.bias[co] : 0.f), a.relu);
       if (a.res) v += a.res[o];
@@ -621,9 +621,10 @@ static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
     if (!strcmp(e, "winograd4")) return w4 ? RPST_CONV_WINOGRAD4 : RPST_CONV_WINOGRAD;
   }
   // measured (profiles/r01_bench_conv_wino4.log): F(4x4) wins every layer with >= 16 input
-  // channels it supports, the 16-wide 32->16 decoder layer included; the narrow 3->16 /
-  // 16->3 layers run on the VALU kernel (0.51 / 0.30 ms vs 0.57 / 0.64 on MFMA tiles) and
-  // the other 3-channel input layers (VGG 3->64) faster direct
+  // channels it supports, the 16-wide 32->16 decoder layer included; the narrow shapes
+  // (3->16 / 16->3 of the RP stacks, <= 4-channel outputs) run on the VALU kernel (3->16
+  // 0.44 / 16->3 0.16 ms vs 0.57 / 0.64 on MFMA tiles); the wider 3-channel first convs
+  // stay direct (VGG 3->64 1.63 ms vs 2.49 on the VALU kernel, MultiScale 3->32 1.22 vs 1.37)
   if (nr) return RPST_CONV_NARROW;
   if (Cin < 16) return RPST_CONV_DIRECT;
   if (w4 && !t_conv_precise) return RPST_CONV_WINOGRAD4;
@@ -884,7 +885,8 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   if (args_out) *args_out = a;
   if (algo == RPST_CONV_NARROW) {
     const int rpt = narrow_rpt(Cout);
-    RPST_REQUIRE(Cin * 9 * (Cout <= 4 ? 4 : 16) <= kNrWl, "conv2d: narrow weights exceed LDS");
+    const int nco = Cout <= 4 ? 4 : 16;
+    RPST_REQUIRE(Cin * 9 * nco <= kNrWl, "conv2d: narrow weights exceed LDS");
     dim3 grid((unsigned)((a.W + kNrTW - 1) / kNrTW), (unsigned)((a.H + 4 * rpt - 1) / (4 * rpt)), N);
     if (in_op == RPST_IN_ADD_ADAIN) {
       RPST_REQUIRE(Cout <= 4, "conv2d: narrow skip-AdaIN conv needs Cout <= 4");
