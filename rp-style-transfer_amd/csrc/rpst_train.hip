@@ -630,7 +630,9 @@ static int wgrad_tc(int Cin, int Cout) {
     return e ? std::atoi(e) : 0;
   }();
   if (force == 64) return 64;
-  return (Cin <= 32 && Cout <= 32) ? 32 : 64;
+  // both <= 32, or one side <= 8 (a 64-wide tile would run >= 7/8 of its rows or columns
+  // on padding: the decoders' 64->3 / 16->3 last convs)
+  return (Cin <= 32 && Cout <= 32) || Cin <= 8 || Cout <= 8 ? 32 : 64;
 }
 
 static void wgrad_geometry(int N, int Cin, int H, int W, int Cout, int* splits,

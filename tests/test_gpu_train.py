@@ -67,7 +67,7 @@ def test_conv_wgrad(cuda, shape):
 
 @pytest.mark.parametrize("shape", [(2, 16, 12, 20, 32), (1, 3, 9, 7, 16), (2, 64, 33, 70, 40),
                                    (1, 8, 2, 2, 8), (1, 32, 16, 64, 24), (1, 16, 5, 132, 16),
-                                   (1, 32, 5, 129, 3), (2, 32, 3, 256, 32)])
+                                   (1, 32, 5, 129, 3), (2, 32, 3, 256, 32), (1, 64, 6, 140, 3)])
 def test_conv_wgrad_reflect(cuda, shape):
     """ReflectionPad2d(1) + conv3x3 weight / bias gradient (rpst_conv_wgrad_pad, reflection in
     the loader): against float64 autograd, and equal to the zero-pad wgrad of the
