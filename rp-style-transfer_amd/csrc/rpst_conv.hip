@@ -624,8 +624,11 @@ static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
   // channels it supports, the 16-wide 32->16 decoder layer included; the narrow shapes
   // (3->16 / 16->3 of the RP stacks, <= 4-channel outputs) run on the VALU kernel (3->16
   // 0.44 / 16->3 0.16 ms vs 0.57 / 0.64 on MFMA tiles); the wider 3-channel first convs
-  // stay direct (VGG 3->64 1.63 ms vs 2.49 on the VALU kernel, MultiScale 3->32 1.22 vs 1.37)
+  // (VGG 3->64, MultiScale 3->32) run on F(4x4): 3->64 reflect at 512^2, N = 64: 1.25 ms vs
+  // 1.59 direct and 2.49 on the VALU kernel (tools/bench_conv.py); other inputs below 16
+  // channels, and precise mode, stay direct
   if (nr) return RPST_CONV_NARROW;
+  if (Cin <= 4 && w4 && !t_conv_precise) return RPST_CONV_WINOGRAD4;
   if (Cin < 16) return RPST_CONV_DIRECT;
   if (w4 && !t_conv_precise) return RPST_CONV_WINOGRAD4;
   if (w4) return RPST_CONV_WINOGRAD;  // precise mode, same shapes as F(4x4)

@@ -98,7 +98,8 @@ def test_conv_algorithm_choice_is_host_only(monkeypatch):
     assert lib.rpst_conv2d_algorithm(128, 256, 512, 512, 3, 4) == W4   # AdaIN-in-loader
     assert lib.rpst_conv2d_algorithm(256, 256, 32, 32, 3, 2) == W4     # upsample
     assert lib.rpst_conv2d_algorithm(128, 64, 64, 64, 3, 1) == W2      # max-pool loader
-    assert lib.rpst_conv2d_algorithm(64, 3, 512, 512, 3, 0) == D        # 3-channel input
+    assert lib.rpst_conv2d_algorithm(64, 3, 512, 512, 3, 0) == W4       # 3-channel input
+    assert lib.rpst_conv2d_algorithm(64, 8, 512, 512, 3, 0) == D        # 8-channel input
     assert lib.rpst_conv2d_algorithm(3, 32, 512, 512, 3, 5) == NR       # skip-AdaIN 32->3
     assert lib.rpst_conv2d_algorithm(3, 64, 512, 512, 3, 0) != NR       # Cin > 32
     assert lib.rpst_conv2d_algorithm(16, 3, 512, 512, 3, 0) == NR      # RP 3->16
@@ -110,7 +111,7 @@ def test_conv_algorithm_choice_is_host_only(monkeypatch):
     assert lib.rpst_conv2d_grid_threads(2, 3, 512, 512, 16, 3, 0) == 2 * 8 * 64 * 256
     monkeypatch.setenv("RPST_CONV_NARROW", "0")
     assert lib.rpst_conv2d_algorithm(3, 16, 512, 512, 3, 0) == W4
-    assert lib.rpst_conv2d_algorithm(16, 3, 512, 512, 3, 0) == D
+    assert lib.rpst_conv2d_algorithm(16, 3, 512, 512, 3, 0) == W4     # 3-channel input: F(4x4)
     monkeypatch.delenv("RPST_CONV_NARROW")
     assert lib.rpst_conv2d_algorithm(16, 32, 512, 512, 3, 0) == W4
     assert lib.rpst_conv2d_algorithm(512, 512, 64, 64, 1, 0) == D
