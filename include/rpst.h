@@ -171,6 +171,10 @@ int rpst_maxpool2x2_ceil(const float* in, float* out, int N, int C, int H, int W
                          rpst_stream_t stream);
 int rpst_upsample_nearest2x(const float* in, float* out, int N, int C, int H, int W,
                             rpst_stream_t stream);
+/* out (N,C,H,W) = a + upsample_nearest2x(b), b (N,C,H/2,W/2), H and W even: the merge
+ * conv's input of Transform.forward (sanet.py:140-149) when that conv runs on F(4x4). */
+int rpst_add_upsample_nearest2x(const float* a, const float* b, float* out, int N, int C, int H,
+                                int W, rpst_stream_t stream);
 
 /* ---- a11: SANet attention core  network/sanet.py:86-94 ------------------------------
  * O[b] = H[b] softmax_rows(F[b]^T G[b])^T  for F, G, H, O of shape (B, C, HW):

@@ -1104,6 +1104,30 @@ __global__ void upsample2_kernel(const float* __restrict__ in, float* __restrict
   out[i] = in[p * H * W + (int64_t)(y >> 1) * W + (x >> 1)];
 }
 
+// out = a + upsample_nearest2x(b): a (planes, H, W), b (planes, H/2, W/2) read at
+// (y >> 1, x >> 1), the RPST_IN_ADD_UPSAMPLE2 loader's operand, materialised
+__global__ void add_upsample2_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                     float* __restrict__ out, int64_t planes, int H, int W) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= planes * H * W) return;
+  const int x = (int)(i % W);
+  const int64_t r = i / W;
+  const int y = (int)(r % H);
+  const int64_t p = r / H;
+  const int Wb = W >> 1, Hb = H >> 1;
+  out[i] = a[i] + b[(p * Hb + (y >> 1)) * Wb + (x >> 1)];
+}
+
+extern "C" int rpst_add_upsample_nearest2x(const float* a, const float* b, float* out, int N,
+                                           int C, int H, int W, rpst_stream_t stream) {
+  RPST_REQUIRE(a && b && out && N > 0 && C > 0 && H >= 2 && W >= 2 && H % 2 == 0 && W % 2 == 0,
+               "add_upsample2x: bad args");
+  const int64_t total = (int64_t)N * C * H * W;
+  add_upsample2_kernel<<<(unsigned)((total + 255) / 256), 256, 0, as_stream(stream)>>>(
+      a, b, out, (int64_t)N * C, H, W);
+  return launch_status("add_upsample2_kernel");
+}
+
 extern "C" int rpst_maxpool2x2_ceil(const float* in, float* out, int N, int C, int H, int W,
                                     rpst_stream_t stream) {
   RPST_REQUIRE(in && out && N > 0 && C > 0 && H > 0 && W > 0, "maxpool2x2: bad args");

@@ -45,6 +45,7 @@ SIGNATURES = {
     "rpst_conv2d_skip_adain": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_maxpool2x2_ceil": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "rpst_upsample_nearest2x": (_I, [_P, _P, _I, _I, _I, _I, _P]),
+    "rpst_add_upsample_nearest2x": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
     "rpst_sanet_attention_workspace_size": (_SZ, [_I, _I]),
     "rpst_sanet_attention": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
     "rpst_conv_weight_flip": (_I, [_P, _P, _I, _I, _I, _P]),

@@ -172,6 +172,7 @@ def conv_out_hw(h: int, w: int, in_op: int) -> Tuple[int, int]:
     return h, w
 
 
+ALGO_DIRECT, ALGO_WINOGRAD, ALGO_WINOGRAD4, ALGO_NARROW = 0, 1, 2, 3  # rpst_conv2d_algorithm
 _ALGO_TAG = {0: "conv", 1: "wino", 2: "wino4", 3: "narrow"}
 
 
@@ -325,6 +326,23 @@ def upsample_nearest2x(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty((n, c, 2 * h, 2 * w), device=x.device, dtype=x.dtype)
     _lib.call("rpst_upsample_nearest2x", x.data_ptr(), out.data_ptr(), n, c, h, w, _stream(x))
     return out
+
+
+def add_upsample_nearest2x(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a + upsample_nearest2x(b) (the merge conv's input, sanet.py:147-149)."""
+    _check(a, b)
+    a, b = _c(a), _c(b)
+    n, c, h, w = a.shape
+    assert tuple(b.shape) == (n, c, h // 2, w // 2) and h % 2 == 0 and w % 2 == 0
+    out = torch.empty_like(a)
+    _lib.call("rpst_add_upsample_nearest2x", a.data_ptr(), b.data_ptr(), out.data_ptr(), n, c,
+              h, w, _stream(a))
+    return out
+
+
+def conv_algorithm(cout: int, cin: int, hs: int, ws: int, ksize: int, in_op: int) -> int:
+    """The library's algorithm choice for a conv (0 direct, 1 F(2x2), 2 F(4x4), 3 narrow)."""
+    return int(_lib.load().rpst_conv2d_algorithm(cout, cin, hs, ws, ksize, in_op))
 
 
 # Cap on the materialised attention matrix per launch; larger batches are chunked.

@@ -47,6 +47,27 @@ def test_transform_golden(cuda, golden):
     assert rel_l2(out, g["tr_out"]) < 1e-5
 
 
+def test_add_upsample_and_merge_conv_paths(cuda):
+    """a + upsample2(b) materialised (rpst_add_upsample_nearest2x, bit-exact vs torch) and the
+    merge conv on it (F(4x4), Transform.forward's path at even sizes) against the fused
+    two-operand loader (RPST_IN_ADD_UPSAMPLE2) and float64."""
+    from rpst import ops
+    a = gen(90, (2, 64, 12, 18)).to(cuda)
+    b = gen(91, (2, 64, 6, 9)).to(cuda)
+    z = ops.add_upsample_nearest2x(a, b)
+    assert torch.equal(z, a + torch.nn.functional.interpolate(b, scale_factor=2, mode="nearest"))
+    wt = gen(92, (64, 64, 3, 3), 0.05).to(cuda)
+    bias = gen(93, (64,), 0.05).to(cuda)
+    p = ops.pack_conv_weight(wt)
+    assert ops.conv_algorithm(64, 64, 12, 18, 3, ops.IN_NONE) == ops.ALGO_WINOGRAD4
+    y4 = ops.conv2d(z, p, bias, 64, 3, pad=ops.PAD_REFLECT)
+    yf = ops.conv2d(a, p, bias, 64, 3, pad=ops.PAD_REFLECT, in_op=ops.IN_ADD_UPSAMPLE2, aux=b)
+    ref = torch.nn.functional.conv2d(torch.nn.functional.pad(z.double(), (1, 1, 1, 1),
+                                                             mode="reflect"),
+                                     wt.double(), bias.double())
+    assert rel_l2(y4, ref) < 1e-5 and rel_l2(yf, ref) < 1e-5
+
+
 def test_samodel_test_golden(cuda, golden):
     import network as net
     g = golden("sanet")
