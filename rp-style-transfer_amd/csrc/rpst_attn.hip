@@ -16,13 +16,15 @@
 // are lane-contiguous; global tiles are loaded with 16-B loads along whichever dim is
 // contiguous (RK: row-major rows with k contiguous; KR: k-rows with m/n contiguous).
 // Register prefetch of tile t+1 overlaps the MFMAs of tile t.
+#include <cstdlib>
+
 #include "rpst_common.h"
 
 namespace rpst {
 
 enum { LAY_RK = 0, LAY_KR = 1 };
 
-constexpr int kGBM = 128, kGBN = 128, kGBK = 32, kGPad = 4;
+constexpr int kGBN = 128, kGBK = 32, kGPad = 4;  // M tile: 128 * MW (gemm_f32_kernel)
 
 // B-operand staging transforms (applied to S while it is staged; row r = query index):
 //   BX_NONE   v
@@ -133,12 +135,11 @@ __device__ __forceinline__ void g_load(float (&reg)[16], const float* __restrict
 // B = 32, C = 512, HW = 4096: 10.54 -> 10.33 ms, tools/bench_attn.py; a 64-deep k tile
 // (11.2 ms) and double-buffered LDS with the exp applied at the LDS store (11.2 ms) were
 // slower.)
-template <int LAY>
-constexpr int g_ld() { return LAY == LAY_RK ? 128 + 1 : 128 + kGPad; }
+template <int LAY, int W = 128>
+constexpr int g_ld() { return LAY == LAY_RK ? W + 1 : W + kGPad; }
 
-template <int LAY>
+template <int LAY, int LD = g_ld<LAY>()>
 __device__ __forceinline__ void g_store(float* __restrict__ Xs, const float (&reg)[16], int tid) {
-  constexpr int LD = g_ld<LAY>();
   if (LAY == LAY_KR) {
     const int kk = tid >> 5, r4 = (tid & 31) * 4;
 #pragma unroll
@@ -154,13 +155,16 @@ __device__ __forceinline__ void g_store(float* __restrict__ Xs, const float (&re
   }
 }
 
-template <int ALAY, int BLAY, int BX, bool VECA, bool VECB>
+// MW = 2: 256-row M tiles (each wave 128 x 64): the B tile (and, for the attention, its
+// exp / AEA transform) is staged once per 256 rows of A instead of per 128
+template <int ALAY, int BLAY, int BX, bool VECA, bool VECB, int MW>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
-  constexpr int LDA = g_ld<ALAY>(), LDB = g_ld<BLAY>();
+  constexpr int BMT = 128 * MW;
+  constexpr int LDA = g_ld<ALAY, BMT>(), LDB = g_ld<BLAY>();
   __shared__ float As[kGBK * LDA];
   __shared__ float Bs[kGBK * LDB];
   const int b = blockIdx.z;
-  const int m0 = blockIdx.y * kGBM, n0 = blockIdx.x * kGBN;
+  const int m0 = blockIdx.y * BMT, n0 = blockIdx.x * kGBN;
   const float* A = g.A + b * g.sA;
   const float* B = g.B + b * g.sB;
   float* C = g.C + b * g.sC;
@@ -171,35 +175,42 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, j = lane & 31;
 
-  floatx16 acc[2][2];
+  floatx16 acc[2 * MW][2];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < 2 * MW; ++mt)
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
 
-  float ra[16], rb[16];
+  float ra[MW][16], rb[16];
   const int ktiles = (g.K + kGBK - 1) / kGBK;
-  g_load<ALAY, BX_NONE, VECA>(ra, A, g.lda, m0, 0, g.M, g.K, g.rv, 0, tid);
+#pragma unroll
+  for (int i = 0; i < MW; ++i)
+    g_load<ALAY, BX_NONE, VECA>(ra[i], A, g.lda, m0 + 128 * i, 0, g.M, g.K, g.rv, 0, tid);
   g_load<BLAY, BX, VECB>(rb, B, g.ldb, n0, 0, g.N, g.K, g.rv, voff, tid);
   for (int kt = 0; kt < ktiles; ++kt) {
-    g_store<ALAY>(As, ra, tid);
-    g_store<BLAY>(Bs, rb, tid);
+#pragma unroll
+    for (int i = 0; i < MW; ++i) g_store<ALAY, LDA>(As + 128 * i, ra[i], tid);
+    g_store<BLAY, LDB>(Bs, rb, tid);
     __syncthreads();
     if (kt + 1 < ktiles) {
-      g_load<ALAY, BX_NONE, VECA>(ra, A, g.lda, m0, (kt + 1) * kGBK, g.M, g.K, g.rv, 0, tid);
+#pragma unroll
+      for (int i = 0; i < MW; ++i)
+        g_load<ALAY, BX_NONE, VECA>(ra[i], A, g.lda, m0 + 128 * i, (kt + 1) * kGBK, g.M, g.K,
+                                    g.rv, 0, tid);
       g_load<BLAY, BX, VECB>(rb, B, g.ldb, n0, (kt + 1) * kGBK, g.N, g.K, g.rv, voff, tid);
     }
 #pragma unroll
     for (int kk = 0; kk < kGBK / 2; ++kk) {
-      float av[2], bv[2];
+      float av[2 * MW], bv[2];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) av[mt] = As[(2 * kk + h) * LDA + wm * 64 + mt * 32 + j];
+      for (int mt = 0; mt < 2 * MW; ++mt)
+        av[mt] = As[(2 * kk + h) * LDA + wm * 64 * MW + mt * 32 + j];
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) bv[nt] = Bs[(2 * kk + h) * LDB + wn * 64 + nt * 32 + j];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < 2 * MW; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mt], bv[nt], acc[mt][nt], 0, 0, 0);
@@ -214,10 +225,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     const float cs = cscale ? cscale[n] : 1.f;
     const float cb = g.colbias ? g.colbias[n] : 0.f;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < 2 * MW; ++mt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int m = m0 + wm * 64 * MW + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         float v = acc[mt][nt][r] * cs;
         if (g.colbias) v += cb;
         if (g.act == 1) v = v > 0.f ? v : 0.2f * v;
@@ -263,17 +274,25 @@ __global__ __launch_bounds__(256) void rowstats_kernel(const float* __restrict__
 
 template <int ALAY, int BLAY, int BX>
 static void launch_gemm(const GemmArgs& g, int batch, hipStream_t st) {
-  dim3 grid((g.N + kGBN - 1) / kGBN, (g.M + kGBM - 1) / kGBM, batch);
+  static const int mw_env = [] {
+    const char* e = std::getenv("RPST_GEMM_MW");  // A/B: 1 = 128-row tiles everywhere
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  const int mw = mw_env == 1 ? 1 : (g.M >= 256 ? 2 : 1);
+  dim3 grid((g.N + kGBN - 1) / kGBN, (g.M + 128 * mw - 1) / (128 * mw), batch);
   auto aligned = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   // 16-B loads need the contiguous dim, the leading dim and the batch stride % 4 == 0
   const bool va = aligned(g.A) && (g.lda % 4 == 0) && (g.sA % 4 == 0) &&
                   ((ALAY == LAY_KR) ? (g.M % 4 == 0) : (g.K % 4 == 0));
   const bool vb = aligned(g.B) && (g.ldb % 4 == 0) && (g.sB % 4 == 0) &&
                   ((BLAY == LAY_KR) ? (g.N % 4 == 0) : (g.K % 4 == 0));
-  if (va && vb)
-    gemm_f32_kernel<ALAY, BLAY, BX, true, true><<<grid, 256, 0, st>>>(g);
-  else
-    gemm_f32_kernel<ALAY, BLAY, BX, false, false><<<grid, 256, 0, st>>>(g);
+  if (mw == 2) {
+    if (va && vb) gemm_f32_kernel<ALAY, BLAY, BX, true, true, 2><<<grid, 256, 0, st>>>(g);
+    else gemm_f32_kernel<ALAY, BLAY, BX, false, false, 2><<<grid, 256, 0, st>>>(g);
+  } else {
+    if (va && vb) gemm_f32_kernel<ALAY, BLAY, BX, true, true, 1><<<grid, 256, 0, st>>>(g);
+    else gemm_f32_kernel<ALAY, BLAY, BX, false, false, 1><<<grid, 256, 0, st>>>(g);
+  }
 }
 
 
