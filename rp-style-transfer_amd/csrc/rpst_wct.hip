@@ -662,6 +662,33 @@ __global__ void ns_state_init_kernel(int* stop, int* cnt, double* res, int batch
   res[b] = __longlong_as_double(0x7ff0000000000000LL);  // +inf until measured
 }
 
+// Host-side early exit of the iteration launches: every 4 iterations from the 8th the
+// per-matrix convergence flags are copied to pinned memory and the stream is synchronised;
+// once every matrix has converged the remaining launches (whose blocks would exit at once,
+// ~4.6 us each plus the dispatch gap) are not issued. A run of 9 iterations then launches 12
+// instead of 64 (WCT-RP at n = 16: ~200 empty launches per step). RPST_WCT_NS_POLL=0 issues
+// all kNSMaxIters (the kernels' per-matrix exit alone).
+static bool ns_all_converged(const int* stop, int batch, hipStream_t st) {
+  thread_local int* pinned = nullptr;
+  thread_local int cap = 0;
+  if (cap < batch) {
+    if (pinned) (void)hipHostFree(pinned);
+    pinned = nullptr;
+    if (hipHostMalloc((void**)&pinned, sizeof(int) * (size_t)batch) != hipSuccess) {
+      cap = 0;
+      return false;  // no pinned buffer: keep launching (the kernels still exit early)
+    }
+    cap = batch;
+  }
+  if (hipMemcpyAsync(pinned, stop, sizeof(int) * (size_t)batch, hipMemcpyDeviceToHost, st) !=
+          hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return false;
+  for (int b = 0; b < batch; ++b)
+    if (pinned[b] >= kNSMaxIters) return false;
+  return true;
+}
+
 // out = (A + add I)^p for p = +-1/2 (both if both outputs are given), batched n x n.
 // work: ns_work_doubles(n, batch); res_out: per-matrix final residual (may be null).
 static int ns_power(const double* A, double add, double* sqrt_out, double* isqrt_out, int n,
@@ -684,6 +711,10 @@ static int ns_power(const double* A, double add, double* sqrt_out, double* isqrt
   ns_init_kernel<<<batch, 256, 0, st>>>(A, Y, Z, svec, n, add);
   G64Args ns{};
   ns.stop = stop;
+  static const bool poll = [] {
+    const char* e = std::getenv("RPST_WCT_NS_POLL");
+    return !(e && *e && std::atoi(e) == 0);
+  }();
   for (int it = 0; it < kNSMaxIters; ++it) {
     ns.iter = it;
     ns.tile_sq = tile_sq;
@@ -698,6 +729,9 @@ static int ns_power(const double* A, double add, double* sqrt_out, double* isqrt
     t = Z;
     Z = Z2;
     Z2 = t;
+    if (poll && it + 1 >= 8 && (it + 1) % 4 == 0 && it + 1 < kNSMaxIters &&
+        ns_all_converged(stop, batch, st))
+      break;
   }
   const unsigned blocks = (unsigned)((nn + 255) / 256);
   if (sqrt_out)
