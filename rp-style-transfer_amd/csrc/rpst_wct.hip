@@ -31,6 +31,9 @@
 
 namespace rpst {
 
+#ifndef RPST_WCT_BK
+#define RPST_WCT_BK 32  // k depth of a staged fp64 GEMM tile (16: wct_params 17.77 vs 16.86 ms)
+#endif
 constexpr int kNSMaxIters = 64;
 constexpr double kNSTol = 1e-10;  // on ||I - Z Y||_F (||I||_F = sqrt(n)); quadratic from here
 
@@ -121,7 +124,7 @@ __device__ __forceinline__ void load_run(double (&v)[N], __amdgpu_buffer_rsrc_t 
 
 template <int BT, int SRCA, int SRCB, int BLAY, int OUT, bool VEC>
 __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
-  constexpr int BK = 16, LD = BT + 16, WT = BT / 2, MT = WT / 16;
+  constexpr int BK = RPST_WCT_BK, LD = BT + 16, WT = BT / 2, MT = WT / 16;
   constexpr int EPT = BT * BK / 256;  // elements staged per thread per operand
   __shared__ double As[BK * LD];
   __shared__ double Bs[BK * LD];
