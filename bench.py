@@ -158,6 +158,28 @@ def cpu_info():
     return model, os.cpu_count(), avail
 
 
+def process_group_backend(kind, cuda=True):
+    """torch.distributed backend of a multi-rank run: RCCL ("nccl") only for the training
+    workloads, whose gradient all-reduce is the path's one real exchange step; every
+    inference workload is a per-image split with nothing to exchange (north_star: no RCCL
+    collectives), so its barrier and host-time reductions use gloo."""
+    return "nccl" if (cuda and kind in TRAIN_KINDS) else "gloo"
+
+
+def cpu_share():
+    """Host threads the CPU baseline may use: the CPU share the node allots this job. The
+    GPU pool gives each GPU's job a fixed share of the host's cores and states it in
+    OMP_NUM_THREADS (16 per GPU on an 8-GPU MI355X node, whose os.cpu_count() reports all
+    256); without that variable, every CPU in this process's affinity mask."""
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        return int(omp), "OMP_NUM_THREADS (the node's per-GPU CPU share)"
+    try:
+        return len(os.sched_getaffinity(0)), "sched_getaffinity"
+    except AttributeError:
+        return os.cpu_count() or 1, "os.cpu_count"
+
+
 def cpu_baseline(kind, size, reps=3):
     """Time the CPU oracle on a bounded sample: B=2 content/style pairs at size^2 (B=1 for
     WCT, training and 1024^2), one warm-up then the median of `reps` runs."""
@@ -208,6 +230,9 @@ def cpu_baseline(kind, size, reps=3):
     b = CPU_SAMPLE_BATCH.get(kind, 2) if size <= 512 else 1  # 1024^2: ~6 s per image
     c = torch.from_numpy(synth.image(11, (b, 3, size, size)))
     s = torch.from_numpy(synth.image(12, (b, 3, size, size)))
+    share, share_src = cpu_share()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(share)
     threads = torch.get_num_threads()
     fn(c, s, sd)  # warm-up
     times = []
@@ -216,12 +241,14 @@ def cpu_baseline(kind, size, reps=3):
         fn(c, s, sd)
         times.append(time.perf_counter() - t0)
     med = sorted(times)[len(times) // 2]
+    torch.set_num_threads(prev)
     model, host_cpus, avail = cpu_info()
     return {"value": b / med, "unit": "images/s", "cores": threads, "kind": "port",
             "cpu_model": model, "host_cpus": host_cpus, "cpus_available": avail,
-            "sample": f"oracle (PyTorch-CPU restatement) {kind} test() on B={b} at "
+            "cpu_share": share, "cpu_share_source": share_src,
+            "sample": f"oracle (PyTorch-CPU restatement) {kind} on B={b} at "
                       f"{size}x{size}, median of {reps} after 1 warm-up ({med:.2f}s each), "
-                      f"{threads} torch threads"}
+                      f"{threads} torch threads = the CPUs this job is allotted ({share_src})"}
 
 
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
@@ -443,8 +470,15 @@ def main():
     from rpst.shard import partition
 
     cuda = model_kind != "selftest"
+    tgroup = None
     if world > 1:
-        dist.init_process_group("nccl" if cuda else "gloo")
+        # inference has no data-path collective (per-image split): the barrier and the
+        # MAX / SUM of per-rank host times go over gloo, so no RCCL communicator is created.
+        # Training's one gradient all-reduce per step is the only RCCL traffic; its timing
+        # reductions still use a gloo side group on host scalars.
+        backend = process_group_backend(model_kind, cuda)
+        dist.init_process_group(backend)
+        tgroup = dist.new_group(backend="gloo") if backend != "gloo" else dist.group.WORLD
     if cuda:
         dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)
@@ -512,7 +546,7 @@ def main():
 
     ops.TRACE = ops.Trace() if cuda else None
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=tgroup)
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -520,7 +554,7 @@ def main():
     sync()
     dt_rank = time.perf_counter() - t0
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=tgroup)
     dt = time.perf_counter() - t0
     summary = ops.TRACE.summary() if cuda else {}
     order = None
@@ -534,19 +568,19 @@ def main():
                                           out.shape == (last_chunk,) + shape[1:])
 
     per_rank = [dt_rank]
-    if world > 1:
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    if world > 1:  # host scalars over gloo
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=tgroup)
         dt = float(tt.item())
-        rt = torch.zeros(world, device=dev, dtype=torch.float64)
+        rt = torch.zeros(world, dtype=torch.float64)
         rt[rank] = dt_rank
-        dist.all_reduce(rt, op=dist.ReduceOp.SUM)
-        per_rank = [float(v) for v in rt.cpu()]
+        dist.all_reduce(rt, op=dist.ReduceOp.SUM, group=tgroup)
+        per_rank = [float(v) for v in rt]
     value = total * args.steps / dt
     gathered_ok = None
     if host is not None:
         if world > 1:
-            dist.barrier()  # every rank's slice is in the shared buffer
+            dist.barrier(group=tgroup)  # every rank's slice is in the shared buffer
         gathered_ok = bool(torch.isfinite(host.full).all()) if rank == 0 else None
         if not cuda and rank == 0:  # selftest: the gathered batch equals the unsplit result
             full = (torch.from_numpy(synth.image(1000, (total, 3, size, size))),
@@ -568,6 +602,7 @@ def main():
                                        "all-reduce per step") if model_kind.startswith("train") else
                        f"per-image batch split over {world} GPU(s), no collectives",
                        "host_gather": bool(host is not None),
+                       "process_group": process_group_backend(model_kind, cuda) if world > 1 else None,
                        "micro_batch": mb},
             "per_rank_s": [round(v, 4) for v in per_rank],
         }
@@ -593,7 +628,7 @@ def main():
         print(json.dumps(rec), flush=True)
     if host is not None:
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=tgroup)
         host.close()
     if world > 1:
         dist.destroy_process_group()

@@ -56,6 +56,28 @@ def test_launcher_weak_scaling():
     assert rec["config"]["global_batch"] == 6 and rec["config"]["per_gpu_batch"] == 3
 
 
+def test_inference_creates_no_rccl_group():
+    """north_star: the inference path has no collective; only training's gradient
+    all-reduce may use RCCL (bench.py process_group_backend)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for kind in ("adain", "wct", "sanet", "multiscale", "source", "adaptive", "selftest"):
+        assert bench.process_group_backend(kind, cuda=True) == "gloo", kind
+    for kind in bench.TRAIN_KINDS:
+        assert bench.process_group_backend(kind, cuda=True) == "nccl", kind
+    rec = _bench("--gpus", "2", "--batch", "2", "--steps", "1", "--warmup", "0", "--size", "8")
+    assert rec["config"]["process_group"] == "gloo"
+
+
+def test_cpu_share_follows_omp_num_threads(monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    assert bench.cpu_share()[0] == 16
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.cpu_share()[0] == len(os.sched_getaffinity(0))
+
+
 def test_world_size_mismatch_rejected():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "selftest",

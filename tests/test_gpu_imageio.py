@@ -87,3 +87,38 @@ def test_stylize_driver_end_to_end(cuda, tmp_path, batch_size):
             assert got.shape == ref.shape, suffix
             diff = np.abs(got.astype(int) - ref.astype(int))
             assert diff.max() <= 1 and (diff == 0).mean() > 0.99, (suffix, diff.max())
+
+
+def test_baseline_config0_256_pair(cuda, tmp_path):
+    """BASELINE configs[0]: one AdaIN content+style pair at 256x256 through the test.py
+    counterpart (reference test.py:49-54,128-150) with the deeper-RP configuration
+    (config/rl/train_deeper_rp_adain.yaml: rp_blocks 5, hidden_dim 16); the written
+    {cn}-{sn}.png and -cat.png match the CPU oracle pipeline within 1 LSB."""
+    from PIL import Image
+
+    import stylize
+    from rpst.imageio import PairedDataset, load_image
+    root = str(tmp_path / "data")
+    _write_pairs(root, [(300, 280, "RGB")])  # resized to 256x256 like test.py's Resize
+    cfg = {"network": "adain", "vgg": "unused", "rp_blocks": 5, "hidden_dim": 16,
+           "content_weight": 1.0, "style_weight": 10.0, "resume": False, "use_mask": False,
+           "img_size": 256, "test_dir": root, "test_dataset": "paired",
+           "batch_size": 1, "num_workers": 1, "output": str(tmp_path / "out")}
+    cfg_path = str(tmp_path / "cfg.yaml")
+    with open(cfg_path, "w") as f:
+        yaml.safe_dump(cfg, f)
+    assert stylize.main(["--config", cfg_path, "--synthetic-weights", "3"]) == 0
+    net = stylize.build_network(cfg, synthetic_seed=3)
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    ds = PairedDataset(root)
+    cp, sp, cn, sn, _, _ = ds.item(0)
+    c = R.to_tensor_u8(load_image(cp, 256))[None]
+    s = R.to_tensor_u8(load_image(sp, 256))[None]
+    y = R.adain_rp_test(c, s, sd, 5)
+    out_dir = tmp_path / "out" / "test" / "test_output"
+    for suffix, ref in (("", R.save_image_u8(y[0], nrow=1)),
+                        ("-cat", R.save_image_u8(torch.cat([c, s, y]), nrow=3))):
+        got = np.asarray(Image.open(out_dir / f"{cn}-{sn}{suffix}.png"))
+        assert got.shape == ref.shape, suffix
+        diff = np.abs(got.astype(int) - ref.astype(int))
+        assert diff.max() <= 1 and (diff == 0).mean() > 0.99, (suffix, diff.max())
