@@ -180,7 +180,7 @@ def cpu_share():
         return os.cpu_count() or 1, "os.cpu_count"
 
 
-def cpu_baseline(kind, size, reps=3):
+def cpu_baseline(kind, size, reps=3, batch=None):
     """Time the CPU oracle on a bounded sample: B=2 content/style pairs at size^2 (B=1 for
     WCT, training and 1024^2), one warm-up then the median of `reps` runs."""
     import torch
@@ -227,7 +227,7 @@ def cpu_baseline(kind, size, reps=3):
     synth.synth_module_(m, 0)
     # (.cpu(): SourceNet shares the module-level decoder, which build_model moved to the GPU)
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
-    b = CPU_SAMPLE_BATCH.get(kind, 2) if size <= 512 else 1  # 1024^2: ~6 s per image
+    b = batch or (CPU_SAMPLE_BATCH.get(kind, 2) if size <= 512 else 1)  # 1024^2: ~6 s/image
     c = torch.from_numpy(synth.image(11, (b, 3, size, size)))
     s = torch.from_numpy(synth.image(12, (b, 3, size, size)))
     share, share_src = cpu_share()
@@ -252,22 +252,32 @@ def cpu_baseline(kind, size, reps=3):
 
 
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+# per-config PMC tables (tools/prof_pmc.sh with --config k): BASELINE config -> table
+PMC_CONFIG = {i: os.path.join(ROOT, "profiles", f"r03_pmc_traffic_config{i}.json")
+              for i in (1, 2, 3, 4)}
 
 
-def pmc_table():
-    if not os.path.exists(PMC_TRAFFIC):
-        return {}
-    return json.load(open(PMC_TRAFFIC))
+def pmc_table(path=None):
+    path = path if path and os.path.exists(path) else PMC_TRAFFIC
+    if not os.path.exists(path):
+        return {}, None
+    return json.load(open(path)), path
 
 
-def pmc_lookup(section, key):
+def pmc_lookup(section, key, path=None):
     """HBM bytes per launch of one traced launch (tools/pmc_traffic.py attributes every PMC
     dispatch to the bench launch that issued it); None if that launch was not profiled."""
-    rec = pmc_table().get(section, {}).get(key)
+    table, _ = pmc_table(path)
+    rec = table.get(section, {}).get(key)
     return None if rec is None else rec["traffic_bytes"]
 
 
-def roofline_from_trace(summary):
+def pmc_source(path=None):
+    _, p = pmc_table(path)
+    return os.path.relpath(p, ROOT) if p else None
+
+
+def roofline_from_trace(summary, pmc_path=None):
     from rpst import _lib
     best = None
     for name, a in summary.items():
@@ -291,7 +301,7 @@ def roofline_from_trace(summary):
              "wgrad": "conv_wgrad_kernel", "narrow": "conv3x3_narrow_kernel"}.get(
         next((p for p in ("wino4", "wino", "wgrad", "narrow") if name.startswith(p)), ""),
         "conv_mfma_kernel")
-    traffic = pmc_lookup("launches", name)
+    traffic = pmc_lookup("launches", name, pmc_path)
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
             "traffic": traffic, "kernel": f"{kname} [{name}]",
@@ -301,7 +311,7 @@ def roofline_from_trace(summary):
                 else "direct implicit GEMM fp32"),
             "effective_tflops": round(effective, 2),
             "launch_ms": round(avg_ms, 4), "flop_per_launch": flop,
-            "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None}
+            "traffic_source": pmc_source(pmc_path) if traffic else None}
 
 
 def measure_adain_standalone(dev, n, c, hw, reps=3):
@@ -338,7 +348,7 @@ def stats_roofline(summary):
                     "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
                     "kernel": f"plane_stats_kernel + stat merge [{name}]",
                     "launch_ms": round(avg_ms, 4), "bytes_per_launch": a["bytes"],
-                    "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None}
+                    "traffic_source": pmc_source() if traffic else None}
     return None
 
 
@@ -352,7 +362,7 @@ def adain_roofline(summary):
                     "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
                     "kernel": f"plane_stats_kernel+plane_apply_kernel [{name}]",
                     "launch_ms": round(avg_ms, 4), "bytes_per_launch": a["bytes"],
-                    "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None}
+                    "traffic_source": pmc_source() if traffic else None}
     return None
 
 
@@ -425,6 +435,208 @@ def selftest_model():
     return _M()
 
 
+def run_workload(kind, size, batch, gbatch, gather, micro, steps, warmup, world, rank, dev,
+                 tgroup, cuda=True):
+    """Build `kind` with synthetic weights, run `warmup` untimed and `steps` timed steps (a
+    barrier + device sync on both sides, MAX over ranks) and return the measurement."""
+    import torch
+    import torch.distributed as dist
+    from rpst import ops, synth
+    from rpst.shard import partition
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
+    if gbatch is not None:
+        start, end = partition(gbatch, world, rank)
+        B, scaling, total = end - start, "strong", gbatch
+    else:
+        start, end = rank * batch, (rank + 1) * batch
+        B, scaling, total = batch, "weak", batch * world
+    if B < 1:
+        raise SystemExit(f"bench.py: rank {rank} has no images (global batch {gbatch})")
+    model = selftest_model() if not cuda else build_model(kind, dev)
+    shape = (B, 3, size, size)
+    # image i of the global batch is the same tensor whatever the rank count
+    content = torch.from_numpy(synth.image_range(1000, (total, 3, size, size), start, end)).to(dev)
+    style = torch.from_numpy(synth.image_range(2000, (total, 3, size, size), start, end)).to(dev)
+
+    if kind in TRAIN_KINDS:
+        from rpst.shard import GradientAllReduce
+        trained = model.rp_decoder if kind == "train_wct" else model
+        params = [p for p in trained.parameters() if p.requires_grad]
+        optimizer = torch.optim.Adam(params, lr=1e-4)
+        reduce_grads = GradientAllReduce(params) if world > 1 else None
+
+        def step():
+            optimizer.zero_grad()
+            _, tot = model(content, style)
+            tot.backward()
+            if reduce_grads is not None:
+                reduce_grads()
+            optimizer.step()
+            return tot
+    host = None
+    if gather:
+        tag = (f"{os.environ.get('MASTER_PORT', 'solo')}_"
+               f"{os.getppid() if world > 1 else os.getpid()}_{kind}{size}")
+        host = HostGather(tag, (total, 3, size, size), start, end, rank, cuda)
+    mb = micro if micro and micro < B else B
+    # the D2H gather of chunk i runs on a copy stream while chunk i + 1 computes
+    copy_stream = torch.cuda.Stream(dev) if (cuda and host is not None) else None
+
+    if kind not in TRAIN_KINDS:
+        def step():
+            out = None
+            for s0 in range(0, B, mb):
+                out = model.test(content[s0:s0 + mb], style[s0:s0 + mb])
+                if host is not None:
+                    if copy_stream is None:
+                        host.put(out, s0)
+                        continue
+                    done = torch.cuda.Event()
+                    done.record()
+                    with torch.cuda.stream(copy_stream):
+                        copy_stream.wait_event(done)
+                        host.put(out, s0)
+                        out.record_stream(copy_stream)
+            return out
+
+    for _ in range(warmup):
+        out = step()
+    sync()
+
+    ops.TRACE = ops.Trace() if cuda else None
+    if world > 1:
+        dist.barrier(group=tgroup)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    sync()
+    dt_rank = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier(group=tgroup)
+    dt = time.perf_counter() - t0
+    summary = ops.TRACE.summary() if cuda else {}
+    order = None
+    if cuda:
+        names = [r[0] for r in ops.TRACE.records]
+        order = {"steps": steps, "warmup": warmup, "per_step": names[:len(names) // max(steps, 1)]}
+    ops.TRACE = None
+    last_chunk = B - mb * ((B - 1) // mb)
+    assert torch.isfinite(out).all() and (kind.startswith("train") or
+                                          out.shape == (last_chunk,) + shape[1:])
+
+    per_rank = [dt_rank]
+    if world > 1:  # host scalars over gloo
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=tgroup)
+        dt = float(tt.item())
+        rt = torch.zeros(world, dtype=torch.float64)
+        rt[rank] = dt_rank
+        dist.all_reduce(rt, op=dist.ReduceOp.SUM, group=tgroup)
+        per_rank = [float(v) for v in rt]
+    gathered_ok = None
+    host_rec = None
+    if host is not None:
+        if world > 1:
+            dist.barrier(group=tgroup)  # every rank's slice is in the shared buffer
+        gathered_ok = bool(torch.isfinite(host.full).all()) if rank == 0 else None
+        if not cuda and rank == 0:  # selftest: the gathered batch equals the unsplit result
+            full = (torch.from_numpy(synth.image(1000, (total, 3, size, size))),
+                    torch.from_numpy(synth.image(2000, (total, 3, size, size))))
+            gathered_ok = gathered_ok and torch.equal(host.full, model.test(*full))
+        host_rec = {"pinned": host.pinned, "bytes_per_step": total * 3 * size * size * 4,
+                    "all_finite": gathered_ok}
+        if world > 1:
+            dist.barrier(group=tgroup)
+        host.close()
+    del model, content, style, out
+    if cuda:
+        torch.cuda.empty_cache()
+    return {"value": total * steps / dt, "dt": dt, "per_rank": per_rank, "summary": summary,
+            "order": order, "B": B, "total": total, "scaling": scaling, "mb": mb,
+            "host": host_rec, "steps": steps, "warmup": warmup}
+
+
+def stack_roofline(summary, steps, dt):
+    """Whole-step MFMA utilisation of the conv stack (north_star: "MFMA utilisation for the
+    conv stack"): the FLOPs the conv launches of one step execute (Winograd priced on the
+    multiplies its algorithm performs, like `roofline`) divided by the whole step time, and
+    their share of the step's device time."""
+    flop = conv_ms = 0.0
+    for name, a in summary.items():
+        if not name.startswith(("conv", "wino", "narrow", "wgrad")):
+            continue
+        f = 0.25 if name.startswith("wino4") else (4.0 / 9.0 if name.startswith("wino") else 1.0)
+        flop += a["flops"] * f * a["launches"]
+        conv_ms += a["ms"]
+    if not flop:
+        return None
+    step_s = dt / steps
+    achieved = flop / steps / step_s / 1e12
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+            "executed_flop_per_step": flop / steps, "ms_per_step": round(1e3 * step_s, 3),
+            "conv_kernel_ms_per_step": round(conv_ms / steps, 3),
+            "conv_share_of_step": round(conv_ms / steps / (1e3 * step_s), 4)}
+
+
+def wct_roofline(summary):
+    """fp64 rate of rpst_wct_params (covariances + matrix functions, wct_rp.py:82-109) on the
+    covariance FLOPs alone (2 x 2 C^2 HW per image: a lower bound on the work) against the
+    fp64 MFMA peak; the launch is bound by the fp64 MFMA (SURVEY §8(d) config #3)."""
+    for name, a in summary.items():
+        if name.startswith("wct_params"):
+            avg_ms = a["ms"] / a["launches"]
+            tf = a["flops"] / (avg_ms * 1e-3) / 1e12
+            return {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP64_TFLOPS,
+                    "unit": "TFLOP/s (fp64)", "frac": round(tf / PEAK_FP64_TFLOPS, 4),
+                    "kernel": f"cov_syrk_kernel + matfun_kernel [{name}]",
+                    "launch_ms": round(avg_ms, 4), "flop_per_launch": a["flops"],
+                    "traffic": pmc_lookup("wct", name, PMC_CONFIG.get(2)),
+                    "flop_basis": "covariances 2 x 2 C^2 HW per image"}
+    return None
+
+
+def sub_record(cfg_index, meas, kind, size, world, steps, with_cpu):
+    """One BASELINE config measured in the same run as the headline line."""
+    rec = {"config": cfg_index, "workload": WORKLOADS[kind], "image": f"{size}x{size}",
+           "value": round(meas["value"], 3), "unit": "images/s",
+           "ms_per_step": round(1e3 * meas["dt"] / steps, 3), "steps": steps,
+           "warmup": meas["warmup"], "per_gpu_batch": meas["B"], "global_batch": meas["total"],
+           "micro_batch": meas["mb"], "scaling": meas["scaling"], "n_gpus": world,
+           "roofline": roofline_from_trace(meas["summary"], PMC_CONFIG.get(cfg_index)),
+           "roofline_stack": stack_roofline(meas["summary"], steps, meas["dt"]),
+           "kernel_ms_per_step": {k: round(v["ms"] / steps, 3) for k, v in sorted(
+               meas["summary"].items(), key=lambda kv: -kv[1]["ms"])[:8]}}
+    if kind == "wct":
+        rec["roofline_wct"] = wct_roofline(meas["summary"])
+    if meas["host"] is not None:
+        rec["host_gather"] = meas["host"]
+    if kind == "sanet":
+        for name, a in meas["summary"].items():
+            if name.startswith("sanet_attention"):
+                avg = a["ms"] / a["launches"]
+                tf = a["flops"] / (avg * 1e-3) / 1e12
+                rec["roofline_attention"] = {
+                    "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP32_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(tf / PEAK_FP32_TFLOPS, 4),
+                    "kernel": f"gemm_f32_kernel + rowstats_kernel [{name}]",
+                    "launch_ms": round(avg, 4)}
+                break
+    rec["cpu_baseline"] = cpu_baseline(kind, size) if with_cpu else None
+    return rec
+
+
+def config0_record():
+    """BASELINE configs[0]: one AdaIN content+style pair at 256x256 through test() on PyTorch
+    CPU (the plumbing case): the oracle timed on this host (tests/test_gpu_imageio.py runs
+    the same pair through stylize.py on the GPU against it)."""
+    rec = cpu_baseline("adain", 256, reps=5, batch=1)
+    return {"config": 0, "workload": "AdaINRPNet.test() on one 256x256 content+style pair, "
+            "PyTorch CPU (the reference's plumbing case; oracle restatement)",
+            "value": rec["value"], "unit": "images/s", "cpu_baseline": rec}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -442,10 +654,13 @@ def main():
     ap.add_argument("--micro-batch", type=int, default=None,
                     help="images per test() call within a step (default: the whole batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="default run only: skip the configs[0], [2]-[4] sub-records")
     ap.add_argument("--layer-order", default=None,
                     help="write the traced launch names of one step (tools/pmc_traffic.py)")
     args = ap.parse_args()
 
+    default_run = args.config is None and args.model is None
     model_kind, size, batch, gbatch, gather, micro = CONFIGS[args.config or 1]
     if args.config is None:
         model_kind, size, batch, gbatch, gather, micro = "adain", 512, None, None, False, None
@@ -466,8 +681,6 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from rpst import ops, synth
-    from rpst.shard import partition
 
     cuda = model_kind != "selftest"
     tgroup = None
@@ -484,138 +697,62 @@ def main():
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
-    sync = torch.cuda.synchronize if cuda else (lambda: None)
 
-    if gbatch is not None:
-        start, end = partition(gbatch, world, rank)
-        B, scaling, total = end - start, "strong", gbatch
-    else:
-        start, end = rank * batch, (rank + 1) * batch
-        B, scaling, total = batch, "weak", batch * world
-    if B < 1:
-        raise SystemExit(f"bench.py: rank {rank} has no images (global batch {gbatch})")
-    model = selftest_model() if not cuda else build_model(model_kind, dev)
-    shape = (B, 3, size, size)
-    # image i of the global batch is the same tensor whatever the rank count
-    content = torch.from_numpy(synth.image_range(1000, (total, 3, size, size), start, end)).to(dev)
-    style = torch.from_numpy(synth.image_range(2000, (total, 3, size, size), start, end)).to(dev)
-
-    if model_kind in TRAIN_KINDS:
-        from rpst.shard import GradientAllReduce
-        trained = model.rp_decoder if model_kind == "train_wct" else model
-        params = [p for p in trained.parameters() if p.requires_grad]
-        optimizer = torch.optim.Adam(params, lr=1e-4)
-        reduce_grads = GradientAllReduce(params) if world > 1 else None
-
-        def step():
-            optimizer.zero_grad()
-            _, tot = model(content, style)
-            tot.backward()
-            if reduce_grads is not None:
-                reduce_grads()
-            optimizer.step()
-            return tot
-    host = None
-    if gather:
-        tag = f"{os.environ.get('MASTER_PORT', 'solo')}_{os.getppid() if world > 1 else os.getpid()}"
-        host = HostGather(tag, (total, 3, size, size), start, end, rank, cuda)
-    mb = micro if micro and micro < B else B
-    # the D2H gather of chunk i runs on a copy stream while chunk i + 1 computes
-    copy_stream = torch.cuda.Stream(dev) if (cuda and host is not None) else None
-
-    if model_kind not in TRAIN_KINDS:
-        def step():
-            out = None
-            for s0 in range(0, B, mb):
-                out = model.test(content[s0:s0 + mb], style[s0:s0 + mb])
-                if host is not None:
-                    if copy_stream is None:
-                        host.put(out, s0)
-                        continue
-                    done = torch.cuda.Event()
-                    done.record()
-                    with torch.cuda.stream(copy_stream):
-                        copy_stream.wait_event(done)
-                        host.put(out, s0)
-                        out.record_stream(copy_stream)
-            return out
-
-    for _ in range(args.warmup):
-        out = step()
-    sync()
-
-    ops.TRACE = ops.Trace() if cuda else None
-    if world > 1:
-        dist.barrier(group=tgroup)
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    sync()
-    dt_rank = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier(group=tgroup)
-    dt = time.perf_counter() - t0
-    summary = ops.TRACE.summary() if cuda else {}
-    order = None
-    if cuda:
-        names = [r[0] for r in ops.TRACE.records]
-        order = {"steps": args.steps, "warmup": args.warmup,
-                 "per_step": names[:len(names) // max(args.steps, 1)]}
-    ops.TRACE = None
-    last_chunk = B - mb * ((B - 1) // mb)
-    assert torch.isfinite(out).all() and (model_kind.startswith("train") or
-                                          out.shape == (last_chunk,) + shape[1:])
-
-    per_rank = [dt_rank]
-    if world > 1:  # host scalars over gloo
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=tgroup)
-        dt = float(tt.item())
-        rt = torch.zeros(world, dtype=torch.float64)
-        rt[rank] = dt_rank
-        dist.all_reduce(rt, op=dist.ReduceOp.SUM, group=tgroup)
-        per_rank = [float(v) for v in rt]
-    value = total * args.steps / dt
-    gathered_ok = None
-    if host is not None:
-        if world > 1:
-            dist.barrier(group=tgroup)  # every rank's slice is in the shared buffer
-        gathered_ok = bool(torch.isfinite(host.full).all()) if rank == 0 else None
-        if not cuda and rank == 0:  # selftest: the gathered batch equals the unsplit result
-            full = (torch.from_numpy(synth.image(1000, (total, 3, size, size))),
-                    torch.from_numpy(synth.image(2000, (total, 3, size, size))))
-            gathered_ok = gathered_ok and torch.equal(host.full, model.test(*full))
+    meas = run_workload(model_kind, size, batch, gbatch, gather, micro, args.steps, args.warmup,
+                        world, rank, dev, tgroup, cuda)
+    summary, dt = meas["summary"], meas["dt"]
+    sub = []
+    if cuda and default_run and not args.no_configs:
+        # every BASELINE config in the same driver-timed run: configs[2] / [3] (one GPU's
+        # batch) on rank 0 of a 1-GPU run, configs[4] (128 images at 1024^2 split over the
+        # ranks, host gather) at every GPU count
+        ksub, wsub = max(3, args.steps // 4), min(args.warmup, 2)
+        cfgs = (2, 3, 4) if world == 1 else (4,)
+        for ci in cfgs:
+            kind, sz, bt, gb, ga, mi = CONFIGS[ci]
+            m = run_workload(kind, sz, bt, gb, ga, mi, ksub, max(wsub, 1), world, rank, dev,
+                             tgroup, cuda)
+            if rank == 0:
+                sub.append(sub_record(ci, m, kind, sz, world, ksub,
+                                      world == 1 and not args.no_cpu_baseline))
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            sub.insert(0, config0_record())
 
     if rank == 0:
         rec = {
-            "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
+            "metric": METRIC, "value": round(meas["value"], 3), "unit": "images/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True,
-            "scaling": scaling, "vs_baseline": None,
+            "scaling": meas["scaling"], "vs_baseline": None,
             "dtype": "fp32 conv / f64 WCT" if model_kind == "wct" else "fp32",
             "data": "synthetic U[0,1) images, synthetic He-uniform weights",
-            "config": {"workload": WORKLOADS[model_kind], "per_gpu_batch": B,
-                       "global_batch": total, "image": f"{size}x{size}",
-                       "baseline_config": args.config,
+            "config": {"workload": WORKLOADS[model_kind], "per_gpu_batch": meas["B"],
+                       "global_batch": meas["total"], "image": f"{size}x{size}",
+                       "baseline_config": args.config if args.config is not None else (
+                           1 if default_run else None),
                        "parallelism": (f"data parallel over {world} GPU(s), one gradient "
                                        "all-reduce per step") if model_kind.startswith("train") else
                        f"per-image batch split over {world} GPU(s), no collectives",
-                       "host_gather": bool(host is not None),
+                       "host_gather": meas["host"] is not None,
                        "process_group": process_group_backend(model_kind, cuda) if world > 1 else None,
-                       "micro_batch": mb},
-            "per_rank_s": [round(v, 4) for v in per_rank],
+                       "micro_batch": meas["mb"]},
+            "per_rank_s": [round(v, 4) for v in meas["per_rank"]],
         }
-        if host is not None:
-            rec["host_gather"] = {"pinned": host.pinned, "bytes_per_step": total * 3 * size * size * 4,
-                                  "all_finite": gathered_ok}
+        if meas["host"] is not None:
+            rec["host_gather"] = meas["host"]
         if cuda:
-            rec["roofline"] = roofline_from_trace(summary)
-            adain_summary = measure_adain_standalone(dev, min(B, 32), 256, min(size, 512) ** 2)
+            cfg_i = args.config if args.config is not None else (1 if default_run else None)
+            rec["roofline"] = roofline_from_trace(summary, PMC_CONFIG.get(cfg_i))
+            rec["roofline_stack"] = stack_roofline(summary, args.steps, dt)
+            if model_kind == "wct":
+                rec["roofline_wct"] = wct_roofline(summary)
+            adain_summary = measure_adain_standalone(dev, min(meas["B"], 32), 256,
+                                                     min(size, 512) ** 2)
             rec["roofline_adain"] = adain_roofline(
                 summary if any(k.startswith("adain") for k in summary) else adain_summary)
             rec["roofline_adain_stats"] = stats_roofline(adain_summary)
             if args.layer_order:
+                order = meas["order"]
                 order["adain_name"] = next((k for k in adain_summary if k.startswith("adain")), None)
                 order["stats_name"] = next((k for k in adain_summary if k.startswith("stats")), None)
                 json.dump(order, open(args.layer_order, "w"), indent=1)
@@ -625,11 +762,9 @@ def main():
                 rec["cpu_baseline"] = None
             kernels = sorted(summary.items(), key=lambda kv: -kv[1]["ms"])[:12]
             rec["kernel_ms_per_step"] = {k: round(v["ms"] / args.steps, 3) for k, v in kernels}
+            if sub:
+                rec["configs"] = sub
         print(json.dumps(rec), flush=True)
-    if host is not None:
-        if world > 1:
-            dist.barrier(group=tgroup)
-        host.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -9,23 +9,16 @@
 //   Mid = (Sc Cs Sc + 1e-4 I)^(1/2)                                         wct_rp.py:107
 //   T = Ic Mid Ic ; out = T (cF - mu_c) + mu_s  -> fp32                     wct_rp.py:109-113
 //   (the last product on the fp32 MFMA for fp32 features, T rounded once; see below)
-// Matrix square roots: coupled Newton-Schulz on A/||A||_F (GEMM-only):
-//   T_k = (3I - Z_k Y_k)/2, Y_{k+1} = Y_k T_k, Z_{k+1} = T_k Z_k  ->  Y = (A/s)^(1/2),
-//   Z = (A/s)^(-1/2). The reference's SVD truncation (singular values < 1e-5) can never
-//   trigger because every input carries +1e-4 I on a PSD matrix, and V diag(e^p) V^T of
-//   an SVD equals the principal power, so the two agree to fp64 rounding (~1e-13).
-//   Convergence is checked per matrix: after each T_k a residual kernel computes
-//   r_k = ||I - Z_k Y_k||_F = 2 ||T_k - I||_F; once r_k < kNSTol the matrix takes that last
-//   update and every later iteration skips it (its blocks exit at once), so a batch costs
-//   the iterations of its slowest matrix (10-25 on encoder covariances) up to kNSMaxIters.
-//   The final residual of every matrix is written out; a matrix that has not converged
-//   (an input that is not symmetric positive semi-definite after the +1e-4 I shift, or
-//   beyond kNSMaxIters' reach) is reported by the caller instead of being returned silently.
+// The covariances of fp32 features with C <= 256 come from cov_syrk_kernel and the matrix
+// functions (Newton-Schulz square roots, Sc Cs Sc, Ic Mid Ic, mu_s - T mu_c) from the
+// persistent matfun_kernel (rpst_wct_mat.hip); this file keeps the generic tiled fp64 GEMM
+// (covariances for C > 256 or fp64 features, the fp64 colour transform) and the entry points.
 //
 // GEMM: v_mfma_f64_16x16x4_f64 (A[l&15][k=l>>4], B[k=l>>4][l&15], D col=l&15,
 // row=(l>>4)+4r). Tiles BT x BT (64 or 128) x 16, 256 threads = 2x2 waves, operands
 // staged k-major in LDS with a 16-double pad (conflict-free ds_read_b64 halves).
 #include "rpst_common.h"
+#include "rpst_wct.h"
 
 #include <cstdlib>
 
@@ -34,8 +27,6 @@ namespace rpst {
 #ifndef RPST_WCT_BK
 #define RPST_WCT_BK 32  // k depth of a staged fp64 GEMM tile (16: wct_params 17.77 vs 16.86 ms)
 #endif
-constexpr int kNSMaxIters = 64;
-constexpr double kNSTol = 1e-10;  // on ||I - Z Y||_F (||I||_F = sqrt(n)); quadratic from here
 
 enum { SRC_F64 = 0, SRC_F64C = 1, SRC_F32C = 2 };  // plain fp64 / centered fp64 / centered fp32
 enum { B_KN = 0, B_NK = 1 };
@@ -61,16 +52,6 @@ struct G64Args {
   const void* B2;
   void* C2;
   int dual;
-  // Newton-Schulz early exit (iteration `iter`): batch entry b is skipped once it converged
-  // in an earlier iteration (stop[b] < iter). With tile_sq set (the T = (3I - ZY)/2
-  // product), every block also reduces sum (T - I)^2 over its tile; the last block of a
-  // matrix to finish sums the tiles in fixed order: res[b] = 2 ||T - I||_F =
-  // ||I - Z Y||_F, and stop[b] = iter once res[b] < kNSTol.
-  int* stop;
-  int iter;
-  double* tile_sq;
-  int* tile_cnt;
-  double* res;
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -155,7 +136,6 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
     gB = g.B2;
     gC = g.C2;
   }
-  if (g.stop && g.stop[b] < g.iter) return;  // converged matrix (block-uniform)
   const int m0 = ti * BT, n0 = tj * BT;
   // split-K ranges are whole BK tiles
   const int kper = ((g.K + g.ksplit - 1) / g.ksplit + BK - 1) / BK * BK;
@@ -257,7 +237,6 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
 
   // epilogue: D col = lane&15, row = (lane>>4) + 4r
   const double alpha = g.alpha * (g.avec ? g.avec[b] : 1.0);
-  double sq = 0.0;  // Newton-Schulz residual: sum over this thread's outputs of (out - I)^2
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
 #pragma unroll
@@ -273,42 +252,13 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
         if (OUT == OUT_PARTIAL) {
           static_cast<double*>(gC)[(int64_t)z * g.sC + (int64_t)m * g.ldc + n] = v;
         } else if (OUT == OUT_F64) {
-          const double o = alpha * v + (m == n ? g.beta_diag : 0.0);
-          static_cast<double*>(gC)[b * g.sC + (int64_t)m * g.ldc + n] = o;
-          const double dv = o - (m == n ? 1.0 : 0.0);
-          sq = fma(dv, dv, sq);
+          static_cast<double*>(gC)[b * g.sC + (int64_t)m * g.ldc + n] =
+              alpha * v + (m == n ? g.beta_diag : 0.0);
         } else if (OUT == OUT_F32_BIAS) {
           static_cast<float*>(gC)[b * g.sC + (int64_t)m * g.ldc + n] = (float)(v + bias);
         } else {
           static_cast<double*>(gC)[b * g.sC + (int64_t)m * g.ldc + n] = v + bias;
         }
-      }
-    }
-  }
-  if (OUT == OUT_F64 && g.tile_sq) {
-    // block sum (fixed order), then the last block of matrix b reduces the tiles
-    // (MI355X_MICROARCH.md, inter-workgroup visibility: release fence + explicit vmcnt
-    // wait before the counter add, acquire fence before reading the other tiles' partials)
-    sq = wave_sum(sq);
-    __shared__ double red[4];
-    if (lane == 0) red[wave] = sq;
-    __syncthreads();
-    if (tid == 0) {
-      const int ntiles = (int)(gridDim.x * gridDim.y);
-      const int tile = (int)(blockIdx.y * gridDim.x + blockIdx.x);
-      g.tile_sq[(int64_t)b * ntiles + tile] = (red[0] + red[1]) + (red[2] + red[3]);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int old = __hip_atomic_fetch_add(g.tile_cnt + b, 1, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-      if (old == ntiles - 1) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        double tot = 0.0;
-        for (int t = 0; t < ntiles; ++t) tot += g.tile_sq[(int64_t)b * ntiles + t];
-        const double r = 2.0 * sqrt(tot);
-        g.res[b] = r;
-        if (r < kNSTol) g.stop[b] = g.iter;
-        g.tile_cnt[b] = 0;  // the next iteration's launch starts from 0
       }
     }
   }
@@ -544,37 +494,6 @@ __global__ void cov_reduce_kernel(const double* __restrict__ P, double* __restri
   C[i] = s * scale + (r == c ? diag : 0.0);
 }
 
-// Newton-Schulz init: s_b = ||A_b + add I||_F ; Y_b = (A_b + add I)/s_b ; Z_b = I.
-__global__ __launch_bounds__(256) void ns_init_kernel(const double* __restrict__ A,
-                                                      double* __restrict__ Y,
-                                                      double* __restrict__ Z,
-                                                      double* __restrict__ svec, int n,
-                                                      double add) {
-  const int b = blockIdx.x;
-  const double* a = A + (int64_t)b * n * n;
-  double s = 0.0;
-  for (int i = threadIdx.x; i < n * n; i += 256) {
-    const double v = a[i] + ((i / n) == (i % n) ? add : 0.0);
-    s += v * v;
-  }
-  s = wave_sum(s);
-  __shared__ double red[4];
-  __shared__ double tot;
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    tot = sqrt((red[0] + red[1]) + (red[2] + red[3]));
-    svec[b] = tot;
-  }
-  __syncthreads();
-  const double inv = 1.0 / tot;
-  for (int i = threadIdx.x; i < n * n; i += 256) {
-    const bool d = (i / n) == (i % n);
-    Y[(int64_t)b * n * n + i] = (a[i] + (d ? add : 0.0)) * inv;
-    Z[(int64_t)b * n * n + i] = d ? 1.0 : 0.0;
-  }
-}
-
 // ---- host-side pipeline ------------------------------------------------------------
 template <int BT, int SRCA, int SRCB, int BLAY, int OUT>
 static void gemm64(const G64Args& g, dim3 grid, hipStream_t st) {
@@ -595,167 +514,6 @@ static void gemm64(const G64Args& g, dim3 grid, hipStream_t st) {
 
 static int env_int(const char* name, int dflt);
 
-// C[b] = alpha*avec[b]*A[b]B[b] + beta_diag*I for batched n x n fp64 matrices.
-static void small_gemm(const double* A, const double* B, double* C, int n, int batch,
-                       double alpha, double beta_diag, const double* avec, hipStream_t st,
-                       const double* A2 = nullptr, const double* B2 = nullptr,
-                       double* C2 = nullptr, const G64Args* ns = nullptr) {
-  if (A2 && 2 * batch > 65535) {  // grid.z limit: two launches
-    small_gemm(A, B, C, n, batch, alpha, beta_diag, avec, st, nullptr, nullptr, nullptr, ns);
-    small_gemm(A2, B2, C2, n, batch, alpha, beta_diag, avec, st, nullptr, nullptr, nullptr, ns);
-    return;
-  }
-  G64Args g{};
-  if (ns) {  // Newton-Schulz early-exit / residual fields
-    g.stop = ns->stop;
-    g.iter = ns->iter;
-    g.tile_sq = ns->tile_sq;
-    g.tile_cnt = ns->tile_cnt;
-    g.res = ns->res;
-  }
-  g.A = A;
-  g.B = B;
-  g.C = C;
-  if (A2) {  // second product C2 = A2 B2 in the same launch
-    g.A2 = A2;
-    g.B2 = B2;
-    g.C2 = C2;
-    g.dual = batch;
-  }
-  const int zb = A2 ? 2 * batch : batch;
-  g.avec = avec;
-  g.alpha = alpha;
-  g.beta_diag = beta_diag;
-  g.M = g.N = g.K = n;
-  g.lda = g.ldb = g.ldc = n;
-  g.sA = g.sB = g.sC = (int64_t)n * n;
-  g.ksplit = 1;
-  // 32x32 tiles: at n = 256, batch 16 that is 1024 workgroups instead of 256 (one per CU
-  // would leave each CU a single latency-bound 64x64 tile); RPST_WCT_NS_BT=64 restores
-  const int bt = env_int("RPST_WCT_NS_BT", 32);
-  if (bt == 32) {
-    const int t = (n + 31) / 32;
-    gemm64<32, SRC_F64, SRC_F64, B_KN, OUT_F64>(g, dim3(t, t, zb), st);
-  } else {
-    const int t = (n + 63) / 64;
-    gemm64<64, SRC_F64, SRC_F64, B_KN, OUT_F64>(g, dim3(t, t, zb), st);
-  }
-}
-
-
-// out_b = buf[(last_b + 1) & 1]_b * s_b^p with last_b = min(stop_b, kNSMaxIters - 1): the
-// matrix's newest iterate (the ping-pong buffers swap every iteration on the host, a
-// converged matrix stops being updated after its iteration stop_b)
-__global__ void ns_final_kernel(const double* __restrict__ buf0, const double* __restrict__ buf1,
-                                double* __restrict__ out, const double* __restrict__ svec,
-                                const int* __restrict__ stop, double p, int64_t per, int batch) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= per * batch) return;
-  const int64_t b = i / per;
-  const int last = min(stop[b], kNSMaxIters - 1);
-  const double* src = ((last + 1) & 1) ? buf1 : buf0;
-  out[i] = src[i] * pow(svec[b], p);
-}
-
-__global__ void ns_state_init_kernel(int* stop, int* cnt, double* res, int batch) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= batch) return;
-  stop[b] = 1 << 30;
-  cnt[b] = 0;
-  res[b] = __longlong_as_double(0x7ff0000000000000LL);  // +inf until measured
-}
-
-// Host-side early exit of the iteration launches: every 4 iterations from the 8th the
-// per-matrix convergence flags are copied to pinned memory and the stream is synchronised;
-// once every matrix has converged the remaining launches (whose blocks would exit at once,
-// ~4.6 us each plus the dispatch gap) are not issued. A run of 9 iterations then launches 12
-// instead of 64 (WCT-RP at n = 16: ~200 empty launches per step). RPST_WCT_NS_POLL=0 issues
-// all kNSMaxIters (the kernels' per-matrix exit alone).
-static bool ns_all_converged(const int* stop, int batch, hipStream_t st) {
-  thread_local int* pinned = nullptr;
-  thread_local int cap = 0;
-  if (cap < batch) {
-    if (pinned) (void)hipHostFree(pinned);
-    pinned = nullptr;
-    if (hipHostMalloc((void**)&pinned, sizeof(int) * (size_t)batch) != hipSuccess) {
-      cap = 0;
-      return false;  // no pinned buffer: keep launching (the kernels still exit early)
-    }
-    cap = batch;
-  }
-  if (hipMemcpyAsync(pinned, stop, sizeof(int) * (size_t)batch, hipMemcpyDeviceToHost, st) !=
-          hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return false;
-  for (int b = 0; b < batch; ++b)
-    if (pinned[b] >= kNSMaxIters) return false;
-  return true;
-}
-
-// out = (A + add I)^p for p = +-1/2 (both if both outputs are given), batched n x n.
-// work: ns_work_doubles(n, batch); res_out: per-matrix final residual (may be null).
-static int ns_power(const double* A, double add, double* sqrt_out, double* isqrt_out, int n,
-                    int batch, double* work, hipStream_t st, double* res_out = nullptr) {
-  const int64_t nn = (int64_t)n * n * batch;
-  double* Y = work;
-  double* Z = Y + nn;
-  double* T = Z + nn;
-  double* Y2 = T + nn;
-  double* Z2 = Y2 + nn;
-  double* svec = Z2 + nn;
-  double* res = svec + batch;
-  const int tiles = (n + 31) / 32;  // small_gemm's 32 x 32 tiles (RPST_WCT_NS_BT=64: 64)
-  double* tile_sq = res + batch;
-  int* stop = reinterpret_cast<int*>(tile_sq + (size_t)batch * tiles * tiles);
-  int* cnt = stop + batch;
-  double* const buf0[2] = {Y, Z};
-  double* const buf1[2] = {Y2, Z2};
-  ns_state_init_kernel<<<(batch + 255) / 256, 256, 0, st>>>(stop, cnt, res, batch);
-  ns_init_kernel<<<batch, 256, 0, st>>>(A, Y, Z, svec, n, add);
-  G64Args ns{};
-  ns.stop = stop;
-  static const bool poll = [] {
-    const char* e = std::getenv("RPST_WCT_NS_POLL");
-    return !(e && *e && std::atoi(e) == 0);
-  }();
-  for (int it = 0; it < kNSMaxIters; ++it) {
-    ns.iter = it;
-    ns.tile_sq = tile_sq;
-    ns.tile_cnt = cnt;
-    ns.res = res;
-    small_gemm(Z, Y, T, n, batch, -0.5, 1.5, nullptr, st, nullptr, nullptr, nullptr, &ns);
-    ns.tile_sq = nullptr;  // Y <- Y T, Z <- T Z (skipped after the converging iteration)
-    small_gemm(Y, T, Y2, n, batch, 1.0, 0.0, nullptr, st, T, Z, Z2, &ns);
-    double* t = Y;
-    Y = Y2;
-    Y2 = t;
-    t = Z;
-    Z = Z2;
-    Z2 = t;
-    if (poll && it + 1 >= 8 && (it + 1) % 4 == 0 && it + 1 < kNSMaxIters &&
-        ns_all_converged(stop, batch, st))
-      break;
-  }
-  const unsigned blocks = (unsigned)((nn + 255) / 256);
-  if (sqrt_out)
-    ns_final_kernel<<<blocks, 256, 0, st>>>(buf0[0], buf1[0], sqrt_out, svec, stop, 0.5,
-                                            (int64_t)n * n, batch);
-  if (isqrt_out)
-    ns_final_kernel<<<blocks, 256, 0, st>>>(buf0[1], buf1[1], isqrt_out, svec, stop, -0.5,
-                                            (int64_t)n * n, batch);
-  if (res_out)
-    RPST_REQUIRE(hipMemcpyAsync(res_out, res, sizeof(double) * batch, hipMemcpyDeviceToDevice,
-                                st) == hipSuccess, "newton-schulz: residual copy failed");
-  return launch_status("newton-schulz");
-}
-
-static size_t ns_work_doubles(int n, int batch) {
-  const size_t tiles = (size_t)(n + 31) / 32;
-  // Y Z T Y2 Z2, svec, res, per-tile residual partials, stop + counter (ints)
-  return 5 * (size_t)n * n * batch + 2 * (size_t)batch + (size_t)batch * tiles * tiles +
-         (size_t)batch;
-}
-
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return (e && *e) ? atoi(e) : dflt;
@@ -774,17 +532,20 @@ static int pick_ksplit(int64_t K) {
 
 struct WctLayout {
   int n, C, ksplit, BT, tiles, symtiles;
+  bool v2;  // fp32 features with C <= 256: cov_syrk_kernel (rpst_wct_mat.hip)
   int64_t HW;
   // offsets in doubles
-  size_t mu_c, mu_s, part, cc, cs, sc, ic, m0, mid, tmp, tm, ns;
+  size_t mu_c, mu_s, mu32, part, cc, cs, tm, off, tf, mf;
   size_t total;
 };
 
-static WctLayout wct_layout(int n, int C, int64_t HW) {
+// src_f32: the features are fp32 (the v2 covariance applies for C <= 256)
+static WctLayout wct_layout(int n, int C, int64_t HW, bool src_f32) {
   WctLayout L{};
   L.n = n;
   L.C = C;
   L.HW = HW;
+  L.v2 = src_f32 && cov_v2_supported(C) && env_int("RPST_WCT_COV_V2", 1) != 0;
   L.BT = (C >= 128 && env_int("RPST_WCT_COV_BT", 128) == 128) ? 128 : 64;
   L.tiles = (C + L.BT - 1) / L.BT;
   L.symtiles = L.tiles * (L.tiles + 1) / 2;
@@ -793,16 +554,14 @@ static WctLayout wct_layout(int n, int C, int64_t HW) {
   size_t o = 0;
   L.mu_c = o; o += (size_t)n * C;
   L.mu_s = o; o += (size_t)n * C;
-  L.part = o; o += (size_t)2 * n * L.ksplit * C * C;
+  L.mu32 = o; o += ((size_t)2 * n * C + 1) / 2;  // fp32 centring means (v2 without `means`)
+  L.part = o; o += L.v2 ? cov_v2_work_doubles(n, C, HW) : (size_t)2 * n * L.ksplit * C * C;
   L.cc = o; o += cc;
   L.cs = o; o += cc;
-  L.sc = o; o += cc;
-  L.ic = o; o += cc;
-  L.m0 = o; o += cc;
-  L.mid = o; o += cc;
-  L.tmp = o; o += cc;
   L.tm = o; o += cc;
-  L.ns = o; o += ns_work_doubles(C, n);
+  L.off = o; o += (size_t)n * C;
+  L.tf = o; o += cc / 2 + (size_t)n * C + 2;  // fp32 transform operands (wct_run)
+  L.mf = o; o += matfun_wct_work_doubles(n, C);
   L.total = o;
   return L;
 }
@@ -815,106 +574,103 @@ __global__ void widen_means_kernel(const float* __restrict__ m, double* __restri
   if (i < count) out[i] = (double)m[i];
 }
 
-// c[b][m] = mu_s[b][m] - sum_k T[b][m][k] mu_c[b][k]  (fixed order, fp64): the constant of
-// T (x - mu_c) + mu_s = T x + c
-__global__ void wct_offset_kernel(const double* __restrict__ T, const double* __restrict__ mu_c,
-                                  const double* __restrict__ mu_s, double* __restrict__ c,
-                                  int n, int C) {
+__global__ void narrow_means_kernel(const double* __restrict__ m, float* __restrict__ out,
+                                    int64_t count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)n * C) return;
-  const int64_t b = i / C;
-  const double* t = T + i * C;  // row m of image b
-  const double* mc = mu_c + b * C;
-  double s = 0.0;
-  for (int k = 0; k < C; ++k) s = fma(t[k], mc[k], s);
-  c[i] = mu_s[i] - s;
+  if (i < count) out[i] = (float)m[i];
 }
 
-// WCT matrices of every image: means (mu_c, mu_s in the workspace), covariances, the
-// Newton-Schulz powers and T = Ic Mid Ic (wct_rp.py:85-109). SRC is SRC_F32C (fp32
-// features) or SRC_F64C (fp64). means: optional fp32 (2n x C) row means; residual (2n,
-// optional): final Newton-Schulz residuals of (Cc + 1e-4 I) and of Mid's argument.
+// WCT matrices of every image (wct_rp.py:85-109): fp64 means (mu_c, mu_s in the workspace),
+// covariances, then T = Ic Mid Ic and offset = mu_s - T mu_c from the persistent matfun
+// launch. SRC is SRC_F32C (fp32 features) or SRC_F64C (fp64). means: optional fp32 (2n x C)
+// row means (content rows then style rows), used to centre; residual (2n, optional): final
+// Newton-Schulz residuals of (Cc + 1e-4 I) and of Mid's argument. T / offset: n x C x C / n x C.
 template <int SRC>
 static int wct_matrices(const void* cF, const void* sF, const float* means, int n, int C,
-                        int64_t HW, const WctLayout& L, double* ws, double* residual,
-                        hipStream_t st) {
-  double *mu_c = ws + L.mu_c, *mu_s = ws + L.mu_s, *part = ws + L.part;
-  double *Cc = ws + L.cc, *Cs = ws + L.cs, *Sc = ws + L.sc, *Ic = ws + L.ic;
-  double *M0 = ws + L.m0, *Mid = ws + L.mid, *tmp = ws + L.tmp, *Tm = ws + L.tm;
-  double* nsw = ws + L.ns;
-
-  // 1. means (content rows then style rows; mu_s follows mu_c in the workspace)
-  if (means) {
-    const int64_t cnt = (int64_t)2 * n * C;
-    widen_means_kernel<<<(unsigned)((cnt + 255) / 256), 256, 0, st>>>(means, mu_c, cnt);
-    if (int e = launch_status("widen_means_kernel")) return e;
-  } else {
-    if (SRC == SRC_F32C)
+                        int64_t HW, const WctLayout& L, double* ws, double* T, double* offset,
+                        double* residual, hipStream_t st) {
+  double *mu_c = ws + L.mu_c, *part = ws + L.part;
+  double *Cc = ws + L.cc, *Cs = ws + L.cs;
+  const int64_t cnt = (int64_t)2 * n * C;
+  if (SRC == SRC_F32C && L.v2) {
+    // centre on fp32 means (given, or the fp64 row means rounded); cov_v2 recovers the exact
+    // fp64 means and covariances from the centred row sums
+    const float* mu32 = means;
+    if (!mu32) {
       rowmean_kernel<float><<<2 * n * C, 256, 0, st>>>(static_cast<const float*>(cF),
                                                       static_cast<const float*>(sF), n * C, HW, mu_c);
-    else
-      rowmean_kernel<double><<<2 * n * C, 256, 0, st>>>(static_cast<const double*>(cF),
-                                                       static_cast<const double*>(sF), n * C, HW, mu_c);
-    if (int e = launch_status("rowmean_kernel")) return e;
+      float* m32 = reinterpret_cast<float*>(ws + L.mu32);
+      narrow_means_kernel<<<(unsigned)((cnt + 255) / 256), 256, 0, st>>>(mu_c, m32, cnt);
+      if (int e = launch_status("rowmean_kernel")) return e;
+      mu32 = m32;
+    }
+    if (int e = cov_v2(static_cast<const float*>(cF), static_cast<const float*>(sF), mu32, n, C,
+                       HW, Cc, Cs, mu_c, part, st))
+      return e;
+  } else {
+    // 1. means (content rows then style rows; mu_s follows mu_c in the workspace)
+    if (means) {
+      widen_means_kernel<<<(unsigned)((cnt + 255) / 256), 256, 0, st>>>(means, mu_c, cnt);
+      if (int e = launch_status("widen_means_kernel")) return e;
+    } else {
+      if (SRC == SRC_F32C)
+        rowmean_kernel<float><<<2 * n * C, 256, 0, st>>>(static_cast<const float*>(cF),
+                                                        static_cast<const float*>(sF), n * C, HW, mu_c);
+      else
+        rowmean_kernel<double><<<2 * n * C, 256, 0, st>>>(static_cast<const double*>(cF),
+                                                         static_cast<const double*>(sF), n * C, HW, mu_c);
+      if (int e = launch_status("rowmean_kernel")) return e;
+    }
+    double* mu_s = ws + L.mu_s;
+    // 2. covariances: upper-triangular tiles, split-K partials, fixed-order reduce
+    for (int which = 0; which < 2; ++which) {
+      G64Args g{};
+      g.A = g.B = which == 0 ? cF : sF;
+      g.C = part + (size_t)which * n * L.ksplit * C * C;
+      g.amean = g.bmean = which == 0 ? mu_c : mu_s;
+      g.sMean = C;
+      g.M = g.N = C;
+      g.K = (int)HW;
+      g.lda = g.ldb = (int)HW;
+      g.ldc = C;
+      g.sA = g.sB = (int64_t)C * HW;
+      g.sC = (int64_t)C * C;
+      g.ksplit = L.ksplit;
+      g.sym = 1;
+      g.tiles_n = L.tiles;
+      dim3 grid(L.symtiles, 1, n * L.ksplit);
+      if (L.BT == 128)
+        gemm64<128, SRC, SRC, B_NK, OUT_PARTIAL>(g, grid, st);
+      else
+        gemm64<64, SRC, SRC, B_NK, OUT_PARTIAL>(g, grid, st);
+      if (int e = launch_status("gemm_f64_kernel(cov)")) return e;
+    }
+    const int64_t nel = (int64_t)n * C * C;
+    const unsigned rb = (unsigned)((nel + 255) / 256);
+    cov_reduce_kernel<<<rb, 256, 0, st>>>(part, Cc, C, L.ksplit, L.BT, 1.0 / (double)(HW - 1), 1.0, n);
+    cov_reduce_kernel<<<rb, 256, 0, st>>>(part + (size_t)n * L.ksplit * C * C, Cs, C, L.ksplit, L.BT,
+                                          1.0 / (double)(HW - 1), 0.0, n);
+    if (int e = launch_status("cov_reduce_kernel")) return e;
   }
-
-  // 2. covariances: upper-triangular tiles, split-K partials, fixed-order reduce
-  for (int which = 0; which < 2; ++which) {
-    G64Args g{};
-    g.A = g.B = which == 0 ? cF : sF;
-    g.C = part + (size_t)which * n * L.ksplit * C * C;
-    g.amean = g.bmean = which == 0 ? mu_c : mu_s;
-    g.sMean = C;
-    g.M = g.N = C;
-    g.K = (int)HW;
-    g.lda = g.ldb = (int)HW;
-    g.ldc = C;
-    g.sA = g.sB = (int64_t)C * HW;
-    g.sC = (int64_t)C * C;
-    g.ksplit = L.ksplit;
-    g.sym = 1;
-    g.tiles_n = L.tiles;
-    dim3 grid(L.symtiles, 1, n * L.ksplit);
-    if (L.BT == 128)
-      gemm64<128, SRC, SRC, B_NK, OUT_PARTIAL>(g, grid, st);
-    else
-      gemm64<64, SRC, SRC, B_NK, OUT_PARTIAL>(g, grid, st);
-    if (int e = launch_status("gemm_f64_kernel(cov)")) return e;
-  }
-  const int64_t nel = (int64_t)n * C * C;
-  const unsigned rb = (unsigned)((nel + 255) / 256);
-  cov_reduce_kernel<<<rb, 256, 0, st>>>(part, Cc, C, L.ksplit, L.BT, 1.0 / (double)(HW - 1), 1.0, n);
-  cov_reduce_kernel<<<rb, 256, 0, st>>>(part + (size_t)n * L.ksplit * C * C, Cs, C, L.ksplit, L.BT,
-                                        1.0 / (double)(HW - 1), 0.0, n);
-  if (int e = launch_status("cov_reduce_kernel")) return e;
-
-  // 3. Sc, Ic = (Cc + 1e-4 I)^(+-1/2)
-  if (int e = ns_power(Cc, 1e-4, Sc, Ic, C, n, nsw, st, residual)) return e;
-  // 4. Mid = (Sc Cs Sc + 1e-4 I)^(1/2)
-  small_gemm(Sc, Cs, tmp, C, n, 1.0, 0.0, nullptr, st);
-  small_gemm(tmp, Sc, M0, C, n, 1.0, 0.0, nullptr, st);
-  if (int e = ns_power(M0, 1e-4, Mid, nullptr, C, n, nsw, st, residual ? residual + n : nullptr))
-    return e;
-  // 5. T = Ic Mid Ic
-  small_gemm(Ic, Mid, tmp, C, n, 1.0, 0.0, nullptr, st);
-  small_gemm(tmp, Ic, Tm, C, n, 1.0, 0.0, nullptr, st);
-  return launch_status("wct matrix functions");
+  // 3. Sc, Ic = (Cc + 1e-4 I)^(+-1/2); Mid = (Sc Cs Sc + 1e-4 I)^(1/2); T = Ic Mid Ic;
+  //    offset = mu_s - T mu_c: one persistent launch
+  return matfun_wct(Cc, Cs, mu_c, T, offset, residual, n, C, ws + L.mf, st);
 }
 
 // Shared WCT body: the matrices, then out = T (cF - mu_c) + mu_s.
 template <int SRC, int OUTM>
 static int wct_run(const void* cF, const void* sF, void* out, int n, int C, int64_t HW,
                    void* workspace, double* residual, hipStream_t st) {
-  const WctLayout L = wct_layout(n, C, HW);
+  const WctLayout L = wct_layout(n, C, HW, SRC == SRC_F32C);
   double* ws = static_cast<double*>(workspace);
-  if (int e = wct_matrices<SRC>(cF, sF, nullptr, n, C, HW, L, ws, residual, st)) return e;
-  double *mu_c = ws + L.mu_c, *mu_s = ws + L.mu_s;
-  double *M0 = ws + L.m0, *Mid = ws + L.mid, *Tm = ws + L.tm;
+  double *mu_c = ws + L.mu_c, *mu_s = ws + L.mu_s, *Tm = ws + L.tm;
+  if (int e = wct_matrices<SRC>(cF, sF, nullptr, n, C, HW, L, ws, Tm, ws + L.off, residual, st))
+    return e;
 
-  // 6. out = T (cF - mu_c) + mu_s; fp32 features -> fp32 MFMA (RPST_WCT_T_F64=1: fp64)
+  // out = T (cF - mu_c) + mu_s; fp32 features -> fp32 MFMA (RPST_WCT_T_F64=1: fp64)
   if (SRC == SRC_F32C && OUTM == OUT_F32_BIAS && !env_int("RPST_WCT_T_F64", 0)) {
-    float* Tf = reinterpret_cast<float*>(M0);  // M0 / Mid are free after step 5
-    float* muf = reinterpret_cast<float*>(Mid);
+    float* Tf = reinterpret_cast<float*>(ws + L.tf);
+    float* muf = Tf + (size_t)n * C * C;
     const int64_t nT = (int64_t)n * C * C, nmu = (int64_t)2 * n * C;  // mu_c, mu_s adjacent
     wct_f32_prep_kernel<<<(unsigned)((std::max(nT, nmu) + 255) / 256), 256, 0, st>>>(Tm, mu_c, Tf, muf, nT, nmu, C);
     if (int e = launch_status("wct_f32_prep_kernel")) return e;
@@ -954,7 +710,9 @@ using namespace rpst;
 
 extern "C" size_t rpst_wct_workspace_size(int n, int C, int64_t HW) {
   if (n <= 0 || C <= 0 || HW <= 1) return 0;
-  return wct_layout(n, C, HW).total * sizeof(double);
+  // the larger of the fp32-feature and fp64-feature layouts (one size for every entry point)
+  const size_t a = wct_layout(n, C, HW, true).total, b = wct_layout(n, C, HW, false).total;
+  return (a > b ? a : b) * sizeof(double);
 }
 
 extern "C" int rpst_wct_fuse(const float* content, const float* style, float* out, int n, int C,
@@ -962,7 +720,7 @@ extern "C" int rpst_wct_fuse(const float* content, const float* style, float* ou
                              size_t workspace_bytes, rpst_stream_t stream) {
   RPST_REQUIRE(content && style && out, "wct_fuse: null pointer");
   RPST_REQUIRE(n > 0 && C > 0 && HW > 1, "wct_fuse: bad shape n=%d C=%d HW=%lld", n, C, (long long)HW);
-  RPST_REQUIRE(HW <= 0x7fffffffLL && n <= 65535, "wct_fuse: shape too large");
+  RPST_REQUIRE(HW <= 0x7fffffffLL && n <= 32767 && C <= 1024, "wct_fuse: shape too large");
   if (!workspace || workspace_bytes < rpst_wct_workspace_size(n, C, HW)) {
     set_error("wct_fuse: workspace %zu < %zu bytes", workspace_bytes, rpst_wct_workspace_size(n, C, HW));
     return RPST_EWORKSPACE;
@@ -984,23 +742,18 @@ extern "C" int rpst_wct_params(const float* content, const float* style, const f
               rpst_wct_workspace_size(n, C, HW));
     return RPST_EWORKSPACE;
   }
+  RPST_REQUIRE(C <= 1024, "wct_params: C=%d > 1024", C);
   hipStream_t st = as_stream(stream);
-  const WctLayout L = wct_layout(n, C, HW);
-  double* ws = static_cast<double*>(workspace);
-  if (int e = wct_matrices<SRC_F32C>(content, style, means, n, C, HW, L, ws, residual, st)) return e;
-  RPST_REQUIRE(hipMemcpyAsync(T, ws + L.tm, sizeof(double) * n * C * C, hipMemcpyDeviceToDevice,
-                              st) == hipSuccess, "wct_params: copy of T failed");
-  const int64_t nc = (int64_t)n * C;
-  wct_offset_kernel<<<(unsigned)((nc + 255) / 256), 256, 0, st>>>(ws + L.tm, ws + L.mu_c,
-                                                                  ws + L.mu_s, offset, n, C);
-  return launch_status("wct_offset_kernel");
+  const WctLayout L = wct_layout(n, C, HW, true);
+  return wct_matrices<SRC_F32C>(content, style, means, n, C, HW, L, static_cast<double*>(workspace),
+                                T, offset, residual, st);
 }
 
 extern "C" int rpst_whiten_and_color_f64(const double* cF, const double* sF, double* out, int C,
                                          int64_t HW, double* residual, void* workspace,
                                          size_t workspace_bytes, rpst_stream_t stream) {
   RPST_REQUIRE(cF && sF && out, "whiten_and_color: null pointer");
-  RPST_REQUIRE(C > 0 && HW > 1 && HW <= 0x7fffffffLL, "whiten_and_color: bad shape");
+  RPST_REQUIRE(C > 0 && C <= 1024 && HW > 1 && HW <= 0x7fffffffLL, "whiten_and_color: bad shape");
   if (!workspace || workspace_bytes < rpst_wct_workspace_size(1, C, HW)) {
     set_error("whiten_and_color: workspace too small");
     return RPST_EWORKSPACE;
@@ -1011,20 +764,18 @@ extern "C" int rpst_whiten_and_color_f64(const double* cF, const double* sF, dou
 
 extern "C" size_t rpst_matrix_power_workspace_size(int n, int batch) {
   if (n <= 0 || batch <= 0) return 0;
-  return ns_work_doubles(n, batch) * sizeof(double);
+  return matfun_power_work_doubles(n, batch) * sizeof(double);
 }
 
 extern "C" int rpst_matrix_power_psd_f64(const double* A, double* out, int n, int batch,
                                          int inverse, double* residual, void* workspace,
                                          size_t workspace_bytes, rpst_stream_t stream) {
   RPST_REQUIRE(A && out, "matrix_power: null pointer");
-  RPST_REQUIRE(n > 0 && batch > 0 && batch <= 65535, "matrix_power: bad shape");
+  RPST_REQUIRE(n > 0 && n <= 1024 && batch > 0 && batch <= 65535, "matrix_power: bad shape");
   if (!workspace || workspace_bytes < rpst_matrix_power_workspace_size(n, batch)) {
     set_error("matrix_power: workspace too small");
     return RPST_EWORKSPACE;
   }
-  hipStream_t st = as_stream(stream);
-  double* w = static_cast<double*>(workspace);
-  if (inverse) return ns_power(A, 1e-4, nullptr, out, n, batch, w, st, residual);
-  return ns_power(A, 1e-4, out, nullptr, n, batch, w, st, residual);
+  return matfun_power(A, out, n, batch, inverse, residual, static_cast<double*>(workspace),
+                      as_stream(stream));
 }

@@ -38,17 +38,18 @@ def wct_rp_fused(encoder, decoder, content, style):
                               torch.cat([content, style], dim=0), stats_last=True)
     T, c, res = ops.wct_params(feats[:n], feats[n:], means=mean.reshape(2 * n, -1))
     out = plan.run(plan.compile_layers(decoder.children()), feats[:n], first_mix=(T, c))
-    ops.check_ns_residual(res, "WCTRPNet.test")  # after every launch is queued
+    # res: the Newton-Schulz residuals (2n), on the device; no host sync here: an image whose
+    # iteration did not converge (non-finite features) has NaN T and c, so its output is NaN
     return out
 
 
 def matrix_inv_sqrt(A):
-    """(A + 1e-4 I)^(-1/2) for symmetric PSD A (wct_rp.py:7-22), fp64 on the GPU."""
+    """V diag(s^-1/2) V^T of svd(A + 1e-4 I), s >= 1e-5 (wct_rp.py:7-22), fp64 on the GPU."""
     return ops.matrix_power_psd(A, -0.5)
 
 
 def matrix_sqrt(A):
-    """(A + 1e-4 I)^(1/2) for symmetric PSD A (wct_rp.py:24-40), fp64 on the GPU."""
+    """V diag(s^1/2) V^T of svd(A + 1e-4 I), s >= 1e-5 (wct_rp.py:24-40), fp64 on the GPU."""
     return ops.matrix_power_psd(A, 0.5)
 
 

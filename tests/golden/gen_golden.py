@@ -216,6 +216,44 @@ def gen_wct_large(net):
     np.savez_compressed(os.path.join(HERE, "wct_large.npz"), ncase=len(cases), **out)
 
 
+def wct_edge_inputs():
+    """Inputs of gen_wct_edge (regenerated by the tests): the matrix functions on inputs the
+    Newton-Schulz path must hand to the SVD form, and whiten_and_color at C = 512 with a dead
+    style channel and a style covariance reaching ~1e4 (the fixed 1e-10 residual
+    bar failed such valid inputs)."""
+    from rpst import synth
+    mats = {}
+    q = np.linalg.qr(2.0 * synth.uniform01(71, "edge_q", 24 * 24).reshape(24, 24) - 1.0)[0]
+    ev = np.linspace(-3.0, 5.0, 24)  # indefinite symmetric
+    mats["indef"] = q @ np.diag(ev) @ q.T
+    q2 = np.linalg.qr(2.0 * synth.uniform01(72, "edge_q", 20 * 20).reshape(20, 20) - 1.0)[0]
+    ev2 = np.concatenate([[-1e-4 + 4e-6, -1e-4 + 2e-6], np.linspace(0.05, 2.0, 18)])
+    mats["trunc"] = q2 @ np.diag(ev2) @ q2.T  # A + 1e-4 I has two singular values < 1e-5
+    mats["nonsym"] = 2.0 * synth.uniform01(73, "edge_ns", 16 * 16).reshape(16, 16) - 1.0 + 3.0 * np.eye(16)
+    cdim, hw = 512, 1536
+    cf = synth.conditioned_features(950, cdim, hw, 1.5) * 4.0
+    sf = synth.conditioned_features(951, cdim, hw, 3.0) * 80.0
+    sf[7] = 0.0  # dead style channel: singular style covariance
+    ph = 2.0 * synth.uniform01(950, "hwprobe", hw * 4).reshape(hw, 4) - 1.0
+    return mats, cf, sf, ph
+
+
+def gen_wct_edge(net):
+    from network.wct_rp import matrix_inv_sqrt, matrix_sqrt
+    mats, cf, sf, ph = wct_edge_inputs()
+    out = {}
+    for k, a in mats.items():
+        out[f"sqrt_{k}"] = matrix_sqrt(t(a)).numpy()
+        out[f"isqrt_{k}"] = matrix_inv_sqrt(t(a)).numpy()
+    m = net.WCTRPNet(rp_config(2), copy.deepcopy(net.vgg))
+    wc = m.whiten_and_color(t(cf), t(sf)).numpy()
+    sm = sf - sf.mean(1, keepdims=True)
+    out["style_cov_max_eig"] = np.linalg.eigvalsh(sm @ sm.T / (sf.shape[1] - 1)).max()
+    out["wcP"] = wc @ ph
+    out["wcCols"] = wc[:, :32].copy()
+    np.savez_compressed(os.path.join(HERE, "wct_edge.npz"), **out)
+
+
 def gen_sanet(net):
     from network.sanet import SANet, Transform, mean_variance_norm
     out = {}
@@ -580,7 +618,7 @@ GENERATORS = {"keys": gen_keys, "stats": gen_stats, "adain_rp": gen_adain_rp,
               "adaptive": gen_adaptive, "deeper": gen_deeper, "grads": gen_grads,
               "grads_wct": gen_grads_wct, "wct_large": gen_wct_large,
               "grads_sam": gen_grads_sam, "grads_src": gen_grads_src,
-              "grads_ms": gen_grads_ms}
+              "grads_ms": gen_grads_ms, "wct_edge": gen_wct_edge}
 
 
 def main():

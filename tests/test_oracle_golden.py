@@ -120,6 +120,24 @@ def test_wct_large_reference(golden):
         assert rel_l2(wc[:, :32], g[f"wcCols{i}"]) < 1e-11, i
 
 
+def test_wct_edge_reference(golden):
+    """The oracle's SVD form on the inputs the kernels route to the Jacobi SVD (indefinite,
+    truncated, non-symmetric) and whiten_and_color at C = 512 with a dead style channel,
+    against the reference (gen_golden.gen_wct_edge)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from gen_golden import wct_edge_inputs
+    mats, cf, sf, ph = wct_edge_inputs()
+    g = golden("wct_edge")
+    for k, a in mats.items():
+        assert rel_l2(R.matrix_sqrt(t(a)), g[f"sqrt_{k}"]) < 1e-12, k
+        assert rel_l2(R.matrix_inv_sqrt(t(a)), g[f"isqrt_{k}"]) < 1e-12, k
+    wc = R.whiten_and_color(t(cf), t(sf)).numpy()
+    assert rel_l2(wc @ ph, g["wcP"]) < 1e-11 and rel_l2(wc[:, :32], g["wcCols"]) < 1e-11
+    assert 5e3 < float(g["style_cov_max_eig"]) < 2e4
+
+
 def test_wct_rp_test(golden):
     import network as net
     g = golden("wct")
