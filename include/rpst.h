@@ -306,6 +306,40 @@ int rpst_mean_variance_norm_backward(const float* y, const float* dy, const floa
 int rpst_softmax_rows(const float* S, float* P, int64_t rows, int cols, rpst_stream_t stream);
 int rpst_softmax_rows_backward(const float* P, const float* dP, float* dS, int64_t rows,
                                int cols, rpst_stream_t stream);
+/* SANet attention backward (sanet.py:86-94 under autograd; the rocBLAS batched GEMMs of
+ * round 2 replaced): for F (B,C,HWc), G, H (B,C,HWs) and dO (B,C,HWc), with S = F^T G and
+ * P = softmax_rows(S): dH = dO P, dP = dO^T H, dS = P (dP - rowsum(dP P)), dF = G dS^T,
+ * dG = F dS. P is formed from S while staged, never stored. Workspace:
+ * rpst_sanet_attention_backward_workspace_size(B, HWc, HWs) (S and dP). */
+size_t rpst_sanet_attention_backward_workspace_size(int B, int HWc, int HWs);
+int rpst_sanet_attention_backward(const float* F, const float* G, const float* H,
+                                  const float* dO, float* dF, float* dG, float* dH, int B, int C,
+                                  int HWc, int HWs, void* workspace, size_t workspace_bytes,
+                                  rpst_stream_t stream);
+/* AdaptiveSANet attention backward (sanet.py:100-138 under autograd; AdaptiveSAModel trains
+ * through it, train.py:118-119): with A the cosine affinity of content / style, c the f_psi
+ * clamp, S = F^T G, P = softmax_rows(S) and Q = AEA(P) (mode 0 aea: sigmoid(scale (P - c)),
+ * mode 1 relu: softmax_rows(relu(P - c))), O = H Q^T: from dO (B,C,HW) -> dF, dG, dH (B,C,HW)
+ * and the f_psi gradients dw1 (hidden,HW), db1 (hidden), dw2 (hidden), db2 (1). Q and P are
+ * formed from S where staged, never stored. Workspace:
+ * rpst_adaptive_attention_backward_workspace_size(B, C, HW, hidden). */
+size_t rpst_adaptive_attention_backward_workspace_size(int B, int C, int HW, int hidden);
+int rpst_adaptive_attention_backward(const float* F, const float* G, const float* H,
+                                     const float* content, const float* style, const float* w1,
+                                     const float* b1, const float* w2, const float* b2,
+                                     int hidden, int mode, float scale, float from,
+                                     float interval, const float* dO, float* dF, float* dG,
+                                     float* dH, float* dw1, float* db1, float* dw2, float* db2,
+                                     int B, int C, int HW, void* workspace,
+                                     size_t workspace_bytes, rpst_stream_t stream);
+/* 1x1 conv weight / bias gradient over a batch (sanet.py:76-80, 97 f / g / h / out_conv):
+ * dw (Cout,Cin) = sum_n dy_n x_n^T, db (Cout, may be NULL) = sum over n and pixels of dy.
+ * Per-image products then a fixed-order batch sum. Workspace:
+ * rpst_conv1x1_wgrad_workspace_size(N, Cin, Cout). */
+size_t rpst_conv1x1_wgrad_workspace_size(int N, int Cin, int Cout);
+int rpst_conv1x1_wgrad(const float* x, const float* dy, float* dw, float* db, int N, int Cin,
+                       int64_t HW, int Cout, void* workspace, size_t workspace_bytes,
+                       rpst_stream_t stream);
 /* *out = scale * sum (a - b)^2 over n elements (fp64 accumulation, fixed order).
  * Workspace: rpst_sq_diff_workspace_size(). */
 size_t rpst_sq_diff_workspace_size(void);

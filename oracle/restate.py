@@ -380,11 +380,14 @@ def samodel_test(content: Tensor, style: Tensor, sd: SD) -> Tensor:
         return decoder(fusion, sd, "decoder.")
 
 
-def samodel_losses(content, style, sd, cfg):
+def samodel_losses(content, style, sd, cfg, transform_fn=None):
     """SAModel.forward (sanet.py:248-275): the loss dict, differentiable w.r.t. the entries
     of sd (the CPU gradient oracle of the SAModel training step). cfg: content_weight,
-    style_weight, l_identity1_weight, l_identity2_weight."""
+    style_weight, l_identity1_weight, l_identity2_weight. transform_fn(c4, s4, c5, s5, sd,
+    prefix) replaces the SANet Transform (AdaptiveSAModel.forward, sanet.py:347-382, has the
+    same losses around its AdaptiveTransform)."""
     mse = F.mse_loss
+    transform = transform_fn or globals()["transform"]
     sfeat = encode_with_intermediate(style, sd, 5)
     cfeat = encode_with_intermediate(content, sd, 5)
     stylized = transform(cfeat[3], sfeat[3], cfeat[4], sfeat[4], sd, "transform.")
@@ -410,13 +413,13 @@ def samodel_losses(content, style, sd, cfg):
             "l_identity2_loss": l2, "total_loss": tot}
 
 
-def samodel_grads(content, style, sd, cfg):
+def samodel_grads(content, style, sd, cfg, transform_fn=None):
     """(loss dict, {name: d total_loss / d param}) for the transform and decoder (the
     encoder is frozen, sanet.py:213-216)."""
     sd = {k: (v.detach().clone().requires_grad_(k.startswith(("transform.", "decoder.")))
               if v.is_floating_point() else v) for k, v in sd.items()}
     with torch.enable_grad():
-        losses = samodel_losses(content, style, sd, cfg)
+        losses = samodel_losses(content, style, sd, cfg, transform_fn)
         names = [k for k, v in sd.items() if v.requires_grad]
         grads = torch.autograd.grad(losses["total_loss"], [sd[k] for k in names])
     return ({k: v.detach() for k, v in losses.items()}, dict(zip(names, grads)))
@@ -476,6 +479,15 @@ def adaptive_samodel_test(content: Tensor, style: Tensor, sd: SD, mode: str) -> 
         fusion = adaptive_transform(cfeat[3], sfeat[3], cfeat[4], sfeat[4], sd, "transform.",
                                     mode)
         return decoder(fusion, sd, "decoder.")
+
+
+def adaptive_samodel_grads(content, style, sd, cfg, mode: str):
+    """AdaptiveSAModel.forward + backward (sanet.py:347-382; train.py:118-119 trains it):
+    the loss dict and d total_loss / d every transform (incl. the AEA f_psi) and decoder
+    parameter."""
+    fn = lambda c4, s4, c5, s5, sd_, prefix: adaptive_transform(  # noqa: E731
+        c4, s4, c5, s5, sd_, prefix, mode)
+    return samodel_grads(content, style, sd, cfg, fn)
 
 
 # ---- f4: host I/O pixel paths (test.py:49-54, 139-149) ---------------------------------

@@ -32,7 +32,14 @@ constexpr int kGBN = 128, kGBK = 32, kGPad = 4;  // M tile: 128 * MW (gemm_f32_k
 //   BX_AEA    sigmoid(scale (exp(v - m_r) inv_r - c_r))     AEAModule clamp (sanet.py:45-47)
 //   BX_AEAR   exp(relu(exp(v - m_r) inv_r - c_r) - m2_r)    AEALReluModule (sanet.py:66-69),
 //             numerator of softmax(relu(P - c)); 1/l2_r is the epilogue column scale
-enum { BX_NONE = 0, BX_EXP = 1, BX_AEA = 2, BX_AEAR = 3 };
+//   BX_PROB   exp(v - m_r) inv_r                            softmax probability (attention
+//             backward: dH = dO P with P formed while S is staged, never stored)
+//   BX_AEARQ  BX_AEAR * inv2_r                              the normalised AEALRelu attention
+//             (AdaptiveSANet backward: dH = dO Q)
+enum { BX_NONE = 0, BX_EXP = 1, BX_AEA = 2, BX_AEAR = 3, BX_PROB = 4, BX_AEARQ = 5 };
+template <int BX> constexpr bool bx_inv() { return BX == BX_AEA || BX == BX_AEAR || BX == BX_PROB || BX == BX_AEARQ; }
+template <int BX> constexpr bool bx_clamp() { return BX == BX_AEA || BX == BX_AEAR || BX == BX_AEARQ; }
+template <int BX> constexpr bool bx_m2() { return BX == BX_AEAR || BX == BX_AEARQ; }
 
 // Per-row vectors of the B operand's transform (each indexed batch * sV + r).
 struct RowVec {
@@ -41,6 +48,7 @@ struct RowVec {
   const float* clamp;  // AEA threshold per query row
   const float* m2;     // BX_AEAR: row max of relu(P - c)
   float scale;         // BX_AEA: sigmoid slope (scale_value)
+  const float* inv2;   // BX_AEARQ: 1 / sum exp(relu(P - c) - m2)
 };
 
 struct GemmArgs {
@@ -57,7 +65,7 @@ struct GemmArgs {
 
 template <int BX>
 __device__ __forceinline__ float bx_apply(float v, float m, float inv, float c, float m2,
-                                          float scale) {
+                                          float scale, float inv2 = 1.f) {
   if (BX == BX_EXP) return expf(v - m);
   if (BX == BX_AEA) {
     const float p = expf(v - m) * inv;
@@ -66,6 +74,11 @@ __device__ __forceinline__ float bx_apply(float v, float m, float inv, float c, 
   if (BX == BX_AEAR) {
     const float p = expf(v - m) * inv;
     return expf(fmaxf(p - c, 0.f) - m2);
+  }
+  if (BX == BX_PROB) return expf(v - m) * inv;
+  if (BX == BX_AEARQ) {
+    const float p = expf(v - m) * inv;
+    return expf(fmaxf(p - c, 0.f) - m2) * inv2;
   }
   return v;
 }
@@ -93,6 +106,19 @@ __device__ __forceinline__ void g_load(float (&reg)[16], const float* __restrict
         for (int e = 0; e < 4; ++e)
           reg[4 * p + e] = (k < K && r + e < R) ? X[(int64_t)k * ld + r + e] : 0.f;
       }
+      if (BX != BX_NONE) {  // KR staging: the row of S (the query) is the k index
+        const int64_t q = voff + (k < K ? k : 0);
+        const float mx = rv.m[q];
+        const float inv = bx_inv<BX>() ? rv.inv[q] : 0.f;
+        const float cl = bx_clamp<BX>() ? rv.clamp[q] : 0.f;
+        const float m2 = bx_m2<BX>() ? rv.m2[q] : 0.f;
+        const float i2 = BX == BX_AEARQ ? rv.inv2[q] : 1.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          reg[4 * p + e] = (k < K && r + e < R)
+                               ? bx_apply<BX>(reg[4 * p + e], mx, inv, cl, m2, rv.scale, i2)
+                               : 0.f;
+      }
     }
   } else {
     // thread -> (r = tid>>3 + 32p, k4 = (tid&7)*4), 4 passes of 32 rows
@@ -116,12 +142,13 @@ __device__ __forceinline__ void g_load(float (&reg)[16], const float* __restrict
       if (BX != BX_NONE) {
         const int64_t q = voff + (r < R ? r : 0);
         const float mx = rv.m[q];
-        const float inv = BX >= BX_AEA ? rv.inv[q] : 0.f;
-        const float cl = BX >= BX_AEA ? rv.clamp[q] : 0.f;
-        const float m2 = BX == BX_AEAR ? rv.m2[q] : 0.f;
+        const float inv = bx_inv<BX>() ? rv.inv[q] : 0.f;
+        const float cl = bx_clamp<BX>() ? rv.clamp[q] : 0.f;
+        const float m2 = bx_m2<BX>() ? rv.m2[q] : 0.f;
+        const float i2 = BX == BX_AEARQ ? rv.inv2[q] : 1.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          v[e] = (r < R && k + e < K) ? bx_apply<BX>(v[e], mx, inv, cl, m2, rv.scale) : 0.f;
+          v[e] = (r < R && k + e < K) ? bx_apply<BX>(v[e], mx, inv, cl, m2, rv.scale, i2) : 0.f;
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) reg[4 * p + e] = v[e];
@@ -295,6 +322,168 @@ static void launch_gemm(const GemmArgs& g, int batch, hipStream_t st) {
   }
 }
 
+
+// ---- SANet attention backward (sanet.py:86-94 under autograd) ---------------------------
+// dS = P (dP - rowsum(dP P)) with P = exp(S - m) inv formed from the logits (P is never
+// stored); in place over dP. One wave per row, fixed-order sums. rowsum(dP P) is divided by
+// the row's own sum of P (1 up to fp32 rounding), so each row of dS sums to zero to fp32
+// rounding: the softmax's shift invariance (the SANet g.bias gradient is exactly zero in exact
+// arithmetic) survives the recomputed P.
+__global__ __launch_bounds__(256) void softmax_bwd_logits_kernel(const float* __restrict__ S,
+                                                                 const float* __restrict__ rmax,
+                                                                 const float* __restrict__ rinv,
+                                                                 float* __restrict__ dP,
+                                                                 int64_t rows, int L) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* s = S + row * L;
+  float* d = dP + row * L;
+  const float m = rmax[row], inv = rinv[row];
+  float dot = 0.f, psum = 0.f;
+  for (int i = lane; i < L; i += 64) {
+    const float p = expf(s[i] - m) * inv;
+    dot = fmaf(d[i], p, dot);
+    psum += p;
+  }
+  dot = wave_sum(dot) / wave_sum(psum);
+  for (int i = lane; i < L; i += 64) d[i] = expf(s[i] - m) * inv * (d[i] - dot);
+}
+
+// out[i] = sum_b in[b][i] (fixed order over b)
+__global__ void batch_sum_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                 int64_t per, int nb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= per) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += in[(int64_t)b * per + i];
+  out[i] = s;
+}
+
+// db[c] = sum_{b, p} dy[b][c][p]: one wave per channel, fixed order
+__global__ __launch_bounds__(256) void channel_sum_kernel(const float* __restrict__ dy,
+                                                          float* __restrict__ db, int nb, int C,
+                                                          int64_t HW) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) {
+    const float* p = dy + ((int64_t)b * C + c) * HW;
+    for (int64_t i = lane; i < HW; i += 64) s += p[i];
+  }
+  s = wave_sum(s);
+  if (lane == 0) db[c] = s;
+}
+
+// ---- AdaptiveSANet backward (sanet.py:100-138 under autograd; train.py:118-119 trains it) --
+// Row pass from dQ (the gradient at the clamped attention) to dS (the gradient at the logits,
+// in place over dQ) and dc (at the per-query clamp value):
+//   aea  Q = sigmoid(scale (P - c)):      dP = dQ scale Q (1 - Q)
+//   relu Q = softmax(relu(P - c)):        dR = Q (dQ - rowsum(dQ Q)), dP = dR [P > c]
+//   dc = -sum_j dP, dS = P (dP - rowsum(dP P))   (P = softmax(S), from the logits)
+// One wave per row; the row sums are divided by the row's own sum of P / Q (1 to rounding) as
+// in softmax_bwd_logits_kernel.
+__global__ __launch_bounds__(256) void aea_bwd_rows_kernel(const float* __restrict__ S,
+                                                           RowVec rv, float* __restrict__ dQ,
+                                                           float* __restrict__ dc, int mode,
+                                                           int64_t rows, int L) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* s = S + row * L;
+  float* d = dQ + row * L;
+  const float m = rv.m[row], inv = rv.inv[row], c = rv.clamp[row], scale = rv.scale;
+  const float m2 = mode == 1 ? rv.m2[row] : 0.f, i2 = mode == 1 ? rv.inv2[row] : 0.f;
+  float dq_dot = 0.f;  // relu: rowsum(dQ Q) / rowsum(Q)
+  if (mode == 1) {
+    float dot = 0.f, qs = 0.f;
+    for (int i = lane; i < L; i += 64) {
+      const float p = expf(s[i] - m) * inv;
+      const float q = expf(fmaxf(p - c, 0.f) - m2) * i2;
+      dot = fmaf(d[i], q, dot);
+      qs += q;
+    }
+    dq_dot = wave_sum(dot) / wave_sum(qs);
+  }
+  auto dp_of = [&](float p, float g) {
+    if (mode == 0) {
+      const float q = 1.f / (1.f + expf(-(scale * (p - c))));
+      return g * scale * q * (1.f - q);
+    }
+    const float q = expf(fmaxf(p - c, 0.f) - m2) * i2;
+    return p - c > 0.f ? q * (g - dq_dot) : 0.f;
+  };
+  float dot = 0.f, ps = 0.f, dcs = 0.f;
+  for (int i = lane; i < L; i += 64) {
+    const float p = expf(s[i] - m) * inv;
+    const float dp = dp_of(p, d[i]);
+    dot = fmaf(dp, p, dot);
+    ps += p;
+    dcs += dp;
+  }
+  dot = wave_sum(dot) / wave_sum(ps);
+  dcs = wave_sum(dcs);
+  for (int i = lane; i < L; i += 64) {
+    const float p = expf(s[i] - m) * inv;
+    d[i] = p * (dp_of(p, d[i]) - dot);
+  }
+  if (lane == 0) dc[row] = -dcs;
+}
+
+// f_psi backward, per query row k (= b * HW + i): t = Z_k . w2 + b2 recomputed in the order
+// clamp_head_kernel used; dt = dc * head'(t) (aea: interval sigmoid'(t), relu: (1 - tanh^2)/2);
+// du[k][n] = dt w2[n] LeakyReLU'(Z[k][n]) (Z = LeakyReLU(u): u > 0 iff Z > 0). One wave per row.
+__global__ __launch_bounds__(256) void fpsi_bwd_rows_kernel(const float* __restrict__ Z,
+                                                            const float* __restrict__ w2,
+                                                            const float* __restrict__ b2,
+                                                            const float* __restrict__ dc,
+                                                            float* __restrict__ dt,
+                                                            float* __restrict__ du, int64_t rows,
+                                                            int hid, int mode, float interval) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* z = Z + row * hid;
+  float acc = 0.f;
+  for (int n = lane; n < hid; n += 64) acc = fmaf(z[n], w2[n], acc);
+  acc = wave_sum(acc);
+  const float t = acc + b2[0];
+  float g;
+  if (mode == 0) {
+    const float sg = 1.f / (1.f + expf(-t));
+    g = dc[row] * interval * sg * (1.f - sg);
+  } else {
+    const float th = tanhf(t);
+    g = dc[row] * 0.5f * (1.f - th * th);
+  }
+  float* u = du + row * hid;
+  for (int n = lane; n < hid; n += 64) u[n] = g * w2[n] * (z[n] > 0.f ? 1.f : 0.2f);
+  if (lane == 0) dt[row] = g;
+}
+
+// dw2[n] = sum_k dt[k] Z[k][n], db1[n] = sum_k du[k][n] (thread per n, fixed order over k);
+// db2 = sum_k dt[k] (thread n == hid)
+__global__ void fpsi_colsum_kernel(const float* __restrict__ Z, const float* __restrict__ du,
+                                   const float* __restrict__ dt, float* __restrict__ dw2,
+                                   float* __restrict__ db1, float* __restrict__ db2, int64_t rows,
+                                   int hid) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n > hid) return;
+  if (n == hid) {
+    float s = 0.f;
+    for (int64_t k = 0; k < rows; ++k) s += dt[k];
+    db2[0] = s;
+    return;
+  }
+  float a = 0.f, b = 0.f;
+  for (int64_t k = 0; k < rows; ++k) {
+    a = fmaf(dt[k], Z[k * hid + n], a);
+    b += du[k * hid + n];
+  }
+  dw2[n] = a;
+  db1[n] = b;
+}
 
 // ---- AdaptiveSANet (sanet.py:12-18, 26-71, 100-138) -----------------------------------
 // functional.normalize(x, dim=1): x / max(||x||_2 over channels, 1e-12), per position.
@@ -621,4 +810,177 @@ extern "C" int rpst_adaptive_attention(const float* F, const float* G, const flo
     launch_gemm<LAY_RK, LAY_RK, BX_AEAR>(g2, B, st);
   }
   return launch_status("gemm_f32_kernel(O=H Q^T)");
+}
+
+extern "C" size_t rpst_sanet_attention_backward_workspace_size(int B, int HWc, int HWs) {
+  if (B <= 0 || HWc <= 0 || HWs <= 0) return 0;
+  return sizeof(float) * (2 * (size_t)B * HWc * HWs + 2 * (size_t)B * HWc);
+}
+
+extern "C" int rpst_sanet_attention_backward(const float* F, const float* G, const float* H,
+                                             const float* dO, float* dF, float* dG, float* dH,
+                                             int B, int C, int HWc, int HWs, void* workspace,
+                                             size_t workspace_bytes, rpst_stream_t stream) {
+  RPST_REQUIRE(F && G && H && dO && dF && dG && dH, "sanet_attention_backward: null pointer");
+  RPST_REQUIRE(B > 0 && C > 0 && HWc > 0 && HWs > 0 && B <= 65535,
+               "sanet_attention_backward: bad shape B=%d C=%d HW=%d/%d", B, C, HWc, HWs);
+  if (!workspace ||
+      workspace_bytes < rpst_sanet_attention_backward_workspace_size(B, HWc, HWs)) {
+    set_error("sanet_attention_backward: workspace too small");
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  const int64_t ss = (int64_t)HWc * HWs, fc = (int64_t)C * HWc, fs = (int64_t)C * HWs;
+  float* S = static_cast<float*>(workspace);
+  float* dP = S + (size_t)B * ss;
+  float* rmax = dP + (size_t)B * ss;
+  float* rinv = rmax + (size_t)B * HWc;
+  // S = F^T G; row statistics of the softmax
+  GemmArgs g1{F, G, S, {}, nullptr, nullptr, 0, HWc, HWs, C, HWc, HWs, HWs, fc, fs, ss, 0};
+  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(g1, B, st);
+  if (int e = launch_status("gemm_f32_kernel(S=F^T G)")) return e;
+  const int64_t rows = (int64_t)B * HWc;
+  rowstats_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rmax, rinv, rows, HWs);
+  if (int e = launch_status("rowstats_kernel")) return e;
+  // dH = dO P: P formed from S while staged (KR: the row of P is the k index)
+  GemmArgs gh{dO, S, dH, {rmax, rinv, nullptr, nullptr, 0.f}, nullptr, nullptr, 0,
+              C, HWs, HWc, HWc, HWs, HWs, fc, ss, fs, HWc};
+  launch_gemm<LAY_RK, LAY_KR, BX_PROB>(gh, B, st);
+  if (int e = launch_status("gemm_f32_kernel(dH=dO P)")) return e;
+  // dP = dO^T H, then dS = P (dP - rowsum(dP P)) in place
+  GemmArgs gp{dO, H, dP, {}, nullptr, nullptr, 0, HWc, HWs, C, HWc, HWs, HWs, fc, fs, ss, 0};
+  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gp, B, st);
+  if (int e = launch_status("gemm_f32_kernel(dP=dO^T H)")) return e;
+  softmax_bwd_logits_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rmax, rinv, dP, rows,
+                                                                        HWs);
+  if (int e = launch_status("softmax_bwd_logits_kernel")) return e;
+  // dF = G dS^T, dG = F dS
+  GemmArgs gf{G, dP, dF, {}, nullptr, nullptr, 0, C, HWc, HWs, HWs, HWs, HWc, fs, ss, fc, 0};
+  launch_gemm<LAY_RK, LAY_RK, BX_NONE>(gf, B, st);
+  if (int e = launch_status("gemm_f32_kernel(dF=G dS^T)")) return e;
+  GemmArgs gg{F, dP, dG, {}, nullptr, nullptr, 0, C, HWs, HWc, HWc, HWs, HWs, fc, ss, fs, 0};
+  launch_gemm<LAY_RK, LAY_KR, BX_NONE>(gg, B, st);
+  return launch_status("gemm_f32_kernel(dG=F dS)");
+}
+
+extern "C" size_t rpst_conv1x1_wgrad_workspace_size(int N, int Cin, int Cout) {
+  if (N <= 0 || Cin <= 0 || Cout <= 0) return 0;
+  return sizeof(float) * (size_t)N * Cin * Cout;
+}
+
+extern "C" int rpst_conv1x1_wgrad(const float* x, const float* dy, float* dw, float* db, int N,
+                                  int Cin, int64_t HW, int Cout, void* workspace,
+                                  size_t workspace_bytes, rpst_stream_t stream) {
+  RPST_REQUIRE(x && dy && dw, "conv1x1_wgrad: null pointer");
+  RPST_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && HW > 0 && HW <= 0x7fffffffLL && N <= 65535,
+               "conv1x1_wgrad: bad shape");
+  if (!workspace || workspace_bytes < rpst_conv1x1_wgrad_workspace_size(N, Cin, Cout)) {
+    set_error("conv1x1_wgrad: workspace too small");
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  float* part = static_cast<float*>(workspace);
+  // part[n][co][ci] = sum_p dy[n][co][p] x[n][ci][p]
+  GemmArgs g{dy, x, part, {}, nullptr, nullptr, 0, Cout, Cin, (int)HW, (int)HW, (int)HW, Cin,
+             (int64_t)Cout * HW, (int64_t)Cin * HW, (int64_t)Cout * Cin, 0};
+  launch_gemm<LAY_RK, LAY_RK, BX_NONE>(g, N, st);
+  if (int e = launch_status("gemm_f32_kernel(dW=dY X^T)")) return e;
+  const int64_t per = (int64_t)Cout * Cin;
+  batch_sum_kernel<<<(unsigned)((per + 255) / 256), 256, 0, st>>>(part, dw, per, N);
+  if (int e = launch_status("batch_sum_kernel")) return e;
+  if (db) {
+    channel_sum_kernel<<<(Cout + 3) / 4, 256, 0, st>>>(dy, db, N, Cout, HW);
+    return launch_status("channel_sum_kernel");
+  }
+  return RPST_OK;
+}
+
+extern "C" size_t rpst_adaptive_attention_backward_workspace_size(int B, int C, int HW,
+                                                                  int hidden) {
+  if (B <= 0 || C <= 0 || HW <= 0 || hidden <= 0) return 0;
+  const size_t hw2 = (size_t)B * HW * HW;
+  return sizeof(float) * (3 * hw2 + 2 * (size_t)B * HW * hidden + 2 * (size_t)B * C * HW +
+                          8 * (size_t)B * HW);
+}
+
+extern "C" int rpst_adaptive_attention_backward(
+    const float* F, const float* G, const float* H, const float* content, const float* style,
+    const float* w1, const float* b1, const float* w2, const float* b2, int hidden, int mode,
+    float scale, float from, float interval, const float* dO, float* dF, float* dG, float* dH,
+    float* dw1, float* db1, float* dw2, float* db2, int B, int C, int HW, void* workspace,
+    size_t workspace_bytes, rpst_stream_t stream) {
+  RPST_REQUIRE(F && G && H && content && style && w1 && b1 && w2 && b2 && dO && dF && dG &&
+                   dH && dw1 && db1 && dw2 && db2,
+               "adaptive_attention_backward: null pointer");
+  RPST_REQUIRE(B > 0 && C > 0 && HW > 0 && hidden > 0 && B <= 65535 &&
+                   (int64_t)B * HW <= 0x7fffffffLL,
+               "adaptive_attention_backward: bad shape B=%d C=%d HW=%d hidden=%d", B, C, HW,
+               hidden);
+  RPST_REQUIRE(mode == 0 || mode == 1, "adaptive_attention_backward: mode must be 0 or 1");
+  if (!workspace ||
+      workspace_bytes < rpst_adaptive_attention_backward_workspace_size(B, C, HW, hidden)) {
+    set_error("adaptive_attention_backward: workspace too small");
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  const int64_t hw2 = (int64_t)HW * HW, fhw = (int64_t)C * HW, rows = (int64_t)B * HW;
+  float* Aff = static_cast<float*>(workspace);
+  float* S = Aff + (size_t)B * hw2;
+  float* dQ = S + (size_t)B * hw2;
+  float* Z = dQ + (size_t)B * hw2;
+  float* du = Z + (size_t)rows * hidden;
+  float* cn = du + (size_t)rows * hidden;
+  float* sn = cn + (size_t)B * fhw;
+  float* rmax = sn + (size_t)B * fhw;
+  float* rinv = rmax + rows;
+  float* clamp = rinv + rows;
+  float* m2 = clamp + rows;
+  float* inv2 = m2 + rows;
+  float* dc = inv2 + rows;
+  float* dt = dc + rows;
+  // forward quantities: affinity, clamp (and Z), logits, softmax / relu-softmax statistics
+  if (int e = affinity(content, style, Aff, cn, sn, B, C, HW, st)) return e;
+  if (int e = clamp_values(Aff, w1, b1, w2, b2, hidden, mode, from, interval, Z, clamp, B, HW,
+                           st))
+    return e;
+  GemmArgs g1{F, G, S, {}, nullptr, nullptr, 0, HW, HW, C, HW, HW, HW, fhw, fhw, hw2, 0};
+  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(g1, B, st);
+  if (int e = launch_status("gemm_f32_kernel(S=F^T G)")) return e;
+  rowstats_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rmax, rinv, rows, HW);
+  if (int e = launch_status("rowstats_kernel")) return e;
+  if (mode == 1) {
+    rowstats_relu_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rmax, rinv, clamp, m2,
+                                                                     inv2, rows, HW);
+    if (int e = launch_status("rowstats_relu_kernel")) return e;
+  }
+  RowVec rv{rmax, rinv, clamp, m2, scale, inv2};
+  // dH = dO Q (Q formed while S is staged: KR staging, the query is the k index)
+  GemmArgs gh{dO, S, dH, rv, nullptr, nullptr, 0, C, HW, HW, HW, HW, HW, fhw, hw2, fhw, HW};
+  if (mode == 0) launch_gemm<LAY_RK, LAY_KR, BX_AEA>(gh, B, st);
+  else launch_gemm<LAY_RK, LAY_KR, BX_AEARQ>(gh, B, st);
+  if (int e = launch_status("gemm_f32_kernel(dH=dO Q)")) return e;
+  // dQ = dO^T H -> dS (in place) and dc
+  GemmArgs gq{dO, H, dQ, {}, nullptr, nullptr, 0, HW, HW, C, HW, HW, HW, fhw, fhw, hw2, 0};
+  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gq, B, st);
+  if (int e = launch_status("gemm_f32_kernel(dQ=dO^T H)")) return e;
+  aea_bwd_rows_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rv, dQ, dc, mode, rows, HW);
+  if (int e = launch_status("aea_bwd_rows_kernel")) return e;
+  // dF = G dS^T, dG = F dS
+  GemmArgs gf{G, dQ, dF, {}, nullptr, nullptr, 0, C, HW, HW, HW, HW, HW, fhw, hw2, fhw, 0};
+  launch_gemm<LAY_RK, LAY_RK, BX_NONE>(gf, B, st);
+  if (int e = launch_status("gemm_f32_kernel(dF=G dS^T)")) return e;
+  GemmArgs gg{F, dQ, dG, {}, nullptr, nullptr, 0, C, HW, HW, HW, HW, HW, fhw, hw2, fhw, 0};
+  launch_gemm<LAY_RK, LAY_KR, BX_NONE>(gg, B, st);
+  if (int e = launch_status("gemm_f32_kernel(dG=F dS)")) return e;
+  // f_psi: dt, du, then dW1 = du^T Aff over all B * HW query rows (one GEMM), the column sums
+  fpsi_bwd_rows_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Z, w2, b2, dc, dt, du, rows,
+                                                                   hidden, mode, interval);
+  if (int e = launch_status("fpsi_bwd_rows_kernel")) return e;
+  GemmArgs gw{du, Aff, dw1, {}, nullptr, nullptr, 0, hidden, HW, (int)rows, hidden, HW, HW,
+              0, 0, 0, 0};
+  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gw, 1, st);
+  if (int e = launch_status("gemm_f32_kernel(dW1=du^T A)")) return e;
+  fpsi_colsum_kernel<<<(hidden + 1 + 255) / 256, 256, 0, st>>>(Z, du, dt, dw2, db1, db2, rows,
+                                                              hidden);
+  return launch_status("fpsi_colsum_kernel");
 }

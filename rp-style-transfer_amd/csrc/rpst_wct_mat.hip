@@ -355,8 +355,11 @@ __device__ __forceinline__ void tile_gemm(MfCtx& c, const double* A, const doubl
     for (int j = 0; j < 2; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
   const int am = m0 + (tid >> 2), ak = (tid & 3) * 8;
   const int bk = tid >> 3, bn = n0 + (tid & 7) * 8;
-  for (int k0 = 0; k0 < n; k0 += kMK) {
-    double ra[8], rb[8];
+  // software pipeline: the k-step kt + 1 operands are loaded into registers while kt's
+  // MFMAs run from the other LDS buffer (one barrier per k-step; the matrices are L2-resident,
+  // so the loads cost latency, not bandwidth)
+  double ra[8], rb[8];
+  auto load = [&](int k0) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int k = k0 + ak + e;
@@ -367,19 +370,25 @@ __device__ __forceinline__ void tile_gemm(MfCtx& c, const double* A, const doubl
       const int k = k0 + bk;
       rb[e] = (k < n && bn + e < n) ? B[(int64_t)k * n + bn + e] : 0.0;
     }
-    __syncthreads();
+  };
+  const int nk = (n + kMK - 1) / kMK;
+  load(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    double* As = c.As + (kt & 1) * kMK * kMLD;
+    double* Bs = c.Bs + (kt & 1) * kMK * kMLD;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) c.As[(ak + e) * kMLD + (tid >> 2)] = ra[e];
+    for (int e = 0; e < 8; ++e) As[(ak + e) * kMLD + (tid >> 2)] = ra[e];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) c.Bs[bk * kMLD + (tid & 7) * 8 + e] = rb[e];
-    __syncthreads();
+    for (int e = 0; e < 8; ++e) Bs[bk * kMLD + (tid & 7) * 8 + e] = rb[e];
+    __syncthreads();  // buffer kt & 1 complete; every wave is done with buffer (kt - 1) & 1
+    if (kt + 1 < nk) load((kt + 1) * kMK);
 #pragma unroll
     for (int ks = 0; ks < kMK / 4; ++ks) {
       double av[2], bv[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) av[i] = c.As[(4 * ks + lk) * kMLD + wm * 32 + i * 16 + lr];
+      for (int i = 0; i < 2; ++i) av[i] = As[(4 * ks + lk) * kMLD + wm * 32 + i * 16 + lr];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bv[j] = c.Bs[(4 * ks + lk) * kMLD + wn * 32 + j * 16 + lr];
+      for (int j = 0; j < 2; ++j) bv[j] = Bs[(4 * ks + lk) * kMLD + wn * 32 + j * 16 + lr];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -387,6 +396,7 @@ __device__ __forceinline__ void tile_gemm(MfCtx& c, const double* A, const doubl
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
   }
+  __syncthreads();  // the next GEMM's first store overwrites buffer 0
   double dev = 0.0, sq = 0.0;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -482,8 +492,8 @@ __device__ __forceinline__ NsOut ns_run(MfCtx& c, const double* X, double add, N
 }
 
 __global__ __launch_bounds__(256) void matfun_kernel(MfArgs a) {
-  __shared__ double As[kMK * kMLD];
-  __shared__ double Bs[kMK * kMLD];
+  __shared__ double As[2 * kMK * kMLD];
+  __shared__ double Bs[2 * kMK * kMLD];
   __shared__ double bc[8];
   // bijective XCD remap (cdna_hip_programming.md 'XCD swizzle must be bijective'): the P
   // workgroups of a group get consecutive ids on one XCD where possible (speed only)

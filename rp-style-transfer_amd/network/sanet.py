@@ -317,5 +317,13 @@ class AdaptiveSAModel(BaseNet):
             return stylized
 
     def forward(self, content, style):
-        """Loss dict of sanet.py:347-382 (inference kernels: call under no_grad)."""
+        """Loss dict of sanet.py:347-382. With autograd enabled and a trainable transform /
+        decoder the losses come from rpst.autograd (the SAModel step with the AdaptiveSANet
+        backward kernels, including the AEA f_psi MLP), so total_loss.backward() trains them
+        as train.py:118-119 does; under no_grad op by op."""
+        if torch.is_grad_enabled() and any(
+                p.requires_grad for p in list(self.transform.parameters()) +
+                list(self.decoder.parameters())):
+            from rpst.autograd import samodel_losses
+            return samodel_losses(self, content, style)
         return SAModel.forward(self, content, style)

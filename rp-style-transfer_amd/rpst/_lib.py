@@ -66,6 +66,15 @@ SIGNATURES = {
     "rpst_mean_variance_norm_backward": (_I, [_P, _P, _P, _P, _I64, _I64, _I, _P]),
     "rpst_softmax_rows": (_I, [_P, _P, _I64, _I, _P]),
     "rpst_softmax_rows_backward": (_I, [_P, _P, _P, _I64, _I, _P]),
+    "rpst_sanet_attention_backward_workspace_size": (_SZ, [_I, _I, _I]),
+    "rpst_sanet_attention_backward": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _SZ,
+                                           _P]),
+    "rpst_adaptive_attention_backward_workspace_size": (_SZ, [_I, _I, _I, _I]),
+    "rpst_adaptive_attention_backward": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _F,
+                                              _F, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I,
+                                              _P, _SZ, _P]),
+    "rpst_conv1x1_wgrad_workspace_size": (_SZ, [_I, _I, _I]),
+    "rpst_conv1x1_wgrad": (_I, [_P, _P, _P, _P, _I, _I, _I64, _I, _P, _SZ, _P]),
     "rpst_u8hwc_to_f32nchw": (_I, [_P, _P, _I, _I, _I, _P]),
     "rpst_f32nchw_to_u8_tile": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_cosine_affinity_workspace_size": (_SZ, [_I, _I, _I]),

@@ -444,7 +444,13 @@ def _conv1x1(conv, x, residual=None):
                       residual=residual)
 
 
+def _is_adaptive(m) -> bool:
+    return hasattr(m, "attention_layer")
+
+
 def _sanet_forward(m, c, s):
+    if _is_adaptive(m):
+        return _adaptive_sanet_forward(m, c, s)
     Fn = ops.mean_variance_norm(c)
     Gn = ops.mean_variance_norm(s)
     F = _conv1x1(m.f, Fn)
@@ -455,33 +461,91 @@ def _sanet_forward(m, c, s):
 
 
 def _lin_grads(dY, X):
-    """1x1 conv weight / bias gradient over a batch: sum_n dY_n X_n^T (rocBLAS GEMM)."""
+    """1x1 conv weight / bias gradient over a batch: sum_n dY_n X_n^T (rpst_conv1x1_wgrad:
+    per-image gemm_f32_kernel products and a fixed-order batch sum)."""
     b, co = dY.shape[:2]
     ci = X.shape[1]
-    dw = torch.bmm(dY.reshape(b, co, -1), X.reshape(b, ci, -1).transpose(1, 2)).sum(0)
-    return dw.reshape(co, ci, 1, 1), dY.sum((0, 2, 3))
+    hw = X[0, 0].numel()
+    dY, X = dY.contiguous(), X.contiguous()
+    dw = torch.empty((co, ci, 1, 1), device=X.device, dtype=torch.float32)
+    db = torch.empty(co, device=X.device, dtype=torch.float32)
+    nbytes = _lib.load().rpst_conv1x1_wgrad_workspace_size(b, ci, co)
+    ws = _ws(nbytes, X)
+    _lib.call("rpst_conv1x1_wgrad", X.data_ptr(), dY.data_ptr(), dw.data_ptr(), db.data_ptr(),
+              b, ci, hw, co, ws.data_ptr(), nbytes, _stream(X))
+    return dw, db
+
+
+def _adaptive_sanet_forward(m, c, s):
+    """AdaptiveSANet.forward (sanet.py:106-131) keeping what its backward needs."""
+    Fn = ops.mean_variance_norm(c)
+    Gn = ops.mean_variance_norm(s)
+    F = _conv1x1(m.f, Fn)
+    G = _conv1x1(m.g, Gn)
+    H = _conv1x1(m.h, s)
+    al = m.attention_layer
+    O, claim, _, _ = ops.adaptive_attention(F, G, H, c, s, al.f_psi, al.mode,
+                                            float(al.scale_value), float(al.from_value),
+                                            float(al.value_interval))
+    m.claim_value = claim
+    return _conv1x1(m.out_conv, O, residual=c), (Fn, Gn, s, F, G, H, O, c)
+
+
+def _adaptive_sanet_backward(m, saved, d_out, grads):
+    """AdaptiveSANet parameter gradients (f, g, h, out_conv and the AEA f_psi MLP) from
+    d_out: rpst_adaptive_attention_backward forms P and the clamped attention Q from the
+    logits where staged; the affinity of the (constant) VGG features feeds f_psi only."""
+    Fn, Gn, s, F, G, H, O, c = saved
+    b, ch, hc, wc = F.shape
+    hw = hc * wc
+    dw, db = _lin_grads(d_out, O)
+    _acc(grads, m.out_conv.weight, dw)
+    _acc(grads, m.out_conv.bias, db)
+    dO = ops.conv2d(d_out, flip_packed_weight(m.out_conv), None, ch, 1).contiguous()
+    al = m.attention_layer
+    w1, b1, w2, b2, hid = ops._mlp_params(al.f_psi)
+    dF, dG, dH = torch.empty_like(F), torch.empty_like(G), torch.empty_like(H)
+    dw1, db1 = torch.empty_like(w1), torch.empty_like(b1)
+    dw2, db2 = torch.empty_like(w2), torch.empty_like(b2)
+    nbytes = _lib.load().rpst_adaptive_attention_backward_workspace_size(b, ch, hw, hid)
+    ws = _ws(nbytes, F)
+    _lib.call("rpst_adaptive_attention_backward", F.data_ptr(), G.data_ptr(), H.data_ptr(),
+              c.data_ptr(), s.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+              b2.data_ptr(), hid, al.mode, float(al.scale_value), float(al.from_value),
+              float(al.value_interval), dO.data_ptr(), dF.data_ptr(), dG.data_ptr(),
+              dH.data_ptr(), dw1.data_ptr(), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr(), b,
+              ch, hw, ws.data_ptr(), nbytes, _stream(F))
+    l1, l2 = al.f_psi[0], al.f_psi[2]
+    _acc(grads, l1.weight, dw1)
+    _acc(grads, l1.bias, db1)
+    _acc(grads, l2.weight, dw2)
+    _acc(grads, l2.bias, db2)
+    for conv, dY, X in ((m.f, dF, Fn), (m.g, dG, Gn), (m.h, dH, s)):
+        dw, db = _lin_grads(dY, X)
+        _acc(grads, conv.weight, dw)
+        _acc(grads, conv.bias, db)
 
 
 def _sanet_backward(m, saved, d_out, grads):
     """SANet parameter gradients from d_out (sanet.py:82-99; the residual's content and
     both inputs are constants of the step)."""
+    if _is_adaptive(m):
+        return _adaptive_sanet_backward(m, saved, d_out, grads)
     Fn, Gn, s, F, G, H, O = saved
     b, c, hc, wc = F.shape
     hwc, hws = hc * wc, G.shape[2] * G.shape[3]
     dw, db = _lin_grads(d_out, O)
     _acc(grads, m.out_conv.weight, dw)
     _acc(grads, m.out_conv.bias, db)
-    dO = ops.conv2d(d_out, flip_packed_weight(m.out_conv), None, c, 1).reshape(b, c, hwc)
-    Fv, Gv, Hv = F.reshape(b, c, hwc), G.reshape(b, c, hws), H.reshape(b, c, hws)
-    S = torch.bmm(Fv.transpose(1, 2), Gv)
-    P = torch.empty_like(S)
-    _lib.call("rpst_softmax_rows", S.data_ptr(), P.data_ptr(), b * hwc, hws, _stream(S))
-    dH = torch.bmm(dO, P)
-    dP = torch.bmm(dO.transpose(1, 2), Hv)
-    _lib.call("rpst_softmax_rows_backward", P.data_ptr(), dP.data_ptr(), dP.data_ptr(),
-              b * hwc, hws, _stream(dP))
-    dF = torch.bmm(Gv, dP.transpose(1, 2))
-    dG = torch.bmm(Fv, dP)
+    dO = ops.conv2d(d_out, flip_packed_weight(m.out_conv), None, c, 1).contiguous()
+    # attention gradients on gemm_f32_kernel (rpst_sanet_attention_backward): S = F^T G, the
+    # softmax probabilities formed while S is staged, dS = P (dP - rowsum(dP P))
+    dF, dG, dH = torch.empty_like(F), torch.empty_like(G), torch.empty_like(H)
+    nbytes = _lib.load().rpst_sanet_attention_backward_workspace_size(b, hwc, hws)
+    ws = _ws(nbytes, F)
+    _lib.call("rpst_sanet_attention_backward", F.data_ptr(), G.data_ptr(), H.data_ptr(),
+              dO.data_ptr(), dF.data_ptr(), dG.data_ptr(), dH.data_ptr(), b, c, hwc, hws,
+              ws.data_ptr(), nbytes, _stream(F))
     for conv, dY, X in ((m.f, dF, Fn), (m.g, dG, Gn), (m.h, dH, s)):
         dw, db = _lin_grads(dY.reshape(X.shape[0], c, *X.shape[2:]), X)
         _acc(grads, conv.weight, dw)
@@ -623,7 +687,9 @@ class _SAModelStep(torch.autograd.Function):
 def samodel_losses(model, content: torch.Tensor, style: torch.Tensor
                    ) -> Tuple[Dict[str, torch.Tensor], torch.Tensor]:
     """SAModel.forward with autograd: the loss dict of sanet.py:248-275 and total_loss,
-    differentiable w.r.t. the transform and decoder parameters."""
+    differentiable w.r.t. the transform and decoder parameters. AdaptiveSAModel.forward
+    (sanet.py:347-382: the same losses around an AdaptiveTransform) runs through the same
+    step, its AdaptiveSANets (and their f_psi MLPs) on rpst_adaptive_attention_backward."""
     ops._check(content, style)
     params: List[torch.Tensor] = list(model.transform.parameters()) + list(model.decoder.parameters())
     c = model.config

@@ -42,7 +42,7 @@ logging.basicConfig(level=logging.INFO,
                     format="%(asctime)s - %(name)s - %(levelname)s - %(message)s")
 logger = logging.getLogger("train")
 
-TRAINABLE = {"adain", "wct", "sanet", "multi_adain", "src"}  # networks with backward kernels (rpst.autograd)
+TRAINABLE = {"adain", "wct", "sanet", "dynamic_sanet", "multi_adain", "src"}  # networks with backward kernels (rpst.autograd)
 
 
 def _begin(network) -> int:

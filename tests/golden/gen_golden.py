@@ -514,6 +514,36 @@ def gen_grads_sam(net):
     np.savez_compressed(os.path.join(HERE, "grads_sam.npz"), n=len(cases), **out)
 
 
+def gen_grads_adaptive(net):
+    """Reference AdaptiveSAModel.forward + total_loss.backward() (sanet.py:347-382, trained by
+    train.py:118-119's dynamic_sanet branch) for both AEA modules: the losses and probes of
+    every transform (incl. f_psi) and decoder gradient. The forward's claim-map extraction
+    (random index, .cpu().numpy()) has no effect on the losses."""
+    out = {}
+    cases = [("aea", (1, 3, 64, 64), 38), ("relu", (2, 3, 64, 64), 39)]
+    for i, (mode, shp, seed) in enumerate(cases):
+        m = net.AdaptiveSAModel(dict(SAM_CFG, ada_module=mode), copy.deepcopy(net.vgg), 0,
+                                shp[-1])
+        m.decoder = copy.deepcopy(m.decoder)  # the module-level decoder is shared
+        ck = synth_model_(m, seed)
+        c = synth.image(3700 + i, shp)
+        s = synth.image(3800 + i, shp)
+        m.zero_grad()
+        d, tot = m.forward(t(c), t(s))
+        tot.backward()
+        out.update({f"mode{i}": mode, f"seed{i}": seed, f"checksum{i}": ck, f"content{i}": c,
+                    f"style{i}": s})
+        for k, v in d.items():
+            out[f"{k}{i}"] = v.detach().numpy()
+        names = []
+        for name, p in m.named_parameters():
+            if p.grad is not None:
+                out[f"gprobe{i}:{name}"] = helpers.grad_probe(name, p.grad.numpy())
+                names.append(name)
+        out[f"names{i}"] = np.array(names)
+    np.savez_compressed(os.path.join(HERE, "grads_adaptive.npz"), n=len(cases), **out)
+
+
 def gen_sourcenet(net):
     """SourceNet.test, classic AdaIN on VGG relu4_1."""
     out = {}
@@ -618,7 +648,8 @@ GENERATORS = {"keys": gen_keys, "stats": gen_stats, "adain_rp": gen_adain_rp,
               "adaptive": gen_adaptive, "deeper": gen_deeper, "grads": gen_grads,
               "grads_wct": gen_grads_wct, "wct_large": gen_wct_large,
               "grads_sam": gen_grads_sam, "grads_src": gen_grads_src,
-              "grads_ms": gen_grads_ms, "wct_edge": gen_wct_edge}
+              "grads_ms": gen_grads_ms, "wct_edge": gen_wct_edge,
+              "grads_adaptive": gen_grads_adaptive}
 
 
 def main():

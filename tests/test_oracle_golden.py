@@ -264,6 +264,32 @@ def test_reference_samodel_training_gradients(golden):
             assert e < 1e-5, (i, name, e)
 
 
+def test_reference_adaptive_samodel_training_gradients(golden):
+    """R.adaptive_samodel_grads under CPU autograd against the reference's
+    AdaptiveSAModel.forward + backward (sanet.py:347-382) for both AEA modules: the losses and
+    probes of every transform (incl. the f_psi MLP) and decoder gradient."""
+    import network as net
+    from helpers import grad_probe, probe_err
+    g = golden("grads_adaptive")
+    cfg = {"content_weight": 1.0, "style_weight": 3.0, "l_identity1_weight": 50.0,
+           "l_identity2_weight": 1.0}
+    for i in range(int(g["n"])):
+        mode = str(g[f"mode{i}"])
+        shp = g[f"content{i}"].shape
+        m = net.AdaptiveSAModel(dict(cfg, ada_module=mode), copy.deepcopy(net.vgg), 0, shp[-1])
+        np.testing.assert_allclose(synth_(m, int(g[f"seed{i}"])), g[f"checksum{i}"], rtol=1e-12)
+        losses, grads = R.adaptive_samodel_grads(t(g[f"content{i}"]), t(g[f"style{i}"]),
+                                                 state_dict_of(m), cfg, mode)
+        for k in ("style_loss", "content_loss", "l_identity1_loss", "l_identity2_loss",
+                  "total_loss"):
+            np.testing.assert_allclose(losses[k].numpy(), g[f"{k}{i}"], rtol=1e-5)
+        names = [str(n) for n in g[f"names{i}"]]
+        assert sorted(names) == sorted(grads)
+        for name in names:
+            e = probe_err(grad_probe(name, grads[name]), g[f"gprobe{i}:{name}"], grads[name].numel())
+            assert e < 1e-5, (i, name, e)
+
+
 def test_reference_sourcenet_training_gradients(golden):
     """R.sourcenet_losses under CPU autograd against the reference's SourceNet.forward +
     backward (base.py:624-649): the losses and probes of every decoder gradient."""
