@@ -582,8 +582,10 @@ def stack_roofline(summary, steps, dt):
 
 def wct_roofline(summary):
     """fp64 rate of rpst_wct_params (covariances + matrix functions, wct_rp.py:82-109) on the
-    covariance FLOPs alone (2 x 2 C^2 HW per image: a lower bound on the work) against the
-    fp64 MFMA peak; the launch is bound by the fp64 MFMA (SURVEY §8(d) config #3)."""
+    covariance FLOPs alone against the fp64 MFMA peak; the launch is bound by the fp64 MFMA
+    (SURVEY §8(d) config #3). The covariances are symmetric, so their algorithmic count is the
+    SYRK one, 2 x C (C + 1) HW per image (one triangle each of cF cF^T and sF sF^T; the
+    reference's full products are 2 x 2 C^2 HW); the Newton-Schulz products are not counted."""
     for name, a in summary.items():
         if name.startswith("wct_params"):
             avg_ms = a["ms"] / a["launches"]
@@ -593,7 +595,7 @@ def wct_roofline(summary):
                     "kernel": f"cov_syrk_kernel + matfun_kernel [{name}]",
                     "launch_ms": round(avg_ms, 4), "flop_per_launch": a["flops"],
                     "traffic": pmc_lookup("wct", name, PMC_CONFIG.get(2)),
-                    "flop_basis": "covariances 2 x 2 C^2 HW per image"}
+                    "flop_basis": "covariances (SYRK) 2 x C (C + 1) HW per image"}
     return None
 
 

@@ -35,4 +35,8 @@ size_t matfun_power_work_doubles(int n, int batch);
 int matfun_power(const double* A, double* out, int n, int batch, int inverse, double* residual,
                  double* work, hipStream_t st);
 
+// out[n] = W T[n] for W (rows x K) fp32 and T (n, K, K) fp64 -> (n, rows, K) fp64 (fp64 MFMA)
+int gemm_f32w_f64(const float* W, const double* T, double* out, int n, int rows, int K,
+                  hipStream_t st);
+
 }  // namespace rpst

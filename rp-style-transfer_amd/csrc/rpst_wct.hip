@@ -28,7 +28,10 @@ namespace rpst {
 #define RPST_WCT_BK 32  // k depth of a staged fp64 GEMM tile (16: wct_params 17.77 vs 16.86 ms)
 #endif
 
-enum { SRC_F64 = 0, SRC_F64C = 1, SRC_F32C = 2 };  // plain fp64 / centered fp64 / centered fp32
+// plain fp64 / centered fp64 / centered fp32 / plain fp32
+enum { SRC_F64 = 0, SRC_F64C = 1, SRC_F32C = 2, SRC_F32 = 3 };
+constexpr bool src_f32(int s) { return s == SRC_F32C || s == SRC_F32; }
+constexpr bool src_centred(int s) { return s == SRC_F64C || s == SRC_F32C; }
 enum { B_KN = 0, B_NK = 1 };
 enum { OUT_F64 = 0, OUT_PARTIAL = 1, OUT_F32_BIAS = 2, OUT_F64_BIAS = 3 };
 
@@ -69,7 +72,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
 template <int SRC, int N, bool VEC, typename OK>
 __device__ __forceinline__ void load_run(double (&v)[N], __amdgpu_buffer_rsrc_t r, unsigned e,
                                          OK ok) {
-  if (SRC == SRC_F32C) {
+  if (src_f32(SRC)) {
     if (VEC) {
 #pragma unroll
       for (int q = 0; q < N / 4; ++q) {
@@ -142,7 +145,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
   const int kbeg = split * kper;
   const int kend = min(g.K, kbeg + kper);
 
-  constexpr unsigned ESA = SRCA == SRC_F32C ? 4u : 8u, ESB = SRCB == SRC_F32C ? 4u : 8u;
+  constexpr unsigned ESA = src_f32(SRCA) ? 4u : 8u, ESB = src_f32(SRCB) ? 4u : 8u;
   const char* Ab = static_cast<const char*>(gA) + (int64_t)b * g.sA * ESA;
   const char* Bb = static_cast<const char*>(gB) + (int64_t)b * g.sB * ESB;
   const __amdgpu_buffer_rsrc_t ra = rsrc(Ab, (unsigned)g.M * g.lda * ESA);
@@ -170,10 +173,10 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
 
   const int am = m0 + sr;
   const bool am_ok = am < g.M;
-  const double amu = (SRCA != SRC_F64 && am_ok) ? amean[am] : 0.0;
+  const double amu = (src_centred(SRCA) && am_ok) ? amean[am] : 0.0;
   const int bn = n0 + sr;  // B_NK row
   const bool bn_ok = bn < g.N;
-  const double bmu_nk = (BLAY == B_NK && SRCB != SRC_F64 && bn_ok) ? bmean[bn] : 0.0;
+  const double bmu_nk = (BLAY == B_NK && src_centred(SRCB) && bn_ok) ? bmean[bn] : 0.0;
 
   double ra_[EPT], rb_[EPT];
   auto load = [&](int k0) {
@@ -193,7 +196,7 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(G64Args g) {
     } else {
       const int k = k0 + kk_;
       const bool kok = k < kend;
-      const double mu = (SRCB != SRC_F64 && kok) ? bmean[k] : 0.0;
+      const double mu = (src_centred(SRCB) && kok) ? bmean[k] : 0.0;
       const int n = n0 + sn;
       load_run<SRCB, EPT, VEC>(rb_, rb, (unsigned)(k * g.ldb + n),
                                [&](int i) { return kok && n + i < g.N; });
@@ -499,7 +502,7 @@ template <int BT, int SRCA, int SRCB, int BLAY, int OUT>
 static void gemm64(const G64Args& g, dim3 grid, hipStream_t st) {
   // 16-B loads need every contiguous run to start on a 16-B boundary: sizes and leading
   // dims in whole vectors (4 floats / 2 doubles), split-K ranges are whole BK tiles.
-  const int va = SRCA == SRC_F32C ? 4 : 2, vb = SRCB == SRC_F32C ? 4 : 2;
+  const int va = src_f32(SRCA) ? 4 : 2, vb = src_f32(SRCB) ? 4 : 2;
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   bool vec = al(g.A) && al(g.B) && g.lda % va == 0 && g.ldb % vb == 0 && g.K % va == 0 &&
              g.sA % va == 0 && g.sB % vb == 0;
@@ -702,6 +705,30 @@ static int wct_run(const void* cF, const void* sF, void* out, int n, int C, int6
     gemm64<64, SRC_F64, SRC, B_KN, OUTM>(g, grid, st);
   }
   return launch_status("gemm_f64_kernel(transform)");
+}
+
+// out[n] = W T[n]: W (rows x K) fp32 shared by the batch, T[n] (K x K) fp64 -> fp64 (rows x K);
+// the per-image folded weights W T_n of rpst_conv2d_mix (rpst_wino4.hip) on the fp64 MFMA
+int gemm_f32w_f64(const float* W, const double* T, double* out, int n, int rows, int K,
+                  hipStream_t st) {
+  G64Args g{};
+  g.A = W;
+  g.B = T;
+  g.C = out;
+  g.alpha = 1.0;
+  g.M = rows;
+  g.N = K;
+  g.K = K;
+  g.lda = K;
+  g.ldb = K;
+  g.ldc = K;
+  g.sA = 0;
+  g.sB = (int64_t)K * K;
+  g.sC = (int64_t)rows * K;
+  g.ksplit = 1;
+  dim3 grid((unsigned)((K + 63) / 64), (unsigned)((rows + 63) / 64), n);
+  gemm64<64, SRC_F32, SRC_F64, B_KN, OUT_F64>(g, grid, st);
+  return launch_status("gemm_f64_kernel(mix weights)");
 }
 
 }  // namespace rpst

@@ -32,6 +32,7 @@
 // the design minimises VALU per MFMA; measured alternatives and their timings:
 // profiles/r01_wino4_variants.log, profiles/r02_wino4_variants.log.
 #include "rpst_conv.h"
+#include "rpst_wct.h"
 
 #include <type_traits>
 
@@ -83,10 +84,12 @@ static_assert(kW4WCH % (64 * 4) == 0, "weight slice = whole 1-KiB LDS-DMA pieces
 // are one 16-B word, and one (co tile, chunk) slice is contiguous (the LDS-DMA copies it
 // verbatim).
 // TW = float (the layer's weights) or double (per-image folded weights, wino4_mix): image
-// b's weights at w + b * Cout * Cin * 9 pack to pk + b * per.
+// b's weights at w + b * Cout * Cin * 9 pack to pk + b * per; element (co, ci, tap) of an
+// image at co * sco + ci * sci + tap * stap (PyTorch layout: Cin * 9, 9, 1).
 template <typename TW>
 __global__ void wino4_pack_kernel(const TW* __restrict__ w, float* __restrict__ pk, int Cout,
-                                  int Cin, int nch, int64_t per, int64_t total) {
+                                  int Cin, int nch, int64_t per, int64_t total, int64_t sco,
+                                  int64_t sci, int64_t stap) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int64_t img = t / per;
@@ -117,12 +120,12 @@ __global__ void wino4_pack_kernel(const TW* __restrict__ w, float* __restrict__ 
                             {1.0 / 24, 1.0 / 12, 1.0 / 6},
                             {1.0 / 24, -1.0 / 12, 1.0 / 6},
                             {0, 0, 1}};
-    const TW* g = w + ((int64_t)co * Cin + ci) * 9;
+    const TW* g = w + co * sco + ci * sci;
     double acc = 0.0;
 #pragma unroll
     for (int u = 0; u < 3; ++u)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) acc += G[i][u] * (double)g[u * 3 + p] * G[jj][p];
+      for (int p = 0; p < 3; ++p) acc += G[i][u] * (double)g[(u * 3 + p) * stap] * G[jj][p];
     v = (float)acc;
   }
   pk[t] = v;
@@ -137,7 +140,8 @@ size_t wino4_packed_floats(int Cout, int Cin) {
 int wino4_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st) {
   const int nch = (Cin + kW4CK - 1) / kW4CK;
   const int64_t t = (int64_t)wino4_packed_floats(Cout, Cin);
-  wino4_pack_kernel<float><<<(unsigned)((t + 255) / 256), 256, 0, st>>>(w, pk, Cout, Cin, nch, t, t);
+  wino4_pack_kernel<float><<<(unsigned)((t + 255) / 256), 256, 0, st>>>(w, pk, Cout, Cin, nch, t, t,
+                                                                    (int64_t)Cin * 9, 9, 1);
   return launch_status("wino4_pack_kernel");
 }
 
@@ -835,7 +839,9 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
 // padding every tap sees s * x + b, so all nine classes are equal). The conv itself then
 // streams the raw feature by plain LDS-DMA: no per-element affine, no extra LDS traffic.
 size_t wino4_fold_floats(int N, int Cin, int Cout) {
-  return (size_t)N * (wino4_packed_floats(Cout, Cin) + (size_t)Cout * 9);
+  // per-image packed U and border biases, then the class sums (fp64)
+  return (size_t)N * (wino4_packed_floats(Cout, Cin) + (size_t)Cout * 9) +
+         2 * (size_t)9 * Cout * Cin + 2;
 }
 
 __global__ void wino4_fold_w_kernel(const float4* __restrict__ pk, float4* __restrict__ out,
@@ -856,36 +862,83 @@ __global__ void wino4_fold_w_kernel(const float4* __restrict__ pk, float4* __res
   out[t] = make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
 }
 
-// btab[(n * Cout + co) * 9 + 3 rc + cc]: rc / cc = 0 first row / column (tap 0 on padding),
-// 1 interior, 2 last; direct-packed weights [chunk][tap][ci % 8][cout_pad]
-__global__ void wino4_fold_b_kernel(const float* __restrict__ dpk, const float* __restrict__ bias,
-                                    const float* __restrict__ aux, float* __restrict__ btab,
-                                    int N, int Cin, int Cout, int cout_pad, int reflect) {
+// Border-class tap sums of the layer weights, S[cls][co][ci] = sum over the taps of class
+// cls = 3 rc + cc that fall inside the image (rc / cc = 0 first row / column: tap 0 on the zero
+// padding, 1 interior, 2 last; with reflect padding every tap is inside: all classes equal),
+// fp64; direct-packed weights [chunk][tap][ci % 8][cout_pad].
+__global__ void class_sums_kernel(const float* __restrict__ dpk, double* __restrict__ S, int Cin,
+                                  int Cout, int cout_pad, int reflect) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)N * Cout * 9) return;
-  const int co = (int)(t % Cout);
-  const int64_t r = t / Cout;
-  const int cls = (int)(r % 9), n = (int)(r / 9);
+  if (t >= (int64_t)9 * Cout * Cin) return;
+  const int ci = (int)(t % Cin);
+  const int64_t r = t / Cin;
+  const int co = (int)(r % Cout), cls = (int)(r / Cout);
   const int rc = cls / 3, cc = cls % 3;
+  const float* w = dpk + ((int64_t)(ci >> 3) * 9 * 8 + (ci & 7)) * cout_pad + co;
+  double tap = 0.0;
+#pragma unroll
+  for (int u = 0; u < 3; ++u)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const bool in = reflect || ((rc != 0 || u != 0) && (rc != 2 || u != 2) &&
+                                  (cc != 0 || p != 0) && (cc != 2 || p != 2));
+      if (in) tap += (double)w[(int64_t)(u * 3 + p) * 8 * cout_pad];
+    }
+  S[t] = tap;
+}
+
+// btab[(n * Cout + co) * 9 + cls] = bias[co] + sum_ci b_n[ci] S[cls][co][ci] (fp64, fixed order:
+// lane-strided partials then a wave sum). b_n = mean_s - mean_c * std_s / std_c (the AdaIN fold,
+// aux = [mean_c | mean_s | std_c | std_s]) or c_n (the WCT fold, cvec). One wave per (n, co).
+__global__ __launch_bounds__(256) void border_bias_kernel(const double* __restrict__ S,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ aux,
+                                                          const double* __restrict__ cvec,
+                                                          float* __restrict__ btab, int N, int Cin,
+                                                          int Cout) {
+  const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (wv >= (int64_t)N * Cout) return;
+  const int co = (int)(wv % Cout), n = (int)(wv / Cout);
   const int64_t nc = (int64_t)N * Cin;
-  double acc = 0.0;
-  for (int ci = 0; ci < Cin; ++ci) {
+  double acc[9];
+#pragma unroll
+  for (int c = 0; c < 9; ++c) acc[c] = 0.0;
+  for (int ci = lane; ci < Cin; ci += 64) {
     const int64_t i = (int64_t)n * Cin + ci;
-    const float sc = aux[3 * nc + i] / aux[2 * nc + i];
-    const double b = (double)aux[nc + i] - (double)aux[i] * (double)sc;
-    const float* w = dpk + ((int64_t)(ci >> 3) * 9 * 8 + (ci & 7)) * cout_pad + co;
-    double tap = 0.0;
+    double b;
+    if (cvec) {
+      b = cvec[i];
+    } else {
+      const float sc = aux[3 * nc + i] / aux[2 * nc + i];
+      b = (double)aux[nc + i] - (double)aux[i] * (double)sc;
+    }
 #pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const bool in = reflect || ((rc != 0 || u != 0) && (rc != 2 || u != 2) &&
-                                    (cc != 0 || p != 0) && (cc != 2 || p != 2));
-        if (in) tap += (double)w[(int64_t)(u * 3 + p) * 8 * cout_pad];
-      }
-    acc += b * tap;
+    for (int c = 0; c < 9; ++c) acc[c] = fma(b, S[((int64_t)c * Cout + co) * Cin + ci], acc[c]);
   }
-  btab[((int64_t)n * Cout + co) * 9 + cls] = (float)((bias ? (double)bias[co] : 0.0) + acc);
+  const double b0 = bias ? (double)bias[co] : 0.0;
+#pragma unroll
+  for (int c = 0; c < 9; ++c) {
+    const double v = wave_sum(acc[c]);
+    if (lane == 0) btab[((int64_t)n * Cout + co) * 9 + c] = (float)(b0 + v);
+  }
+}
+
+static int border_biases(const float* dpk, int cout_pad, const float* bias, const float* aux,
+                         const double* cvec, float* btab, double* S, int N, int Cin, int Cout,
+                         int reflect, hipStream_t st) {
+  const int64_t ns = (int64_t)9 * Cout * Cin;
+  class_sums_kernel<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(dpk, S, Cin, Cout, cout_pad,
+                                                                  reflect);
+  if (int e = launch_status("class_sums_kernel")) return e;
+  const int64_t waves = (int64_t)N * Cout;
+  border_bias_kernel<<<(unsigned)((waves + 3) / 4), 256, 0, st>>>(S, bias, aux, cvec, btab, N, Cin,
+                                                                  Cout);
+  return launch_status("border_bias_kernel");
+}
+
+static double* align8(void* p) {
+  return reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(p) + 7) & ~uintptr_t(7));
 }
 
 int wino4_fold(ConvArgs& a, const float* direct_packed, int direct_cout_pad, float* ws,
@@ -900,11 +953,10 @@ int wino4_fold(ConvArgs& a, const float* direct_packed, int direct_cout_pad, flo
       reinterpret_cast<const float4*>(a.wpk), reinterpret_cast<float4*>(wf), a.aux, a.N, a.Cin,
       nch, per / 4);
   if (int e = launch_status("wino4_fold_w_kernel")) return e;
-  const int64_t nb = (int64_t)a.N * a.Cout * 9;
-  wino4_fold_b_kernel<<<(unsigned)((nb + 127) / 128), 128, 0, st>>>(
-      direct_packed, a.bias, a.aux, bt, a.N, a.Cin, a.Cout, direct_cout_pad,
-      a.pad == RPST_PAD_REFLECT);
-  if (int e = launch_status("wino4_fold_b_kernel")) return e;
+  double* S = align8(bt + (int64_t)a.N * a.Cout * 9);
+  if (int e = border_biases(direct_packed, direct_cout_pad, a.bias, a.aux, nullptr, bt, S, a.N,
+                            a.Cin, a.Cout, a.pad == RPST_PAD_REFLECT, st))
+    return e;
   a.wpk = wf;
   a.wstride = per;
   a.btab = bt;
@@ -919,54 +971,21 @@ int wino4_fold(ConvArgs& a, const float* direct_packed, int direct_cout_pad, flo
 // G^T with one rounding to fp32, and a bias per (n, co) and border class from c_n. With
 // T_n = diag(s), c_n = b this is the AdaIN fold above.
 size_t wino4_mix_floats(int N, int Cin, int Cout) {
-  return wino4_fold_floats(N, Cin, Cout) + 2 * (size_t)N * Cout * Cin * 9;
+  // fold (U, biases, class sums) + W T_n (fp64, [n][tap][co][ci]) + W in [tap][co][m] (fp32)
+  return wino4_fold_floats(N, Cin, Cout) + 2 * (size_t)N * Cout * Cin * 9 +
+         (size_t)9 * Cout * Cin + 4;
 }
 
-__global__ void mix_weights_kernel(const float* __restrict__ dpk, const double* __restrict__ T,
-                                   double* __restrict__ wm, int N, int Cin, int Cout,
-                                   int cout_pad) {
-  // t -> (n, co, tap, k), k fastest: the T[n][m][k] reads of a wave are contiguous
+// Wt[(tap * Cout + co) * Cin + m] = W[co][m][tap] from the direct-packed image (the GEMM A
+// operand of W T_n)
+__global__ void mix_wt_kernel(const float* __restrict__ dpk, float* __restrict__ wt, int Cin,
+                              int Cout, int cout_pad) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)N * Cout * 9 * Cin) return;
-  const int k = (int)(t % Cin);
-  int64_t r = t / Cin;
-  const int tap = (int)(r % 9);
-  r /= 9;
-  const int co = (int)(r % Cout);
-  const int n = (int)(r / Cout);
-  const double* Tn = T + (int64_t)n * Cin * Cin + k;
-  double acc = 0.0;
-  for (int m = 0; m < Cin; ++m)
-    acc = fma((double)dpk[((int64_t)(m >> 3) * 9 + tap) * 8 * cout_pad + (m & 7) * cout_pad + co],
-              Tn[(int64_t)m * Cin], acc);
-  wm[(((int64_t)n * Cout + co) * Cin + k) * 9 + tap] = acc;
-}
-
-// btab[(n * Cout + co) * 9 + cls] = bias[co] + sum_m cvec[n][m] sum_{taps of the class} W
-__global__ void wino4_mix_bias_kernel(const float* __restrict__ dpk, const float* __restrict__ bias,
-                                      const double* __restrict__ cvec, float* __restrict__ btab,
-                                      int N, int Cin, int Cout, int cout_pad, int reflect) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)N * Cout * 9) return;
-  const int co = (int)(t % Cout);
-  const int64_t r = t / Cout;
-  const int cls = (int)(r % 9), n = (int)(r / 9);
-  const int rc = cls / 3, cc = cls % 3;
-  double acc = 0.0;
-  for (int ci = 0; ci < Cin; ++ci) {
-    const float* w = dpk + ((int64_t)(ci >> 3) * 9 * 8 + (ci & 7)) * cout_pad + co;
-    double tap = 0.0;
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const bool in = reflect || ((rc != 0 || u != 0) && (rc != 2 || u != 2) &&
-                                    (cc != 0 || p != 0) && (cc != 2 || p != 2));
-        if (in) tap += (double)w[(int64_t)(u * 3 + p) * 8 * cout_pad];
-      }
-    acc += cvec[(int64_t)n * Cin + ci] * tap;
-  }
-  btab[((int64_t)n * Cout + co) * 9 + cls] = (float)((bias ? (double)bias[co] : 0.0) + acc);
+  if (t >= (int64_t)9 * Cout * Cin) return;
+  const int m = (int)(t % Cin);
+  const int64_t r = t / Cin;
+  const int co = (int)(r % Cout), tap = (int)(r / Cout);
+  wt[t] = dpk[((int64_t)(m >> 3) * 9 + tap) * 8 * cout_pad + (m & 7) * cout_pad + co];
 }
 
 int wino4_mix(ConvArgs& a, const double* T, const double* cvec, const float* direct_packed,
@@ -976,21 +995,22 @@ int wino4_mix(ConvArgs& a, const double* T, const double* cvec, const float* dir
   const int64_t per = (int64_t)wino4_packed_floats(a.Cout, a.Cin);
   float* wf = ws;
   float* bt = ws + (int64_t)a.N * per;
-  double* wm = reinterpret_cast<double*>(bt + (int64_t)a.N * a.Cout * 9 + 1);  // 8-B aligned below
-  wm = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(wm) + 7) & ~uintptr_t(7));
-  const int64_t nw = (int64_t)a.N * a.Cout * 9 * a.Cin;
-  mix_weights_kernel<<<(unsigned)((nw + 255) / 256), 256, 0, st>>>(direct_packed, T, wm, a.N, a.Cin,
-                                                                   a.Cout, direct_cout_pad);
-  if (int e = launch_status("mix_weights_kernel")) return e;
+  double* S = align8(bt + (int64_t)a.N * a.Cout * 9);
+  double* wm = S + (int64_t)9 * a.Cout * a.Cin;  // W T_n: [n][tap][co][k]
+  float* wt = reinterpret_cast<float*>(wm + (int64_t)a.N * a.Cout * 9 * a.Cin);
+  const int64_t nt = (int64_t)9 * a.Cout * a.Cin;
+  mix_wt_kernel<<<(unsigned)((nt + 255) / 256), 256, 0, st>>>(direct_packed, wt, a.Cin, a.Cout,
+                                                              direct_cout_pad);
+  if (int e = launch_status("mix_wt_kernel")) return e;
+  // W'_n = W T_n on the fp64 MFMA: (9 Cout x Cin) x (Cin x Cin) per image
+  if (int e = gemm_f32w_f64(wt, T, wm, a.N, 9 * a.Cout, a.Cin, st)) return e;
   const int64_t tot = (int64_t)a.N * per;
-  wino4_pack_kernel<double><<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(wm, wf, a.Cout, a.Cin,
-                                                                           nch, per, tot);
+  wino4_pack_kernel<double><<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(
+      wm, wf, a.Cout, a.Cin, nch, per, tot, a.Cin, 1, (int64_t)a.Cout * a.Cin);
   if (int e = launch_status("wino4_pack_kernel(mix)")) return e;
-  const int64_t nb = (int64_t)a.N * a.Cout * 9;
-  wino4_mix_bias_kernel<<<(unsigned)((nb + 127) / 128), 128, 0, st>>>(
-      direct_packed, a.bias, cvec, bt, a.N, a.Cin, a.Cout, direct_cout_pad,
-      a.pad == RPST_PAD_REFLECT);
-  if (int e = launch_status("wino4_mix_bias_kernel")) return e;
+  if (int e = border_biases(direct_packed, direct_cout_pad, a.bias, nullptr, cvec, bt, S, a.N,
+                            a.Cin, a.Cout, a.pad == RPST_PAD_REFLECT, st))
+    return e;
   a.wpk = wf;
   a.wstride = per;
   a.btab = bt;

@@ -526,7 +526,7 @@ def wct_params(content: torch.Tensor, style: torch.Tensor, means: Optional[torch
     res = torch.empty(2 * n, device=content.device, dtype=torch.float64)
     nbytes = _lib.load().rpst_wct_workspace_size(n, C, h * w)
     ws = torch.empty(nbytes, device=content.device, dtype=torch.uint8)
-    with _traced(f"wct_params C{C} {h * w}px N{n}", 4.0 * n * C * C * h * w, 0.0):
+    with _traced(f"wct_params C{C} {h * w}px N{n}", 2.0 * n * C * (C + 1) * h * w, 0.0):
         _lib.call("rpst_wct_params", content.data_ptr(), style.data_ptr(), _ptr(means),
                   T.data_ptr(), c.data_ptr(), n, C, h * w, res.data_ptr(), ws.data_ptr(), nbytes,
                   _stream(content))

@@ -146,6 +146,11 @@ def run(steps: List[object], x: torch.Tensor, first_aux=None, first_in_op=None,
     stats_last makes the last conv also return calc_mean_std of its output -> (x, mean,
     std)."""
     mean = std = None
+    if first_mix is not None and (not steps or not isinstance(steps[0], ConvStep)):
+        # the colour transform only fuses into a conv: skipping it would decode raw features
+        raise NotImplementedError("rpst plan: first_mix needs a conv as the plan's first step")
+    if first_in_op is not None and (not steps or not isinstance(steps[0], ConvStep)):
+        raise NotImplementedError("rpst plan: first_in_op needs a conv as the plan's first step")
     for i, s in enumerate(steps):
         if isinstance(s, ConvStep) and i == 0 and first_mix is not None:
             if s.in_op != ops.IN_NONE or (stats_last and len(steps) == 1):

@@ -124,3 +124,19 @@ def test_conv_algorithm_choice_is_host_only(monkeypatch):
     monkeypatch.setenv("RPST_CONV_ALGO", "direct")
     assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == D
     assert lib.rpst_conv2d_algorithm(3, 16, 512, 512, 3, 0) == NR
+
+
+def test_plan_rejects_unfused_first_transform():
+    """A plan whose first step is not a conv cannot fuse the WCT colour transform (first_mix)
+    or an AdaIN input operator: run() must refuse instead of silently decoding raw features."""
+    import torch
+    from rpst import ops, plan
+
+    steps = [plan.OpStep(ops.IN_UPSAMPLE2)]
+    x = torch.zeros(1, 4, 2, 2)
+    with pytest.raises(NotImplementedError, match="first_mix"):
+        plan.run(steps, x, first_mix=(None, None))
+    with pytest.raises(NotImplementedError, match="first_in_op"):
+        plan.run(steps, x, first_in_op=ops.IN_ADAIN)
+    with pytest.raises(NotImplementedError, match="first_mix"):
+        plan.run([], x, first_mix=(None, None))

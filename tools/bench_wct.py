@@ -5,7 +5,7 @@ matrix functions) and rpst_wct_fuse (+ the colour transform), HIP events, best o
 warm-up; fp64 rooflines against the 78.6 TF/s fp64 MFMA peak.
 
 Algorithmic FLOP per image (wct_rp.py:82-114, the reference's op sequence):
-  covariances   2 x 2 C^2 HW   (cF cF^T and sF sF^T)
+  covariances   2 x C (C + 1) HW   (SYRK: one triangle each of cF cF^T and sF sF^T)
   transform     2 C^2 HW       (T cF)
   matrix fns    the Newton-Schulz products are not counted (their iteration count varies):
                 the rate below is a lower bound for the matrix part.
@@ -59,7 +59,7 @@ def main():
                          for i in range(n)]).float().view(n, C, side, side).to(dev)
         t_par = timed(lambda: ops.wct_params(c, s))
         t_fuse = timed(lambda: ops.wct_fuse(c, s))
-        cov = 4.0 * C * C * hw * n
+        cov = 2.0 * C * (C + 1) * hw * n
         rec = {"shape": name, "C": C, "HW": hw, "n": n,
                "wct_params_ms": round(t_par, 3), "wct_fuse_ms": round(t_fuse, 3),
                "params_tflops_cov": round(cov / t_par / 1e9, 2),
