@@ -347,12 +347,15 @@ int rpst_sq_diff_sum(const float* a, const float* b, int64_t n, double scale, fl
                      void* workspace, size_t workspace_bytes, rpst_stream_t stream);
 
 /* ---- a7: matrix_sqrt / matrix_inv_sqrt  network/wct_rp.py:7-40 ----------------------
- * out[b] = (A[b] + 1e-4 I)^(+1/2) (inverse = 0) or ^(-1/2) (inverse = 1) for symmetric PSD
- * fp64 n x n matrices, batch of `batch`. Coupled Newton-Schulz, per matrix until
- * ||I - Z Y||_F < 1e-10 (at most 64 steps); equal to the reference's SVD form because its
- * truncation (< 1e-5) cannot trigger after +1e-4 on a PSD matrix. residual (batch doubles,
- * may be NULL) receives each matrix's last residual: a value >= 1e-10 means the input was
- * not symmetric PSD (the reference's SVD would return V |S|^p V^T there; callers reject it).
+ * out[b] = (A[b] + 1e-4 I)^(+1/2) (inverse = 0) or ^(-1/2) (inverse = 1), fp64 n x n,
+ * batch of `batch`: the reference's SVD form V diag(s^p) V^T with singular values < 1e-5
+ * dropped, for any input. One persistent launch runs coupled Newton-Schulz per matrix
+ * (stop at the product's rounding floor, max(1e-10, 8 eps n ||Y||_F ||Z||_F), or on
+ * stagnation; at most 64 steps) -- equal to the SVD form on symmetric inputs whose smallest
+ * eigenvalue is provably >= 1e-5; a matrix that is not symmetric, may be truncated or did
+ * not converge is recomputed by a one-sided Jacobi SVD (n <= 1024). residual (batch doubles,
+ * may be NULL) receives each matrix's last Newton-Schulz residual (informational). Fully
+ * asynchronous on `stream` (no host synchronisation).
  * Workspace: rpst_matrix_power_workspace_size(n, batch). */
 size_t rpst_matrix_power_workspace_size(int n, int batch);
 int rpst_matrix_power_psd_f64(const double* A, double* out, int n, int batch, int inverse,
@@ -361,7 +364,8 @@ int rpst_matrix_power_psd_f64(const double* A, double* out, int n, int batch, in
 
 /* ---- a8: WCTRPNet.whiten_and_color(cF, sF, 'closed-form')  network/wct_rp.py:82-114 ---
  * cF, sF, out: (C, HW) fp64. out = T (cF - mu_c) + mu_s with the closed-form T.
- * residual (2 doubles or NULL): Newton-Schulz residuals of Cc + 1e-4 I and of Mid's argument.
+ * residual (2 doubles or NULL): Newton-Schulz residuals of Cc + 1e-4 I and of Mid's argument
+ * (informational; a non-finite input gives NaN in out).
  * Workspace: rpst_wct_workspace_size(1, C, HW). */
 size_t rpst_wct_workspace_size(int n, int C, int64_t HW);
 int rpst_whiten_and_color_f64(const double* cF, const double* sF, double* out, int C,

@@ -31,7 +31,12 @@ import json
 import sys
 
 # kernels whose global reads are (predominantly) 16 B per lane: FETCH_SIZE is doubled
-WIDE_READ = ("plane_stats_kernel", "plane_apply_kernel", "rowmean_kernel", "wino4_mfma_kernel")
+WIDE_READ = ("plane_stats_kernel", "plane_apply_kernel", "rowmean_kernel", "wino4_mfma_kernel",
+             "cov_syrk_kernel<16, true>", "cov_syrk_kernel<8, true>", "cov_syrk_kernel<4, true>")
+# the kernels of one rpst_wct_params launch on fp32 features with C <= 256 (configs[2]):
+# covariance SYRK + finish, matrix functions (gemm_f64_kernel is not listed: the decoder's
+# mix-weight GEMM runs on it)
+WCT_KERNELS = ("cov_syrk_kernel", "cov_finish_kernel", "matfun_kernel")
 CONV_MAIN = ("wino4_mfma_kernel", "wino_mfma_kernel", "conv_mfma_kernel", "conv3x3_narrow_kernel")
 CONV_PREFIX = ("conv", "wino", "narrow")
 
@@ -76,6 +81,14 @@ def attribute(disp, order):
                 out["adain"][order["adain_name"]].append(
                     ("plane_stats_kernel+plane_apply_kernel<true>", (disp[k][2], v)))
             last_pair = j
+    # WCT (configs[2]): every dispatch of the wct_params kernels belongs to the step's one
+    # wct_params launch; bytes per launch = their sum / the launches (one matfun each)
+    wct = [n for n in order["per_step"] if n.startswith("wct_params")]
+    if wct:
+        rows = [(name, v) for (_, name, v) in disp
+                if name.split("(")[0].split("<")[0].split("::")[-1] in WCT_KERNELS]
+        if any("matfun_kernel" in name for name, _ in rows):
+            out["wct"][wct[0]] = rows
     if order.get("stats_name"):
         for (i, name, v) in disp[last_pair + 1:]:
             if "plane_stats_kernel" in name:
@@ -90,7 +103,7 @@ def main(fetch_dir, write_dir, order_path, out_path):
     res = {"_note": "bytes per launch (mean over the profiled steps); fetch corrected x2 "
                     "for 16-B-read kernels (MI355X_MICROARCH.md HBM); source: "
                     "tools/pmc_traffic.py, dispatch-order attribution"}
-    for sec in ("launches", "adain", "stats"):
+    for sec in ("launches", "adain", "stats", "wct"):
         res[sec] = {}
         for key in sorted(set(fe.get(sec, {})) | set(wr.get(sec, {}))):
             f_rows, w_rows = fe[sec].get(key, []), wr[sec].get(key, [])
@@ -103,14 +116,20 @@ def main(fetch_dir, write_dir, order_path, out_path):
                     else:
                         vals.append(v * (corr(name) if fetch else 1.0))
                 return sum(vals) / len(vals) if vals else 0.0
+            if sec == "wct":  # per launch: all its dispatches summed / launches (one matfun each)
+                def tot(rows, fetch):
+                    nl = max(1, sum(1 for name, _ in rows if "matfun_kernel" in name))
+                    return sum(v * (corr(name) if fetch else 1.0) for name, v in rows) / nl
             f, w = tot(f_rows, True), tot(w_rows, False)
             kern = (f_rows or w_rows)[0][0]
+            if sec == "wct":
+                kern = "cov_syrk_kernel+cov_finish_kernel+matfun_kernel"
             res[sec][key] = {"kernel": kern.split("(")[0], "dispatches": len(f_rows),
                              "fetch_bytes": f, "write_bytes": w, "traffic_bytes": f + w,
                              "fetch_correction": "x2 (16-B reads)" if (
                                  sec != "launches" or corr(kern) == 2.0) else "raw"}
     json.dump(res, open(out_path, "w"), indent=1)
-    print(f"wrote {sum(len(res[s]) for s in ('launches', 'adain', 'stats'))} launches to {out_path}")
+    print(f"wrote {sum(len(res[s]) for s in ('launches', 'adain', 'stats', 'wct'))} launches to {out_path}")
 
 
 if __name__ == "__main__":
