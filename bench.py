@@ -85,6 +85,8 @@ def build_model(kind, dev):
     elif kind == "train_source":
         m = net.SourceNet(dict(SOURCE_CONFIG), copy.deepcopy(net.vgg))
         m.decoder = copy.deepcopy(m.decoder)  # the module-level decoder is shared
+    elif kind == "train_adaptive":
+        m = net.AdaptiveSAModel(dict(ADAPTIVE_CONFIG), copy.deepcopy(net.vgg), 0, 512)
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, 512)
     synth.synth_module_(m, 0)
@@ -104,7 +106,8 @@ ADAPTIVE_CONFIG = {"ada_module": "relu", "content_weight": 1.0, "style_weight": 
 # config/rl/train_static_sanet.yaml loss weights
 SANET_TRAIN_CONFIG = {"content_weight": 1.0, "style_weight": 3.0, "l_identity1_weight": 50.0,
                       "l_identity2_weight": 1.0}
-TRAIN_KINDS = ("train", "train_wct", "train_sanet", "train_multiscale", "train_source")
+TRAIN_KINDS = ("train", "train_wct", "train_sanet", "train_multiscale", "train_source",
+               "train_adaptive")
 
 
 WORKLOADS = {
@@ -128,17 +131,20 @@ WORKLOADS = {
     "train_multiscale": "MultiScaleAdaINRPNet training iteration: forward() losses + "
                         "total_loss.backward() + Adam step, constant stack hidden 32 x 5 "
                         "(SURVEY 8(f) ranks 1-2)",
+    "train_adaptive": "AdaptiveSAModel training iteration (ada_module=relu, AEA clamp + f_psi "
+                      "MLP differentiated): forward() losses + total_loss.backward() + Adam step "
+                      "on the adaptive transform and decoder (SURVEY 8(f) ranks 2-3)",
     "train_source": "SourceNet training iteration: forward() losses + total_loss.backward() + "
                     "Adam step on the decoder (SURVEY 8(f) ranks 2-3)",
     "selftest": "CPU stand-in per-image function (launcher / timing / gather test only)",
 }
 DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32, "multiscale": 32, "source": 32,
                  "adaptive": 32, "train": 8, "train_wct": 8, "train_sanet": 8,
-                 "train_multiscale": 8, "train_source": 8,
+                 "train_multiscale": 8, "train_source": 8, "train_adaptive": 8,
                  "selftest": 4}
 # CPU-baseline sample per workload (BASELINE.md plan: B=2 at 512^2, B=1 for WCT)
 CPU_SAMPLE_BATCH = {"wct": 1, "train": 1, "train_wct": 1, "train_sanet": 1,
-                    "train_multiscale": 1, "train_source": 1}
+                    "train_multiscale": 1, "train_source": 1, "train_adaptive": 1}
 
 
 def cpu_info():
@@ -221,6 +227,9 @@ def cpu_baseline(kind, size, reps=3, batch=None):
         m = net.SourceNet(dict(SOURCE_CONFIG), copy.deepcopy(net.vgg))
         fn = lambda c, s, sd: R.grads_of(  # noqa: E731
             R.sourcenet_losses, sd, ("decoder.",), c, s, 1.0, 10.0)
+    elif kind == "train_adaptive":
+        m = net.AdaptiveSAModel(dict(ADAPTIVE_CONFIG), copy.deepcopy(net.vgg), 0, size)
+        fn = lambda c, s, sd: R.adaptive_samodel_grads(c, s, sd, ADAPTIVE_CONFIG, "relu")  # noqa: E731
     else:
         m = net.SAModel(cfg, copy.deepcopy(net.vgg), 0, size)
         fn = R.samodel_test

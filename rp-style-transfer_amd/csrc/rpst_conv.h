@@ -239,6 +239,7 @@ constexpr int kW4Rows = 16, kW4Cols = 64, kW4Co = 32;
 bool wino4_supports(int in_op);
 bool wino4_fits(int N, int Cin, int Hs, int Ws, int in_op);
 int wino4_persist();
+int wino4_rows(int Cin, int Cout);  // tile rows per F(4x4) block: 4 (16 output rows) or 2
 size_t wino4_packed_floats(int Cout, int Cin);
 int wino4_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);
 int wino4_launch(ConvArgs& a, int in_op, hipStream_t st);

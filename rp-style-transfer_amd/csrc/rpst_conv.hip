@@ -688,13 +688,14 @@ static ConvGeom conv_geom(int N, int Cin, int Hs, int Ws, int Cout, int ksize, i
   g.tiles_x = (W + kTW - 1) / kTW;
   g.stat_tw = kTW;
   if (g.algo == RPST_CONV_WINOGRAD4) {
+    const int nr = wino4_rows(Cin, Cout);
     g.tiles_x = (W + kW4Cols - 1) / kW4Cols;
-    const int ty = (H + kW4Rows - 1) / kW4Rows;
+    const int ty = (H + 4 * nr - 1) / (4 * nr);
     g.blocks = (int64_t)g.tiles_x * ty * N * (wino4_persist() ? 1 : (Cout + kW4Co - 1) / kW4Co);
-    g.nth = 512;
-    g.stat_P = g.tiles_x * ty * 4;
+    g.nth = 128 * nr;
+    g.stat_P = g.tiles_x * ty * nr;
     g.stat_nt = 4;
-    g.stat_wn = 4;
+    g.stat_wn = nr;
     g.stat_tw = kW4Cols;
     return g;
   }

@@ -66,7 +66,6 @@ constexpr int kW4DMA4 = 5;                 // 16-B pieces (256 floats) on interi
 constexpr int kW4WCH = 36 * kW4BM * kW4CK; // weight floats per (co tile, 8-channel chunk) = 9216
 // LDS ring of 4 stages, one K step (4 input channels) each: patch [4][1280] + weights
 // [2 halves][9][64 lanes][4] = 4608; plus a 1 KiB target for the padding DMA pieces
-constexpr int kW4STG = 4;
 constexpr int kW4SPATCH = 4 * kW4CS;       // 5120
 constexpr int kW4SW = kW4WCH / 2;          // 4608
 constexpr int kW4STAGE = kW4SPATCH + kW4SW;  // 9728 floats = 38 KiB
@@ -76,6 +75,37 @@ static_assert(kW4PH * kW4PS <= kW4DMA * 64 && kW4DMA * 64 <= kW4CS, "patch chann
 static_assert(kW4PH * kW4PS <= kW4DMA4 * 256 && kW4DMA4 * 256 <= kW4CS && kW4PS % 4 == 0,
               "16-B pieces never straddle a patch row");
 static_assert(kW4WCH % (64 * 4) == 0, "weight slice = whole 1-KiB LDS-DMA pieces");
+
+// Block geometry by tile rows NR: NR = 4 is the block described above (8 waves, 16 output
+// rows, 4-stage ring, one block per CU). NR = 2 (layers with few input channels, whose
+// 2-16 K steps leave the block prologue and epilogue exposed): 4 waves, 8 output rows, a
+// 2-stage ring (DMA one step ahead) in 62 KiB and at most 256 VGPRs, so two blocks share a
+// CU and one block's prologue / epilogue runs beside the other's MFMAs. Each wave keeps
+// its 16 tiles x 18 positions x 32 channels; per K step the weight slice (18 pieces) is
+// split over the 4 waves and each wave streams one whole patch channel.
+template <int NR>
+struct W4Geo {
+  static constexpr int NW = 2 * NR;                 // waves
+  static constexpr int NTH = 64 * NW;
+  static constexpr int TH = 4 * NR;                 // output rows per block
+  static constexpr int PH = TH + 2;                 // patch rows
+  static constexpr int NH = NR / 2;                 // waves streaming one patch channel
+  static constexpr int CS = NR == 4 ? 1280 : 768;   // patch channel stride (floats)
+  static constexpr int DMA = NR == 4 ? 20 : 11;     // 4-B pieces per patch channel
+  static constexpr int DMA4 = (PH * 17 + 63) / 64;  // 16-B pieces per patch channel
+  static constexpr int SLOW = DMA / NH;             // 4-B pieces per wave
+  static constexpr int WIDE = (DMA4 + NH - 1) / NH; // 16-B pieces per wave
+  static constexpr int WPI = (18 + NW - 1) / NW;    // weight pieces per wave
+  static constexpr int STG = NR == 4 ? 4 : 2;       // ring stages
+  static constexpr int SPATCH = 4 * CS;
+  static constexpr int STAGE = SPATCH + kW4SW;
+  static constexpr int LAUNCH_WPE = NR == 4 ? 1 : 2;  // __launch_bounds__ waves per SIMD
+  static_assert(PH * kW4PS <= DMA * 64 && DMA * 64 <= CS && DMA % NH == 0, "4-B pieces");
+  static_assert(PH * kW4PS <= DMA4 * 256 && DMA4 * 256 <= CS, "16-B pieces");
+  static_assert(NR * 2048 <= STAGE, "epilogue exchange region fits a stage");
+};
+static_assert(W4Geo<4>::CS == kW4CS && W4Geo<4>::DMA4 == kW4DMA4 && W4Geo<4>::STAGE == kW4STAGE,
+              "NR = 4 is the documented block");
 
 // ---- weight transform + packing -------------------------------------------------------
 // packed[(((((ct * nch + c) * 2 + s) * 2 + h) * 9 + q) * 64 + l) * 4 + e] = U_xi[co][ci]
@@ -156,6 +186,20 @@ bool wino4_fits(int N, int Cin, int Hs, int Ws, int in_op) {
   return (int64_t)(3 * Cin + 8) * plane < (1LL << 32) - (1LL << 20);
 }
 int wino4_persist() { return 1; }  // one block per spatial tile loops over the co tiles
+// tile rows per block (W4Geo): 2 for the layers with Cin * Cout <= RPST_WINO4_HALF (512: the
+// RP stacks' 16->32 and 32->16), 4 otherwise -- a function of the layer's shape only, so an
+// image's bits never depend on its batch. tools/ab_env.sh (bench_conv, ms, NR = 4 / NR = 2,
+// two rounds): 16->32 N64 1.018 / 0.974, 32->16 N32 0.665 / 0.627, 32->64 N64 2.506 / 2.585,
+// 64->32 N32 1.115 / 1.105, 64->128 N64 8.03 / 8.34 (profiles/r03/wino4_half_ab.log): the
+// second block per CU overlaps little (both blocks of a CU run their prologues and
+// epilogues in step), so only the two smallest layers switch.
+int wino4_rows(int Cin, int Cout) {
+  static const int lim = [] {
+    const char* e = getenv("RPST_WINO4_HALF");
+    return (e && *e) ? atoi(e) : 512;
+  }();
+  return (int64_t)Cin * Cout <= lim ? 2 : 4;
+}
 
 // B^T row transform of one 6-vector (in place): the shared terms of rows (1,2) and (3,4)
 // what the F(4x4) epilogue needs besides the tile (wino4_mfma_kernel's epi_ctx)
@@ -266,8 +310,10 @@ __device__ __forceinline__ void w4_tile(int b, int order, int tiles_x, int tiles
 // border-class bias table (a.btab). Both are template arguments so a plain layer's
 // epilogue carries none of their VALU; the two transformed-row halves (ph, waves 0-3 and
 // 4-7) run epilogues specialised for their half.
-template <int INOP, bool STATS, bool BTAB, bool RELU>
-__global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
+template <int NR, int INOP, bool STATS, bool BTAB, bool RELU>
+__global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_mfma_kernel(ConvArgs a) {
+  using Geo = W4Geo<NR>;
+  constexpr int S = Geo::STG, NW = Geo::NW, NH = Geo::NH;
   // timing-only experiments (results wrong; tools/build_variants.sh -DRPST_W4DBG=n): 1 no
   // patch DMA, 2 no weight DMA, 8 no input transform, 16 no barriers, 32 no epilogue,
   // 64 no weight LDS reads, 128 no DMA waits
@@ -278,10 +324,10 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // one __shared__ object per ring stage: the stage a K step reads and the one its DMA
   // fills are then distinct objects, so the compiler's wait insertion does not drain the
   // in-flight DMA before every LDS read (the loop below is unrolled by the ring size)
-  __shared__ __attribute__((aligned(16))) float smem0[kW4STAGE];
-  __shared__ __attribute__((aligned(16))) float smem1[kW4STAGE];
-  __shared__ __attribute__((aligned(16))) float smem2[kW4STAGE];
-  __shared__ __attribute__((aligned(16))) float smem3[kW4STAGE];
+  __shared__ __attribute__((aligned(16))) float smem0[Geo::STAGE];
+  __shared__ __attribute__((aligned(16))) float smem1[Geo::STAGE];
+  __shared__ __attribute__((aligned(16))) float smem2[S > 2 ? Geo::STAGE : 4];
+  __shared__ __attribute__((aligned(16))) float smem3[S > 3 ? Geo::STAGE : 4];
   __shared__ __attribute__((aligned(16))) float dummy[256];  // target of padding DMA pieces
 
   // block -> (column tile, row tile, image), XCD-swizzled (neighbouring spatial tiles share
@@ -298,16 +344,25 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   int tx, ty, n;
   w4_tile(bid, RPST_W4_ORDER, a.tiles_x, a.tiles_y, a.N, tx, ty, n);
   const int nch = a.nchunks, K4 = 2 * nch, G = nct * K4;  // K steps per co tile / in total
-  const int y0 = ty * kW4TH, x0 = tx * kW4TW;
+  const int y0 = ty * Geo::TH, x0 = tx * kW4TW;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int k = lane >> 4, tn = lane & 15;
-  const int wr = wave & 3, ph = wave >> 2;  // tile row, transformed-row half
+  const int wr = wave % NR, ph = wave / NR;  // tile row, transformed-row half
   // optional static priority (a.persist & 2: waves 4-7, & 4: waves 0-3; RPST_WINO4_PRIO=1/2):
   // with the DMA inside the MFMA stream, equal priorities measured fastest (128->256 28.47
   // vs 28.75 ms with waves 4-7 at priority 1; profiles/r02_wino4_variants.log)
   if ((ph && (a.persist & 2)) || (!ph && (a.persist & 4))) __builtin_amdgcn_s_setprio(1);
+  // NR = 2 (two blocks per CU): the second-resident blocks of the first dispatch round
+  // (blockIdx.x in [256, 512): one per CU after the first 256) sleep a.persist >> 8 quanta
+  // of 64 cycles before starting, so the two blocks of a CU run out of phase and one's
+  // prologue / epilogue overlaps the other's MFMAs (RPST_WINO4_STAGGER; A/B experiment)
+  if constexpr (NR == 2) {
+    const int q = a.persist >> 8;
+    if (q > 0 && blockIdx.x >= 256 && blockIdx.x < 512)
+      for (int i = 0; i < q; i += 16) __builtin_amdgcn_s_sleep(16);
+  }
 
   const bool pooled = INOP == RPST_IN_UPSAMPLE2;
   const unsigned in_plane = pooled ? (unsigned)(a.Hs * a.Ws) : (unsigned)(a.H * a.W);
@@ -336,22 +391,22 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // 20 pieces of 4 B per lane (element 64 p + l resolved against the padding), 10 per half.
   // Offsets are computed once per block. ADAIN streams the raw feature the same way and
   // each lane applies the affine in place to the elements its own pieces wrote (fix_own).
-  const int chl = wave >> 1, hf = wave & 1;
+  const int chl = wave / NH, hf = wave % NH;
   const bool zp = a.pad == RPST_PAD_ZERO;
   const int rs = pooled ? a.Ws : a.W;  // source row stride
   constexpr bool kAff = INOP == RPST_IN_ADAIN;
-  constexpr int kSlow = 10;
+  constexpr int kSlow = Geo::SLOW, kWide = Geo::WIDE;
   unsigned poff[kSlow];
   unsigned pvalid = 0;  // bit i: slot i of this lane holds image data (ADAIN's affine applies)
   const bool wide = !pooled && x0 >= 1 && x0 + kW4TW < a.W;
   {
     if (wide) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int p = 3 * hf + i;
-        const int f = 64 * p + lane, row = min(f / 17, kW4PH - 1), j = f - (f / 17) * 17;
+      for (int i = 0; i < kWide; ++i) {
+        const int p = kWide * hf + i;
+        const int f = 64 * p + lane, row = min(f / 17, Geo::PH - 1), j = f - (f / 17) * 17;
         int y = y0 - 1 + row;
-        const bool ok = p < kW4DMA4 && f < kW4PH * 17 && resolve_bf(y, a.H, zp);
+        const bool ok = p < Geo::DMA4 && f < Geo::PH * 17 && resolve_bf(y, a.H, zp);
         poff[i] = ok ? ((unsigned)(y * rs) + (unsigned)(x0 - 1 + 4 * j)) * 4u : oob;
         pvalid |= ok ? (1u << i) : 0u;
       }
@@ -359,7 +414,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < kSlow; ++i) {
         const int f = 64 * (kSlow * hf + i) + lane;
-        const int row = min(f / kW4PS, kW4PH - 1), col = f - (f / kW4PS) * kW4PS;
+        const int row = min(f / kW4PS, Geo::PH - 1), col = f - (f / kW4PS) * kW4PS;
         int y = y0 - 1 + row, x = x0 - 1 + col;
         const bool oky = resolve_bf(y, a.H, zp), okx = resolve_bf(x, a.W, zp);  // both clamp
         const bool ok = col < kW4TW + 2 && oky && okx;
@@ -373,7 +428,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // global loads happen before any DMA is in flight)
   __shared__ float aparm[kAff ? 3 * kW4AffC : 1];
   if constexpr (kAff) {
-    for (int c = tid; c < a.Cin; c += kW4NTH) {
+    for (int c = tid; c < a.Cin; c += Geo::NTH) {
       const AdainP p = adain_params(a.aux, n, c, a);
       aparm[c] = p.mc;
       aparm[kW4AffC + c] = p.scale;
@@ -396,11 +451,11 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
       const int wv = launder(wave);
       const int sw = live ? (ct0 * K4 + g) * kW4SW * 4 + wv * 1024 : 0;  // piece wv's bytes
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const bool real = wv + 8 * i < 18;
+      for (int i = 0; i < Geo::WPI; ++i) {
+        const bool real = wv + NW * i < 18;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rsrc_or_zero(w_img, wbytes, live && real), (lds_ptr_t)(real ? st + kW4SPATCH + wv * 256 + 2048 * i : dummy), 16, lane * 16,
-            real ? sw + 8192 * i : 0, 0, 0);
+            rsrc_or_zero(w_img, wbytes, live && real), (lds_ptr_t)(real ? st + Geo::SPATCH + wv * 256 + NW * 256 * i : dummy), 16, lane * 16,
+            real ? sw + NW * 1024 * i : 0, 0, 0);
       }
     }
   };
@@ -408,22 +463,22 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     {
       if (DBG & 1) return;
       const int wv = launder(wave);
-      const int c = 4 * ks + (wv >> 1);
+      const int c = 4 * ks + wv / NH;
       const bool ok = live && c < a.Cin;
       const auto r = rsrc_or_zero(in_img, oob, ok);
       const int so = ok ? (int)((unsigned)c * in_plane * 4u) : 0;  // < 2^32 (wino4_fits)
-      float* xs = st + (wv >> 1) * kW4CS;
+      float* xs = st + (wv / NH) * Geo::CS;
       if (wide) {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const int p = 3 * (wv & 1) + i;
+        for (int i = 0; i < kWide; ++i) {
+          const int p = kWide * (wv % NH) + i;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              r, (lds_ptr_t)(p < kW4DMA4 ? xs + 256 * p : dummy), 16, (int)poff[i], so, 0, 0);
+              r, (lds_ptr_t)(p < Geo::DMA4 ? xs + 256 * p : dummy), 16, (int)poff[i], so, 0, 0);
         }
       } else {
 #pragma unroll
         for (int i = 0; i < kSlow; ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(xs + 64 * (kSlow * (wv & 1) + i)),
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(xs + 64 * (kSlow * (wv % NH) + i)),
                                                    4, (int)poff[i], so, 0, 0);
       }
     }
@@ -442,12 +497,12 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
       const bool chok = ch < a.Cin;
       const int cc = chok ? ch : 0;
       const float mc = aparm[cc], sc = aparm[kW4AffC + cc], ms = aparm[2 * kW4AffC + cc];
-      float* xs = st + chl * kW4CS;
+      float* xs = st + chl * Geo::CS;
       if (wide) {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const int p = 3 * hf + i;
-          if (p < kW4DMA4) {
+        for (int i = 0; i < kWide; ++i) {
+          const int p = kWide * hf + i;
+          if (p < Geo::DMA4) {
             float4* e = reinterpret_cast<float4*>(xs + 4 * (64 * p + lane));
             const bool ok = chok && ((pvalid >> i) & 1u);
             const float4 v = *e;
@@ -471,7 +526,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // hw / hp: called after MFMA pair kHW / kHP (RPST_W4VAR placement experiments)
   // input rows ph .. ph + 4 of this lane's 6x6 window of one step
   auto load_rows = [&](const float* pbuf, float (&d)[5][6]) {
-    const float* pr = pbuf + k * kW4CS + (4 * wr + ph) * kW4PS + 4 * tn;
+    const float* pr = pbuf + k * Geo::CS + (4 * wr + ph) * kW4PS + 4 * tn;
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const float4 u = *reinterpret_cast<const float4*>(pr + r * kW4PS);
@@ -488,7 +543,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // transform + 36 MFMAs; hw / hp run after MFMA pair kHW / kHP (the DMA of step g + 3)
   auto compute = [&](const float* pbuf, float (&d)[5][6], auto&& hw, auto&& hp) {
     {
-      const float* wq = pbuf + kW4SPATCH + ph * 9 * 256 + lane * 4;
+      const float* wq = pbuf + Geo::SPATCH + ph * 9 * 256 + lane * 4;
       float4 w4[9];
 #pragma unroll
       for (int q = 0; q < 3; ++q)
@@ -589,7 +644,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     w4_tile(xcd_swizzle(blockIdx.x, (int)gridDim.x) / L->cosplit, RPST_W4_ORDER,
             L->tiles_x, L->tiles_y, L->N, btx, bty, e.n);
     const int bx0 = btx * kW4TW;
-    e.gy0 = bty * kW4TH + 4 * wr;
+    e.gy0 = bty * Geo::TH + 4 * wr;
     e.gx0 = bx0 + 4 * tn;
     e.vec = (e.W & 3) == 0 && e.gx0 + 3 < e.W;
     e.rows = max(0, min(4, e.H - e.gy0));
@@ -613,7 +668,7 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     e.btab = L->btab;
     e.statp = L->stat_part;
     e.statP = L->stat_P;
-    e.sidx = (bty * L->tiles_x + btx) * 4 + wr;
+    e.sidx = (bty * L->tiles_x + btx) * NR + wr;
     return e;
   };
   // the bias (interior class for BTAB) is already in Y (partial)
@@ -778,21 +833,29 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
   // read out of range into a stage no later step reads), so the wait before the barrier
   // that opens step g is one constant: the groups of steps g + 1, g + 2 stay in flight
   // (ADAIN's register loads drain everything at their use, so the count stays conservative).
+  // (NR = 2: the 2-stage ring keeps no group in flight past the one being waited for)
   auto wait_ahead2 = [&]() {
     if (DBG & 128) return;
-    if (wide) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // 2 x (3 + 3)
-    else asm volatile("s_waitcnt vmcnt(26)" ::: "memory");       // 2 x (3 + kSlow)
+    if constexpr (S == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      static_assert(S == 4 && Geo::WPI == 3 && kWide == 3 && kSlow == 10, "counted waits");
+      if (wide) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // 2 x (3 + 3)
+      else asm volatile("s_waitcnt vmcnt(26)" ::: "memory");       // 2 x (3 + kSlow)
+    }
   };
   issue(0, 0, true, smem0);
-  issue(1, 1 % K4, G > 1, smem1);
-  issue(2, 2 % K4, G > 2, smem2);
-  int ks3 = 3 % K4;          // chunk step of g + 3
+  if constexpr (S == 4) {
+    issue(1, 1 % K4, G > 1, smem1);
+    issue(2, 2 % K4, G > 2, smem2);
+  }
+  int ks3 = (S - 1) % K4;    // chunk step of g + S - 1
   int ks = 0, ct = ct0;      // chunk step and co tile of g
   if constexpr (kAff) {  // step 0's affine (published by the first step's barrier)
     wait_ahead2();
     fix_own(0, smem0);
   }
-  // K step g from stage `cur`; step g + 3's DMA into `nx3` (the stage step g - 1 used);
+  // K step g from stage `cur`; step g + S - 1's DMA into `nx3` (the stage step g - 1 used);
   // ADAIN: step g + 1's affine on this wave's own pieces in `nx1`, after the MFMAs.
   // (Reading the next step's rows one step ahead, under the MFMAs, needs 30 more VGPRs
   // across the step: 650-1800 spills.)
@@ -801,10 +864,10 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     lds_barrier();  // step g's stage is complete; nx3 is free
     float d[5][6];
     load_rows(cur, d);
-    const bool live3 = g + 3 < G;
-    if constexpr (kHW < 0) issue_w(g + 3, live3, nx3);
+    const bool live3 = g + S - 1 < G;
+    if constexpr (kHW < 0) issue_w(g + S - 1, live3, nx3);
     if constexpr (kHP < 0) issue_p(ks3, live3, nx3);
-    auto hw = [&]() { if constexpr (kHW >= 0) issue_w(g + 3, live3, nx3); };
+    auto hw = [&]() { if constexpr (kHW >= 0) issue_w(g + S - 1, live3, nx3); };
     auto hp = [&]() { if constexpr (kHP >= 0) issue_p(ks3, live3, nx3); };
     compute(cur, d, hw, hp);
     ks3 = ks3 + 1 == K4 ? 0 : ks3 + 1;
@@ -822,11 +885,18 @@ __global__ __launch_bounds__(kW4NTH, 1) void wino4_mfma_kernel(ConvArgs a) {
     ct += ks == K4 - 1 ? 1 : 0;
     ks = ks == K4 - 1 ? 0 : ks + 1;
   };
-  for (int g = 0; g < G; g += kW4STG) {
-    step(g, smem0, smem1, smem3);
-    if (g + 1 < G) step(g + 1, smem1, smem2, smem0);
-    if (g + 2 < G) step(g + 2, smem2, smem3, smem1);
-    if (g + 3 < G) step(g + 3, smem3, smem0, smem2);
+  if constexpr (S == 4) {
+    for (int g = 0; g < G; g += 4) {
+      step(g, smem0, smem1, smem3);
+      if (g + 1 < G) step(g + 1, smem1, smem2, smem0);
+      if (g + 2 < G) step(g + 2, smem2, smem3, smem1);
+      if (g + 3 < G) step(g + 3, smem3, smem0, smem2);
+    }
+  } else {
+    for (int g = 0; g < G; g += 2) {
+      step(g, smem0, smem1, smem1);
+      if (g + 1 < G) step(g + 1, smem1, smem0, smem0);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the padding DMA has landed too
 }
@@ -1024,13 +1094,16 @@ int wino4_launch(ConvArgs& a, int in_op, hipStream_t st) {
   a.Cout_pad = (a.Cout + kW4BM - 1) / kW4BM * kW4BM;
   a.nchunks = (a.Cin + kW4CK - 1) / kW4CK;
   a.tiles_x = (a.W + kW4TW - 1) / kW4TW;
-  a.tiles_y = (a.H + kW4TH - 1) / kW4TH;
+  const int nr = wino4_rows(a.Cin, a.Cout);
+  a.tiles_y = (a.H + 4 * nr - 1) / (4 * nr);
   a.co_tiles = a.Cout_pad / kW4BM;
-  a.stat_P = a.tiles_x * a.tiles_y * 4;
+  a.stat_P = a.tiles_x * a.tiles_y * nr;
   {
     const char* e = getenv("RPST_WINO4_PRIO");  // A/B switch for a static priority
     const int pr = (e && *e) ? atoi(e) : 0;
     a.persist = 1 | (pr == 1 ? 2 : 0) | (pr == 2 ? 4 : 0);
+    const char* sg = getenv("RPST_WINO4_STAGGER");  // 64-cycle sleep quanta (NR = 2)
+    a.persist |= ((sg && *sg) ? atoi(sg) : 0) << 8;
   }
   RPST_REQUIRE((int64_t)a.co_tiles * a.nchunks * kW4WCH * 4 < (1LL << 31),
                "conv2d: winograd4 weight image exceeds 2 GiB");
@@ -1051,12 +1124,19 @@ int wino4_launch(ConvArgs& a, int in_op, hipStream_t st) {
   RPST_REQUIRE(!btab || in_op == RPST_IN_NONE, "conv2d: winograd4 bias table with a loader op");
   // RELU: the activation as one v_med3 per element (the RP stacks and VGG: every large
   // layer); other activations run the general max(y, slope y) form
-#define RPST_W4_GO(OP, S, B)                                              \
-  do {                                                                    \
-    if (a.relu == RPST_ACT_RELU)                                          \
-      wino4_mfma_kernel<OP, S, B, true><<<nb, kW4NTH, 0, st>>>(a);        \
-    else                                                                  \
-      wino4_mfma_kernel<OP, S, B, false><<<nb, kW4NTH, 0, st>>>(a);       \
+#define RPST_W4_GO(OP, S, B)                                                          \
+  do {                                                                                \
+    if (nr == 2) {                                                                    \
+      if (a.relu == RPST_ACT_RELU)                                                    \
+        wino4_mfma_kernel<2, OP, S, B, true><<<nb, W4Geo<2>::NTH, 0, st>>>(a);        \
+      else                                                                            \
+        wino4_mfma_kernel<2, OP, S, B, false><<<nb, W4Geo<2>::NTH, 0, st>>>(a);       \
+    } else {                                                                          \
+      if (a.relu == RPST_ACT_RELU)                                                    \
+        wino4_mfma_kernel<4, OP, S, B, true><<<nb, kW4NTH, 0, st>>>(a);               \
+      else                                                                            \
+        wino4_mfma_kernel<4, OP, S, B, false><<<nb, kW4NTH, 0, st>>>(a);              \
+    }                                                                                 \
   } while (0)
   switch (in_op) {
     case RPST_IN_ADAIN:

@@ -89,8 +89,8 @@ def _check(*ts: torch.Tensor, dtype=torch.float32) -> None:
             raise RuntimeError(f"rpst: tensors on different devices ({dev} vs {t.device})")
         if torch.is_grad_enabled() and t.requires_grad:
             raise NotImplementedError(
-                "rpst: backward kernels are not implemented (training path is SURVEY §8(f) "
-                "rank 2); call under torch.no_grad()")
+                "rpst: a bare kernel op has no autograd formula (the networks train through "
+                "rpst.autograd's model steps); call it under torch.no_grad()")
 
 
 def _c(t: torch.Tensor) -> torch.Tensor:

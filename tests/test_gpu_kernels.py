@@ -306,16 +306,15 @@ def test_adain_rp_vs_oracle_hidden16(cuda):
 
 
 def test_grad_enabled_raises(cuda):
-    """Models without backward kernels (the AdaptiveSAModel family) raise under autograd
-    instead of running ATen (AdaINRPNet, WCTRPNet, SAModel, MultiScaleAdaINRPNet and
-    SourceNet train through rpst.autograd: tests/test_gpu_train.py)."""
-    import network as net
-    cfg = {"ada_module": "relu", "content_weight": 1.0, "style_weight": 3.0,
-           "l_identity1_weight": 50.0, "l_identity2_weight": 1.0}
-    m = net.AdaptiveSAModel(cfg, copy.deepcopy(net.vgg), 0, 64).to(cuda)
-    x = torch.rand(1, 3, 64, 64, device=cuda)
-    with pytest.raises(NotImplementedError):
-        m(x, x)
+    """A bare rpst op on a tensor that requires grad raises under autograd instead of running
+    ATen or silently dropping the graph (every network trains through rpst.autograd's model
+    steps: tests/test_gpu_train.py, including AdaptiveSAModel)."""
+    from rpst import ops
+    x = torch.rand(1, 4, 8, 8, device=cuda, requires_grad=True)
+    with pytest.raises(NotImplementedError, match="no autograd formula"):
+        ops.calc_mean_std(x)
+    with torch.no_grad():
+        ops.calc_mean_std(x)
 
 
 def test_vgg_and_decoder_golden(cuda, golden):

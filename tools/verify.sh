@@ -12,7 +12,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -2 $O/smoke.log
 timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail $O/bench_default.err; exit 1; }
 cat $O/bench_default.json
-for m in ${RUNS:-"--config 2" "--config 3" "--config 4" "--model multiscale" "--model source" "--model adaptive" "--model train" "--model train_wct" "--model train_sanet" "--model train_multiscale" "--model train_source"}; do
+for m in ${RUNS:-"--config 2" "--config 3" "--config 4" "--model multiscale" "--model source" "--model adaptive" "--model train" "--model train_wct" "--model train_sanet" "--model train_multiscale" "--model train_source" "--model train_adaptive"}; do
   f=$O/bench_$(echo $m | tr -d ' -').json
   timeout -k 10 400 python bench.py $m --no-cpu-baseline > $f 2> $f.err || { tail $f.err; exit 1; }
   python -c "import json;d=json.load(open('$f'));r=d['roofline'];print('$m', d['value'], d['ms_per_step'], r['kernel'], r['frac'])"
