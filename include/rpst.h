@@ -128,6 +128,16 @@ int rpst_conv2d_stats(const float* input, const float* aux, const float* packed_
                       int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
                       float* mean, float* std_out, float eps, void* workspace,
                       size_t workspace_bytes, rpst_stream_t stream);
+/* Same, writing `out` for images n < store_n only (1 <= store_n <= N); the statistics cover
+ * all N images. For a batch whose tail images are needed only through their statistics
+ * (AdaINRPNet.test, adain_rp.py:94-101: the style half of the encoder output feeds
+ * calc_mean_std alone). Images >= store_n of `out` are left unspecified. Same workspace. */
+int rpst_conv2d_stats_store(const float* input, const float* aux, const float* packed_weight,
+                            const float* bias, const float* residual, float* out, int N,
+                            int Cin, int Hs, int Ws, int Cout, int ksize, int pad_mode,
+                            int in_op, int relu, float* mean, float* std_out, float eps,
+                            int store_n, void* workspace, size_t workspace_bytes,
+                            rpst_stream_t stream);
 
 /* MultiScaleAdaINRPNet skip fusion (adain_rp.py:301): out = act(conv(pad(x + AdaIN(c))) +
  * bias), x = `stylized` and c = `content` both (N,Cin,H,W), AdaIN with the calc_mean_std

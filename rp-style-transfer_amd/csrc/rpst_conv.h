@@ -29,6 +29,10 @@ struct ConvArgs {
   // [n][co][3 row classes][3 column classes] replacing `bias` (nullptr: use `bias`)
   int64_t wstride;
   const float* btab;
+  // > 0: images n >= skip_from are not written, only their statistics are reduced (the
+  // AdaIN-RP encoder's style half, whose feature only feeds calc_mean_std). F(4x4) honours
+  // it; the other kernels write everything (still correct)
+  int skip_from;
 };
 
 template <int KS>

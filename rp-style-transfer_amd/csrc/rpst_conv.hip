@@ -782,7 +782,7 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
                        const float* bias, const float* residual, float* out, int N, int Cin,
                        int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
                        float2* stat_part, int* stat_P, ConvArgs* args_out, hipStream_t st,
-                       float* fold_ws = nullptr) {
+                       float* fold_ws = nullptr, int skip_from = 0) {
   RPST_REQUIRE(input && packed_weight && out, "conv2d: null pointer");
   RPST_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && Hs > 0 && Ws > 0, "conv2d: bad shape");
   RPST_REQUIRE(ksize == 1 || ksize == 3, "conv2d: ksize must be 1 or 3, got %d", ksize);
@@ -790,6 +790,7 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   RPST_REQUIRE(in_op >= RPST_IN_NONE && in_op <= RPST_IN_ADD_ADAIN, "conv2d: bad in_op");
   RPST_REQUIRE(relu >= RPST_ACT_NONE && relu <= RPST_ACT_LRELU, "conv2d: bad activation %d", relu);
   ConvArgs a{};
+  a.skip_from = skip_from;
   a.in = input;
   a.aux = aux;
   a.aux2 = aux2;
@@ -1039,13 +1040,15 @@ extern "C" size_t rpst_conv2d_stats_workspace_size(int N, int Cin, int Hs, int W
   return stats + fold_bytes(N, Cin, Hs, Ws, Cout, ksize, in_op);
 }
 
-extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
-                                 const float* packed_weight, const float* bias,
-                                 const float* residual, float* out, int N, int Cin, int Hs,
-                                 int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
-                                 float* mean, float* std_out, float eps, void* workspace,
-                                 size_t workspace_bytes, rpst_stream_t stream) {
+static int conv2d_stats_impl(const float* input, const float* aux, const float* packed_weight,
+                             const float* bias, const float* residual, float* out, int N,
+                             int Cin, int Hs, int Ws, int Cout, int ksize, int pad_mode,
+                             int in_op, int relu, float* mean, float* std_out, float eps,
+                             void* workspace, size_t workspace_bytes, int store_n,
+                             rpst_stream_t stream) {
   RPST_REQUIRE(mean && std_out, "conv2d_stats: null statistics pointer");
+  RPST_REQUIRE(store_n >= 1 && store_n <= N, "conv2d_stats: store_n=%d outside [1, N=%d]",
+               store_n, N);
   const size_t need = rpst_conv2d_stats_workspace_size(N, Cin, Hs, Ws, Cout, ksize, in_op);
   if (!workspace || workspace_bytes < need) {
     set_error("conv2d_stats: workspace %zu < %zu bytes", workspace_bytes, need);
@@ -1067,12 +1070,35 @@ extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
                       : nullptr;
   if (int e = conv_common(input, aux, nullptr, packed_weight, bias, residual, out, N, Cin, Hs, Ws,
                           Cout, ksize, pad_mode, in_op, relu, static_cast<float2*>(workspace), &P,
-                          &a, st, fold_ws))
+                          &a, st, fold_ws, store_n < N ? store_n : 0))
     return e;
   stat_merge_kernel<<<(planes + 3) / 4, 256, 0, st>>>(static_cast<const float2*>(workspace), mean,
                                                       std_out, planes, P, a.tiles_x, g.stat_wn,
                                                       g.stat_nt, g.stat_tw, a.H, a.W, eps);
   return launch_status("stat_merge_kernel");
+}
+
+extern "C" int rpst_conv2d_stats(const float* input, const float* aux,
+                                 const float* packed_weight, const float* bias,
+                                 const float* residual, float* out, int N, int Cin, int Hs,
+                                 int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
+                                 float* mean, float* std_out, float eps, void* workspace,
+                                 size_t workspace_bytes, rpst_stream_t stream) {
+  return conv2d_stats_impl(input, aux, packed_weight, bias, residual, out, N, Cin, Hs, Ws, Cout,
+                           ksize, pad_mode, in_op, relu, mean, std_out, eps, workspace,
+                           workspace_bytes, N, stream);
+}
+
+extern "C" int rpst_conv2d_stats_store(const float* input, const float* aux,
+                                       const float* packed_weight, const float* bias,
+                                       const float* residual, float* out, int N, int Cin, int Hs,
+                                       int Ws, int Cout, int ksize, int pad_mode, int in_op,
+                                       int relu, float* mean, float* std_out, float eps,
+                                       int store_n, void* workspace, size_t workspace_bytes,
+                                       rpst_stream_t stream) {
+  return conv2d_stats_impl(input, aux, packed_weight, bias, residual, out, N, Cin, Hs, Ws, Cout,
+                           ksize, pad_mode, in_op, relu, mean, std_out, eps, workspace,
+                           workspace_bytes, store_n, stream);
 }
 
 // ---- stand-alone max-pool / upsample (used where no conv follows directly) ----------

@@ -191,8 +191,10 @@ int wino4_persist() { return 1; }  // one block per spatial tile loops over the 
 // image's bits never depend on its batch. tools/ab_env.sh (bench_conv, ms, NR = 4 / NR = 2,
 // two rounds): 16->32 N64 1.018 / 0.974, 32->16 N32 0.665 / 0.627, 32->64 N64 2.506 / 2.585,
 // 64->32 N32 1.115 / 1.105, 64->128 N64 8.03 / 8.34 (profiles/r03/wino4_half_ab.log): the
-// second block per CU overlaps little (both blocks of a CU run their prologues and
-// epilogues in step), so only the two smallest layers switch.
+// second block per CU overlaps little, and de-phasing the two (the second-resident blocks
+// of the first dispatch round sleeping 16k / 36k cycles first) changed nothing (16->32
+// 0.970 / 0.976 / 0.969 ms, profiles/r03/wino4_half_ab.log): the small layers are not bound
+// by exposed prologues. Only the two smallest layers switch.
 int wino4_rows(int Cin, int Cout) {
   static const int lim = [] {
     const char* e = getenv("RPST_WINO4_HALF");
@@ -205,7 +207,7 @@ int wino4_rows(int Cin, int Cout) {
 // what the F(4x4) epilogue needs besides the tile (wino4_mfma_kernel's epi_ctx)
 struct EpiCtx {
   int W, H, Cout, gy0, gx0, rows, n, sidx, statP;
-  bool vec, full, bst, edge;
+  bool vec, full, bst, edge, store;
   float inv, slope;      // slope: the activation as max(y, slope y): 0 ReLU, 0.2 LReLU, 1 none
   unsigned voff[4];      // bst: byte offset of output row yy inside a channel plane (or OOB)
   float* out;
@@ -354,15 +356,6 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
   // with the DMA inside the MFMA stream, equal priorities measured fastest (128->256 28.47
   // vs 28.75 ms with waves 4-7 at priority 1; profiles/r02_wino4_variants.log)
   if ((ph && (a.persist & 2)) || (!ph && (a.persist & 4))) __builtin_amdgcn_s_setprio(1);
-  // NR = 2 (two blocks per CU): the second-resident blocks of the first dispatch round
-  // (blockIdx.x in [256, 512): one per CU after the first 256) sleep a.persist >> 8 quanta
-  // of 64 cycles before starting, so the two blocks of a CU run out of phase and one's
-  // prologue / epilogue overlaps the other's MFMAs (RPST_WINO4_STAGGER; A/B experiment)
-  if constexpr (NR == 2) {
-    const int q = a.persist >> 8;
-    if (q > 0 && blockIdx.x >= 256 && blockIdx.x < 512)
-      for (int i = 0; i < q; i += 16) __builtin_amdgcn_s_sleep(16);
-  }
 
   const bool pooled = INOP == RPST_IN_UPSAMPLE2;
   const unsigned in_plane = pooled ? (unsigned)(a.Hs * a.Ws) : (unsigned)(a.H * a.W);
@@ -660,7 +653,10 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
     const int64_t plane = (int64_t)e.H * e.W;
     e.bst = (e.W & 3) == 0 && (int64_t)e.Cout * plane * 4 < (1LL << 31);
     e.oimg = e.out + (int64_t)e.n * e.Cout * plane;
-    e.obytes = (unsigned)(e.Cout * plane * 4);
+    // images past a.skip_from: statistics only, every store out of range (dropped)
+    const bool keep = L->skip_from <= 0 || e.n < L->skip_from;
+    e.obytes = keep ? (unsigned)(e.Cout * plane * 4) : 0u;
+    e.store = keep;
 #pragma unroll
     for (int yy = 0; yy < 4; ++yy)
       e.voff[yy] = (yy < e.rows && e.gx0 < e.W) ? (unsigned)(((e.gy0 + yy) * e.W + e.gx0) * 4)
@@ -729,7 +725,7 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro,
                                                (int)(e.voff[yy] + cofs), 0, 0);
       }
-    } else if (cok) {
+    } else if (cok && e.store) {
       float* o = e.out + (((int64_t)n * e.Cout + co) * e.H + gy0) * e.W + gx0;
 #pragma unroll
       for (int yy = 0; yy < 4; ++yy) {
@@ -1102,8 +1098,6 @@ int wino4_launch(ConvArgs& a, int in_op, hipStream_t st) {
     const char* e = getenv("RPST_WINO4_PRIO");  // A/B switch for a static priority
     const int pr = (e && *e) ? atoi(e) : 0;
     a.persist = 1 | (pr == 1 ? 2 : 0) | (pr == 2 ? 4 : 0);
-    const char* sg = getenv("RPST_WINO4_STAGGER");  // 64-cycle sleep quanta (NR = 2)
-    a.persist |= ((sg && *sg) ? atoi(sg) : 0) << 8;
   }
   RPST_REQUIRE((int64_t)a.co_tiles * a.nchunks * kW4WCH * 4 < (1LL << 31),
                "conv2d: winograd4 weight image exceeds 2 GiB");

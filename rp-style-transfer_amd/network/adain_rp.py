@@ -25,17 +25,22 @@ from .base import adaptive_instance_normalization as AdaIN  # noqa: F401 (refere
 
 # RPST_FUSE_ADAIN=0 disables the fused path (A/B measurements, debugging)
 FUSED_ADAIN = os.environ.get("RPST_FUSE_ADAIN", "1") != "0"
+# RPST_ADAIN_STORE_ALL=1 writes the style half of the encoder output too (A/B)
+STORE_ALL = os.environ.get("RPST_ADAIN_STORE_ALL", "0") == "1"
 
 
 def adain_rp_fused(encoder, decoder, content, style):
     """enc -> AdaIN -> dec with AdaIN fused into its neighbours (adain_rp.py:94-101):
     the encoder's last conv emits calc_mean_std of its output from its epilogue, and the
     decoder's first conv applies ((c - mu_c)/sigma_c)*sigma_s + mu_s while loading its
-    input tile, so the AdaIN feature is never written to HBM."""
+    input tile, so the AdaIN feature is never written to HBM. The style half of the encoder
+    output is consumed only through its statistics: that conv writes the content half alone
+    (store_n = n; adain_rp.py:94-101 reads style_feat only via calc_mean_std)."""
     n = content.shape[0]
     assert content.size() == style.size()
     feats, mean, std = plan.run(plan.compile_layers(encoder.children()),
-                                torch.cat([content, style], dim=0), stats_last=True)
+                                torch.cat([content, style], dim=0), stats_last=True,
+                                store_n=None if STORE_ALL else n)
     aux = ops.adain_params(mean[:n], std[:n], mean[n:], std[n:])
     return plan.run(plan.compile_layers(decoder.children()), feats[:n],
                     first_aux=aux, first_in_op=ops.IN_ADAIN)

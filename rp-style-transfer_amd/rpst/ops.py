@@ -281,9 +281,11 @@ def conv2d_skip_adain(x: torch.Tensor, content: torch.Tensor, params: torch.Tens
 
 def conv2d_stats(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], cout: int,
                  ksize: int, pad: int = PAD_ZERO, in_op: int = IN_NONE, relu: bool = False,
-                 aux: Optional[torch.Tensor] = None, eps: float = 1e-5):
+                 aux: Optional[torch.Tensor] = None, eps: float = 1e-5,
+                 store_n: Optional[int] = None):
     """conv2d plus calc_mean_std of its output, reduced in the conv epilogue:
-    returns (out, mean (N,Cout,1,1), std (N,Cout,1,1))."""
+    returns (out, mean (N,Cout,1,1), std (N,Cout,1,1)). store_n: write out[:store_n] only
+    (rpst_conv2d_stats_store; out[store_n:] unspecified, the statistics cover every image)."""
     assert x.dim() == 4
     _check(x, packed, bias, aux)
     x = _c(x)
@@ -297,10 +299,16 @@ def conv2d_stats(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Ten
     ws_t = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
     with _traced(_conv_name(ksize, cin, cout, hs, ws, n, in_op), 2.0 * n * cout * h * w * cin * ksize * ksize,
                  4.0 * (x.numel() + n * cout * h * w)):
-        _lib.call("rpst_conv2d_stats", x.data_ptr(), _ptr(aux), packed.data_ptr(),
-                  _ptr(None if bias is None else _c(bias.detach())), None, out.data_ptr(), n,
-                  cin, hs, ws, cout, ksize, pad, in_op, _act(relu), mean.data_ptr(),
-                  std.data_ptr(), eps, ws_t.data_ptr(), nbytes, _stream(x))
+        if store_n is None or store_n >= n:
+            _lib.call("rpst_conv2d_stats", x.data_ptr(), _ptr(aux), packed.data_ptr(),
+                      _ptr(None if bias is None else _c(bias.detach())), None, out.data_ptr(), n,
+                      cin, hs, ws, cout, ksize, pad, in_op, _act(relu), mean.data_ptr(),
+                      std.data_ptr(), eps, ws_t.data_ptr(), nbytes, _stream(x))
+        else:
+            _lib.call("rpst_conv2d_stats_store", x.data_ptr(), _ptr(aux), packed.data_ptr(),
+                      _ptr(None if bias is None else _c(bias.detach())), None, out.data_ptr(), n,
+                      cin, hs, ws, cout, ksize, pad, in_op, _act(relu), mean.data_ptr(),
+                      std.data_ptr(), eps, int(store_n), ws_t.data_ptr(), nbytes, _stream(x))
     return out, mean, std
 
 

@@ -138,13 +138,14 @@ def run_conv_step(step: ConvStep, x: torch.Tensor, aux=None, residual=None) -> t
 
 
 def run(steps: List[object], x: torch.Tensor, first_aux=None, first_in_op=None,
-        stats_last: bool = False, first_content=None, first_mix=None):
+        stats_last: bool = False, first_content=None, first_mix=None, store_n=None):
     """Run a compiled plan. first_in_op/first_aux override the first conv's input operator
     (e.g. RPST_IN_ADAIN to fuse AdaIN into the decoder's first conv; RPST_IN_ADD_ADAIN
     with first_content = the skip feature, for x + AdaIN(content)); first_mix = (T, c)
     makes the first conv read T_n x + c_n (the WCT colour transform, rpst_conv2d_mix);
     stats_last makes the last conv also return calc_mean_std of its output -> (x, mean,
-    std)."""
+    std); with store_n that conv writes only images < store_n of x (the rest are needed only
+    through their statistics; their part of x is unspecified)."""
     mean = std = None
     if first_mix is not None and (not steps or not isinstance(steps[0], ConvStep)):
         # the colour transform only fuses into a conv: skipping it would decode raw features
@@ -180,7 +181,7 @@ def run(steps: List[object], x: torch.Tensor, first_aux=None, first_in_op=None,
             elif stats_last and i == len(steps) - 1:
                 x, mean, std = ops.conv2d_stats(x, packed_weight(c), c.bias, c.out_channels,
                                                 c.kernel_size[0], pad=s.pad, in_op=in_op,
-                                                relu=s.relu, aux=aux)
+                                                relu=s.relu, aux=aux, store_n=store_n)
             else:
                 x = ops.conv2d(x, packed_weight(c), c.bias, c.out_channels, c.kernel_size[0],
                                pad=s.pad, in_op=in_op, relu=s.relu, aux=aux)

@@ -355,6 +355,40 @@ def test_conv2d_stats_equal_calc_mean_std(cuda, shape, conv_algo):
     assert rel_l2(std, s2) < 1e-6
 
 
+@pytest.mark.parametrize("shape,store", [((4, 16, 64, 96, 256), 2), ((3, 32, 40, 200, 64), 1),
+                                         ((2, 128, 33, 70, 256), 1), ((2, 8, 17, 45, 64), 1)])
+def test_conv2d_stats_store_head(cuda, shape, store, conv_algo):
+    """rpst_conv2d_stats_store (the AdaIN-RP encoder's last conv over [content; style]):
+    images < store_n of the output and every image's statistics are bit-identical to the
+    full conv2d_stats; the rest of the output is not written (sentinel kept on F(4x4))."""
+    from rpst import _lib, ops
+    n, cin, h, w, cout = shape
+    x = gen(53, (n, cin, h, w), 1.0, 0.3).to(cuda)
+    wt = gen(54, (cout, cin, 3, 3), (2.0 / (cin * 9)) ** 0.5).to(cuda)
+    b = gen(55, (cout,), 0.05).to(cuda)
+    p = ops.pack_conv_weight(wt)
+    out, mean, std = ops.conv2d_stats(x, p, b, cout, 3, relu=True)
+    out2, mean2, std2 = ops.conv2d_stats(x, p, b, cout, 3, relu=True, store_n=store)
+    assert torch.equal(out2[:store], out[:store])
+    assert torch.equal(mean2, mean) and torch.equal(std2, std)
+    # through the C ABI with a NaN sentinel: the tail stays untouched on the F(4x4) path
+    lib = _lib.load()
+    nbytes = lib.rpst_conv2d_stats_workspace_size(n, cin, h, w, cout, 3, ops.IN_NONE)
+    ws_t = torch.empty(nbytes, device=cuda, dtype=torch.uint8)
+    o3 = torch.full_like(out, float("nan"))
+    m3, s3 = torch.empty_like(mean), torch.empty_like(std)
+    _lib.call("rpst_conv2d_stats_store", x.data_ptr(), None, p.data_ptr(), b.data_ptr(), None,
+              o3.data_ptr(), n, cin, h, w, cout, 3, ops.PAD_ZERO, ops.IN_NONE, ops.ACT_RELU,
+              m3.data_ptr(), s3.data_ptr(), 1e-5, store, ws_t.data_ptr(), nbytes,
+              torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(o3[:store], out[:store]) and torch.equal(m3, mean)
+    if lib.rpst_conv2d_algorithm(cout, cin, h, w, 3, ops.IN_NONE) == 2:  # RPST_CONV_WINOGRAD4
+        assert torch.isnan(o3[store:]).all()
+    with pytest.raises(RuntimeError):
+        ops.conv2d_stats(x, p, b, cout, 3, relu=True, store_n=0)
+
+
 @pytest.mark.parametrize("fold", [True, False])
 @pytest.mark.parametrize("pad,shape,cin,cout", [(0, (2, 24, 40), 32, 16),
                                                 (0, (3, 37, 70), 64, 48),
