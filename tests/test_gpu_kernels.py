@@ -182,6 +182,29 @@ def test_conv2d_residual(cuda):
     assert rel_l2(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("case", [
+    (3, 40, 5, 7, 72, True, True),       # ragged Cout (72: partial 128-row tile), HW % 4 != 0
+    (2, 512, 64, 64, 512, False, True),  # SANet relu4_1 f / g / h / out_conv shape
+    (1, 512, 32, 32, 512, False, False), # relu5_1
+    (2, 64, 16, 48, 96, True, False),    # ReLU epilogue
+    (1, 3, 13, 13, 5, False, False),     # tiny K and M
+])
+def test_conv1x1(cuda, case):
+    """1x1 convs (SANet f / g / h / out_conv, the VGG pre-conv) at their model shapes and
+    ragged ones: bias, activation, then residual, against an fp64 reference."""
+    from rpst import ops
+    n, cin, h, w_, cout, relu, with_res = case
+    x = gen(30, (n, cin, h, w_), 1.0, 0.2)
+    w = gen(31, (cout, cin, 1, 1), (2.0 / cin) ** 0.5)
+    b = gen(32, (cout,), 0.05)
+    r = gen(33, (n, cout, h, w_)) if with_res else None
+    ref = _conv_ref(x.double(), w.double(), b.double(), 0, 0, relu,
+                    res=None if r is None else r.double())
+    out = ops.conv2d(x.to(cuda), ops.pack_conv_weight(w.to(cuda)), b.to(cuda), cout, 1,
+                     relu=relu, residual=None if r is None else r.to(cuda))
+    assert rel_l2(out, ref) < 1e-5, rel_l2(out, ref)
+
+
 def test_conv2d_residual_3x3_every_algorithm(cuda, conv_algo):
     """A 3x3 conv with a residual runs on a kernel with the residual epilogue whatever
     algorithm the layer would otherwise take (the Winograd kernels have none)."""
