@@ -104,6 +104,14 @@ int rpst_conv2d(const float* input, const float* aux, const float* packed_weight
                 int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
                 rpst_stream_t stream);
 
+/* rpst_conv2d (in_op RPST_IN_NONE, no residual) over the batch [input; input2]: images
+ * 0..n1-1 are input's, n1..N-1 are input2's (N - n1 images), read in place -- an encoder's
+ * first conv over content and style without materialising torch.cat (adain_rp.py:94-95,
+ * wct_rp.py:141-144, sanet.py:240-242 encode both in one pass). 0 < n1 <= N. */
+int rpst_conv2d_pair(const float* input, const float* input2, int n1, const float* packed_weight,
+                     const float* bias, float* out, int N, int Cin, int Hs, int Ws, int Cout,
+                     int ksize, int pad_mode, int relu, rpst_stream_t stream);
+
 /* Same conv with a caller-provided workspace (rpst_conv2d_workspace_size bytes, 0 when the
  * layer needs none). With RPST_IN_ADAIN on the F(4x4) path the workspace holds per-image
  * weights with the AdaIN scale std_s/std_c folded in along Cin and a per-(n, co) bias by

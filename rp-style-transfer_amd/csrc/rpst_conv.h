@@ -33,7 +33,17 @@ struct ConvArgs {
   // AdaIN-RP encoder's style half, whose feature only feeds calc_mean_std). F(4x4) honours
   // it; the other kernels write everything (still correct)
   int skip_from;
+  // > 0: images n >= in2_from are read from in2 + (n - in2_from) * Cin * plane instead of in
+  // (rpst_conv2d_pair: an encoder's first conv over [content; style] without the concat)
+  const float* in2;
+  int in2_from;
 };
+
+// image n's input planes (block-uniform n)
+__device__ __forceinline__ const float* conv_in_img(const ConvArgs& a, int n, int64_t per) {
+  return (a.in2_from > 0 && n >= a.in2_from) ? a.in2 + (int64_t)(n - a.in2_from) * per
+                                             : a.in + (int64_t)n * per;
+}
 
 template <int KS>
 struct ConvK {

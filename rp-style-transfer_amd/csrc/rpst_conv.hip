@@ -86,7 +86,7 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
   const unsigned in_plane = pooled ? (unsigned)(a.Hs * a.Ws) : (unsigned)(a.H * a.W);
   const unsigned aux_plane = aux_plane_of<INOP>(a);
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.in + (int64_t)n * a.Cin * in_plane), (short)0, (int)(a.Cin * in_plane * 4u),
+      (void*)conv_in_img(a, n, (int64_t)a.Cin * in_plane), (short)0, (int)(a.Cin * in_plane * 4u),
       0x00020000);
   const __amdgpu_buffer_rsrc_t raux = aux_rsrc<INOP>(a, n);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
 #pragma unroll
     for (int c2 = 0; c2 < CO / 2; ++c2) acc2[r][c2] = f2{0.f, 0.f};
   const int64_t plane = (int64_t)a.H * a.W;
-  const float* in = a.in + (int64_t)n * a.Cin * plane;
+  const float* in = conv_in_img(a, n, (int64_t)a.Cin * plane);
   // this thread's patch elements (slot s: element tid + 256 s), their in-plane offsets
   // resolved against the padding once (-1: zero padding / outside the patch); channel ci + 1
   // is loaded into registers while channel ci is computed (the load latency hides under
@@ -782,7 +782,8 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
                        const float* bias, const float* residual, float* out, int N, int Cin,
                        int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
                        float2* stat_part, int* stat_P, ConvArgs* args_out, hipStream_t st,
-                       float* fold_ws = nullptr, int skip_from = 0) {
+                       float* fold_ws = nullptr, int skip_from = 0,
+                       const float* in2 = nullptr, int in2_from = 0) {
   RPST_REQUIRE(input && packed_weight && out, "conv2d: null pointer");
   RPST_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && Hs > 0 && Ws > 0, "conv2d: bad shape");
   RPST_REQUIRE(ksize == 1 || ksize == 3, "conv2d: ksize must be 1 or 3, got %d", ksize);
@@ -792,6 +793,8 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   ConvArgs a{};
   a.skip_from = skip_from;
   a.in = input;
+  a.in2 = in2;
+  a.in2_from = in2 ? in2_from : 0;
   a.aux = aux;
   a.aux2 = aux2;
   a.wpk = packed_weight;
@@ -932,6 +935,17 @@ extern "C" int rpst_conv2d(const float* input, const float* aux, const float* pa
   return conv_common(input, aux, nullptr, packed_weight, bias, residual, out, N, Cin, Hs, Ws,
                      Cout, ksize, pad_mode, in_op, relu, nullptr, nullptr, nullptr,
                      as_stream(stream));
+}
+
+extern "C" int rpst_conv2d_pair(const float* input, const float* input2, int n1,
+                                const float* packed_weight, const float* bias, float* out, int N,
+                                int Cin, int Hs, int Ws, int Cout, int ksize, int pad_mode,
+                                int relu, rpst_stream_t stream) {
+  RPST_REQUIRE(n1 > 0 && n1 <= N, "conv2d_pair: need 0 < n1 <= N (n1=%d, N=%d)", n1, N);
+  RPST_REQUIRE(n1 == N || input2, "conv2d_pair: null second input");
+  return conv_common(input, nullptr, nullptr, packed_weight, bias, nullptr, out, N, Cin, Hs, Ws,
+                     Cout, ksize, pad_mode, RPST_IN_NONE, relu, nullptr, nullptr, nullptr,
+                     as_stream(stream), nullptr, 0, n1 < N ? input2 : nullptr, n1 < N ? n1 : 0);
 }
 
 // workspace of the F(4x4) conv with RPST_IN_ADAIN folded into per-image weights (0 for

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(kWinoNTH, 2) void wino_mfma_kernel(ConvArgs a) {
   const unsigned in_plane = pooled ? (unsigned)(a.Hs * a.Ws) : (unsigned)(a.H * a.W);
   const unsigned aux_plane = aux_plane_of<INOP>(a);
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.in + (int64_t)n * a.Cin * in_plane), (short)0, (int)(a.Cin * in_plane * 4u),
+      (void*)conv_in_img(a, n, (int64_t)a.Cin * in_plane), (short)0, (int)(a.Cin * in_plane * 4u),
       0x00020000);
   const __amdgpu_buffer_rsrc_t raux = aux_rsrc<INOP>(a, n);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(

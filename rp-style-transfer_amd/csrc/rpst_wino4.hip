@@ -362,7 +362,7 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
   // out-of-range offset for a padding position: the image's byte size, added to the
   // channel offset (wino4_fits keeps two of them plus the largest channel offset < 2^32)
   const unsigned oob = a.Cin * in_plane * 4u;
-  const float* in_img = a.in + (int64_t)n * a.Cin * in_plane;
+  const float* in_img = conv_in_img(a, n, (int64_t)a.Cin * in_plane);
   const unsigned wbytes = (unsigned)(a.co_tiles * nch * kW4WCH) * 4u;
   const float* w_img = a.wpk + (int64_t)n * a.wstride;
   // descriptors per issue: a dead piece (past the last step, or a channel >= Cin) goes

@@ -38,9 +38,8 @@ def adain_rp_fused(encoder, decoder, content, style):
     (store_n = n; adain_rp.py:94-101 reads style_feat only via calc_mean_std)."""
     n = content.shape[0]
     assert content.size() == style.size()
-    feats, mean, std = plan.run(plan.compile_layers(encoder.children()),
-                                torch.cat([content, style], dim=0), stats_last=True,
-                                store_n=None if STORE_ALL else n)
+    feats, mean, std = plan.run(plan.compile_layers(encoder.children()), content,
+                                x2=style, stats_last=True, store_n=None if STORE_ALL else n)
     aux = ops.adain_params(mean[:n], std[:n], mean[n:], std[n:])
     return plan.run(plan.compile_layers(decoder.children()), feats[:n],
                     first_aux=aux, first_in_op=ops.IN_ADAIN)
@@ -203,10 +202,11 @@ class MultiScaleAdaINRPNet(AdaINRPNet):
                 self.train()
                 return stylized
             n = content.shape[0]
-            x = torch.cat([content, style], dim=0)
+            x, x2 = content, style  # the first block reads both in place (no concat)
             levels = []  # (feature over 2n, mean, std) per encoder block
             for blk in self.rp_shared_encoder:
-                x, mean, std = plan.run(_block_plan(blk), x, stats_last=True)
+                x, mean, std = plan.run(_block_plan(blk), x, stats_last=True, x2=x2)
+                x2 = None
                 levels.append((x, mean, std))
 
             def params(lv):

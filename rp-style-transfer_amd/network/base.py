@@ -227,14 +227,15 @@ def encode_both(encoder, content, style, stats=False):
     in ONE pass of 2N images. stats=True also returns calc_mean_std of the result from
     the last conv's epilogue: -> (feats, mean, std), each over the 2N batch."""
     stages = encoder if isinstance(encoder, (list, tuple)) else [encoder]
-    x = torch.cat([content, style], dim=0)
+    x, x2 = content, style  # the first conv reads both in place (rpst_conv2d_pair)
     mean = std = None
     for k, st in enumerate(stages):
         steps = plan.compile_layers(st.children())
         if stats and k == len(stages) - 1:
-            x, mean, std = plan.run(steps, x, stats_last=True)
+            x, mean, std = plan.run(steps, x, stats_last=True, x2=x2)
         else:
-            x = plan.run(steps, x)
+            x = plan.run(steps, x, x2=x2)
+        x2 = None
     return (x, mean, std) if stats else x
 
 

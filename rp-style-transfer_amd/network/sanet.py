@@ -18,7 +18,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from rpst import ops
+from rpst import ops, plan
 from rpst.plan import KernelSequential, packed_weight
 
 from .base import BaseNet, _make_decoder, calc_mean_std, mse
@@ -176,6 +176,16 @@ class AdaptiveTransform(nn.Module):
 decoder = _make_decoder()
 
 
+def _encode_pair_intermediate(model, a, b):
+    """model.encode_with_intermediate(torch.cat([a, b])) (sanet.py:219-224 over the
+    [style; content] batch of test(), :240-242) with enc_1's first conv reading a and b in
+    place (rpst_conv2d_pair) instead of a concatenated copy."""
+    results = [plan.run(plan.compile_layers(model.enc_1.children()), a, x2=b)]
+    for i in range(1, 5):
+        results.append(getattr(model, 'enc_{:d}'.format(i + 1))(results[-1]))
+    return results
+
+
 class SAModel(nn.Module):
     def __init__(self, config, encoder, start_iter, img_size):
         super().__init__()
@@ -218,7 +228,7 @@ class SAModel(nn.Module):
         self.eval()
         with torch.no_grad():
             n = content.shape[0]
-            feats = self.encode_with_intermediate(torch.cat([style, content], dim=0))
+            feats = _encode_pair_intermediate(self, style, content)
             s4, c4 = feats[3][:n], feats[3][n:]
             s5, c5 = feats[4][:n], feats[4][n:]
             fusion = self.transform(c4, s4, c5, s5)
@@ -309,7 +319,7 @@ class AdaptiveSAModel(BaseNet):
         self.eval()
         with torch.no_grad():
             n = content.shape[0]
-            feats = self.encode_with_intermediate(torch.cat([style, content], dim=0))
+            feats = _encode_pair_intermediate(self, style, content)
             style_feats = [f[:n] for f in feats]
             content_feats = [f[n:] for f in feats]
             stylized = self.decoder(self.fuse(content_feats, style_feats))

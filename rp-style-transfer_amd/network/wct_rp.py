@@ -34,8 +34,8 @@ def wct_rp_fused(encoder, decoder, content, style):
     (rpst_conv2d_mix), so the fused feature T (cF - mu_c) + mu_s is never written."""
     n = content.shape[0]
     assert content.size() == style.size()
-    feats, mean, _ = plan.run(plan.compile_layers(encoder.children()),
-                              torch.cat([content, style], dim=0), stats_last=True)
+    feats, mean, _ = plan.run(plan.compile_layers(encoder.children()), content, x2=style,
+                              stats_last=True)
     T, c, res = ops.wct_params(feats[:n], feats[n:], means=mean.reshape(2 * n, -1))
     out = plan.run(plan.compile_layers(decoder.children()), feats[:n], first_mix=(T, c))
     # res: the Newton-Schulz residuals (2n), on the device; no host sync here: an image whose

@@ -212,6 +212,27 @@ def pool_pass_pays(x: torch.Tensor, cout: int, ksize: int) -> bool:
         cout, cin, (h + 1) // 2, (w + 1) // 2, ksize, IN_NONE) == 2
 
 
+def conv2d_pair(x: torch.Tensor, x2: torch.Tensor, packed: torch.Tensor,
+                bias: Optional[torch.Tensor], cout: int, ksize: int, pad: int = PAD_ZERO,
+                relu: bool = False) -> torch.Tensor:
+    """conv2d over the batch cat([x, x2]) without materialising the concatenation
+    (rpst_conv2d_pair: the kernel reads images >= len(x) from x2 in place)."""
+    assert x.dim() == 4 and x2.dim() == 4 and tuple(x.shape[1:]) == tuple(x2.shape[1:])
+    _check(x, packed, bias, None, None)
+    _check(x2, packed, bias, None, None)
+    x, x2 = _c(x), _c(x2)
+    n1, cin, hs, ws = x.shape
+    n = n1 + x2.shape[0]
+    out = torch.empty((n, cout, hs, ws), device=x.device, dtype=torch.float32)
+    with _traced(_conv_name(ksize, cin, cout, hs, ws, n, IN_NONE),
+                 2.0 * n * cout * hs * ws * cin * ksize * ksize,
+                 4.0 * (x.numel() + x2.numel() + out.numel())):
+        _lib.call("rpst_conv2d_pair", x.data_ptr(), x2.data_ptr(), n1, packed.data_ptr(),
+                  _ptr(None if bias is None else _c(bias.detach())), out.data_ptr(), n, cin,
+                  hs, ws, cout, ksize, pad, _act(relu), _stream(x))
+    return out
+
+
 def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], cout: int,
            ksize: int, pad: int = PAD_ZERO, in_op: int = IN_NONE, relu: bool = False,
            aux: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,

@@ -138,15 +138,34 @@ def run_conv_step(step: ConvStep, x: torch.Tensor, aux=None, residual=None) -> t
 
 
 def run(steps: List[object], x: torch.Tensor, first_aux=None, first_in_op=None,
-        stats_last: bool = False, first_content=None, first_mix=None, store_n=None):
+        stats_last: bool = False, first_content=None, first_mix=None, store_n=None,
+        x2: Optional[torch.Tensor] = None):
     """Run a compiled plan. first_in_op/first_aux override the first conv's input operator
     (e.g. RPST_IN_ADAIN to fuse AdaIN into the decoder's first conv; RPST_IN_ADD_ADAIN
     with first_content = the skip feature, for x + AdaIN(content)); first_mix = (T, c)
     makes the first conv read T_n x + c_n (the WCT colour transform, rpst_conv2d_mix);
     stats_last makes the last conv also return calc_mean_std of its output -> (x, mean,
     std); with store_n that conv writes only images < store_n of x (the rest are needed only
-    through their statistics; their part of x is unspecified)."""
+    through their statistics; their part of x is unspecified). x2: the plan runs over the
+    batch cat([x, x2]); a plain first conv reads both in place (rpst_conv2d_pair), any
+    other first step gets the concatenation."""
     mean = std = None
+    if x2 is not None:
+        s0 = steps[0] if steps else None
+        pair = (isinstance(s0, ConvStep) and s0.in_op == ops.IN_NONE and first_mix is None
+                and first_in_op is None and not (stats_last and len(steps) == 1))
+        if pair:
+            c = s0.conv
+            x = ops.conv2d_pair(x, x2, packed_weight(c), c.bias, c.out_channels,
+                                c.kernel_size[0], pad=s0.pad, relu=s0.relu)
+            steps = steps[1:]
+            if not steps:
+                if stats_last:
+                    mean, std = ops.calc_mean_std(x)
+                    return x, mean, std
+                return x
+        else:
+            x = torch.cat([x, x2], dim=0)
     if first_mix is not None and (not steps or not isinstance(steps[0], ConvStep)):
         # the colour transform only fuses into a conv: skipping it would decode raw features
         raise NotImplementedError("rpst plan: first_mix needs a conv as the plan's first step")

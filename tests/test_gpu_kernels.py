@@ -205,6 +205,27 @@ def test_conv1x1(cuda, case):
     assert rel_l2(out, ref) < 1e-5, rel_l2(out, ref)
 
 
+@pytest.mark.parametrize("case", [
+    (2, 3, 3, 40, 40, 16, 3, 0, True),     # RP encoder first conv (narrow kernel)
+    (1, 2, 3, 37, 70, 32, 3, 1, True),     # MultiScale first conv (F(4x4)), ragged, reflect
+    (3, 3, 3, 24, 24, 3, 1, 0, False),     # VGG 1x1 pre-conv (direct kernel)
+    (2, 2, 64, 20, 72, 64, 3, 1, True),    # a larger direct / Winograd layer
+])
+def test_conv2d_pair_matches_concat(cuda, case, conv_algo):
+    """rpst_conv2d_pair reads images >= n1 from the second input in place: bit-identical to
+    the same conv over torch.cat([x, x2]) on every algorithm (per-image kernels)."""
+    from rpst import ops
+    n1, n2, cin, h, w_, cout, k, pad, relu = case
+    x = gen(40, (n1, cin, h, w_), 1.0, 0.2).to(cuda)
+    x2 = gen(41, (n2, cin, h, w_), 1.0, 0.2).to(cuda)
+    wt = gen(42, (cout, cin, k, k), (2.0 / (cin * k * k)) ** 0.5).to(cuda)
+    b = gen(43, (cout,), 0.05).to(cuda)
+    pk = ops.pack_conv_weight(wt)
+    ref = ops.conv2d(torch.cat([x, x2]), pk, b, cout, k, pad=pad, relu=relu)
+    out = ops.conv2d_pair(x, x2, pk, b, cout, k, pad=pad, relu=relu)
+    assert torch.equal(out, ref)
+
+
 def test_conv2d_residual_3x3_every_algorithm(cuda, conv_algo):
     """A 3x3 conv with a residual runs on a kernel with the residual epilogue whatever
     algorithm the layer would otherwise take (the Winograd kernels have none)."""
