@@ -2,7 +2,8 @@
 // features, the closed-form matrix functions as ONE persistent launch, and the reference's
 // SVD form for inputs Newton-Schulz cannot take.
 //
-// 1. cov_syrk_kernel: one 512-thread workgroup per (image matrix, K split) computes EVERY
+// 1. cov_syrk_kernel (C <= 128) / cov_syrk16_kernel (C in (128, 256], 16 waves, operand reuse:
+//    see its comment): one workgroup per (image matrix, K split) computes EVERY
 //    upper-triangular 16x16 block of the C x C product (C <= 256), so the k-run of all C
 //    rows is staged once (fp32 -> fp64, centred) and serves as both MFMA operands
 //    (v_mfma_f64_16x16x4_f64: A[l&15][k=l>>4] and B[k=l>>4][l&15] are the same lane map of
@@ -29,12 +30,17 @@
 //    truncation (cheap exit for every other matrix; no host decision).
 #include "rpst_wct.h"
 
+#include <type_traits>
+
 namespace rpst {
 
 // ======================= 1. covariance of fp32 features ==================================
 
 constexpr int kCovBK = 32;       // staged k depth
 constexpr int kCovKPer = 32768;  // k per split (HW = 512^2: 8 splits)
+#ifndef RPST_COV_UNROLL  // cov_syrk16_kernel: k sub-steps unrolled per stage (1 / 2 / 8:
+#define RPST_COV_UNROLL 2  // wct_params 12.35 / 12.08 / 13.03 ms at n 16, C 256, 512^2)
+#endif
 
 struct CovArgs {
   const float* X0;     // content (n, C, HW)
@@ -164,6 +170,154 @@ __global__ __launch_bounds__(512, 1) void cov_syrk_kernel(CovArgs a) {
   }
 }
 
+// C in (128, 256] (NB = 16): the same product with 16 waves (four per SIMD) and operand
+// reuse. The upper triangle of 16 x 16 blocks is 10 super-blocks of 4 x 4 blocks: waves 0-11
+// each own half of an off-diagonal super-block (4 x 2 blocks from 6 operand reads per k
+// sub-step: A and B share one lane map, so the registers of block row I serve as A of row I
+// and as B of column I), waves 12-15 one diagonal super-block each (10 blocks from 4 reads);
+// every SIMD (waves s, s + 4, s + 8, s + 12) carries 3 x 8 + 10 = 34 blocks. The strided map
+// of cov_syrk_kernel reads two operands per MFMA. Partials as cov_syrk_kernel<16> (KG = 1).
+template <bool VEC>
+__global__ __launch_bounds__(1024, 1) void cov_syrk16_kernel(CovArgs a) {
+  constexpr int NB = 16, R = 256, LDX = R + 16;
+  constexpr int TPR = 1024 / R, EPT = kCovBK / TPR;
+  constexpr int NBLK = NB * (NB + 1) / 2;
+  static_assert(EPT % 4 == 0, "16-B staging runs");
+  __shared__ __attribute__((aligned(16))) double Xs[2][kCovBK * LDX];
+
+  const int split = blockIdx.x, z = blockIdx.y;
+  const int n = a.n, C = a.C;
+  const float* X = z < n ? a.X0 + (int64_t)z * C * a.HW : a.X1 + (int64_t)(z - n) * C * a.HW;
+  const int64_t kbeg = (int64_t)split * a.kper;
+  const int64_t kend = a.HW < kbeg + a.kper ? a.HW : kbeg + a.kper;
+  const int nst = (int)((kend - kbeg + kCovBK - 1) / kCovBK);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sr = tid % R, sk = tid / R;  // staged row, k segment
+  const bool rok = sr < C;
+  const float mu = rok ? a.mu32[(int64_t)z * C + sr] : 0.f;
+  const float* xr = X + (int64_t)(rok ? sr : 0) * a.HW;
+
+  float rx[EPT];
+  double rs = 0.0;
+  auto load = [&](int st) {
+    const int64_t k0 = kbeg + (int64_t)st * kCovBK + sk * EPT;
+#pragma unroll
+    for (int q = 0; q < EPT / 4; ++q) {
+      const int64_t k = k0 + 4 * q;
+      if (VEC) {
+        float4 v = make_float4(mu, mu, mu, mu);
+        if (rok && k < kend) v = *reinterpret_cast<const float4*>(xr + k);
+        rx[4 * q] = v.x;
+        rx[4 * q + 1] = v.y;
+        rx[4 * q + 2] = v.z;
+        rx[4 * q + 3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) rx[4 * q + e] = (rok && k + e < kend) ? xr[k + e] : mu;
+      }
+    }
+  };
+  auto store = [&](double* xs) {
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const double d = (double)rx[e] - (double)mu;  // exact in fp64
+      rs += d;
+      xs[(sk * EPT + e) * LDX + sr] = d;
+    }
+  };
+
+  // roles: off-diagonal super-block pairs (0,1) (0,2) (0,3) (1,2) (1,3) (2,3), two column
+  // halves each (waves 0-11); diagonal super-blocks 0-3 (waves 12-15)
+  const bool diag = wave >= 12;
+  int rI = 0, cJ = 0;  // first block row / column of the wave's region
+  if (!diag) {
+    const int sb = wave >> 1, h = wave & 1;
+    const int si = sb < 3 ? 0 : (sb < 5 ? 1 : 2);
+    const int sj = sb < 3 ? sb + 1 : (sb < 5 ? sb - 1 : 3);
+    rI = 4 * si;
+    cJ = 4 * sj + 2 * h;
+  } else {
+    rI = cJ = 4 * (wave - 12);
+  }
+  double* P = a.part + ((int64_t)z * a.ksplit + split) * NBLK * 256;
+  auto put = [&](int bi, int bj, const doublex4& v) {
+    const int b = bi * NB - bi * (bi - 1) / 2 + (bj - bi);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) P[(b * 16 + (lane >> 4) + 4 * r) * 16 + (lane & 15)] = v[r];
+  };
+  // one loop per role (the two accumulator layouts never meet in one loop's registers);
+  // both run nst stages with one barrier each, so the workgroup's barriers stay uniform
+  auto run = [&](auto DIAGc) __attribute__((always_inline)) {
+    constexpr bool D = decltype(DIAGc)::value;
+    constexpr int NA = D ? 10 : 8;
+    doublex4 acc[NA];
+#pragma unroll
+    for (int q = 0; q < NA; ++q) acc[q] = doublex4{0.0, 0.0, 0.0, 0.0};
+    if (nst > 0) {
+      load(0);
+      store(Xs[0]);
+    }
+    for (int st = 0; st < nst; ++st) {
+      __syncthreads();  // stage st is in Xs[st & 1]; every wave is done with stage st - 1
+      if (st + 1 < nst) load(st + 1);
+      const double* xs = Xs[st & 1];
+#pragma unroll RPST_COV_UNROLL
+      for (int ks = 0; ks < kCovBK / 4; ++ks) {
+        const double* xk = xs + (4 * ks + (lane >> 4)) * LDX + (lane & 15);
+        double r[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = xk[16 * (rI + i)];
+        if constexpr (!D) {
+          double c[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) c[j] = xk[16 * (cJ + j)];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[2 * i + j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[i], c[j], acc[2 * i + j], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = i; j < 4; ++j) {
+              const int q = i * 4 - i * (i - 1) / 2 + (j - i);
+              acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[i], r[j], acc[q], 0, 0, 0);
+            }
+        }
+      }
+      if (st + 1 < nst) store(Xs[(st + 1) & 1]);
+    }
+    // partial blocks (f64 map: D col = lane & 15, row = (lane >> 4) + 4 r)
+    if constexpr (!D) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) put(rI + i, cJ + j, acc[2 * i + j]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = i; j < 4; ++j) put(rI + i, rI + j, acc[i * 4 - i * (i - 1) / 2 + (j - i)]);
+    }
+  };
+  if (diag) run(std::true_type{});
+  else run(std::false_type{});
+  // row sums over the TPR threads of a row (fixed order)
+  __syncthreads();
+  double* red = Xs[0];
+  red[sk * R + sr] = rs;
+  __syncthreads();
+  if (tid < R && tid < C) {
+    double sum = 0.0;
+#pragma unroll
+    for (int t = 0; t < TPR; ++t) sum += red[t * R + tid];
+    a.rsum[((int64_t)z * a.ksplit + split) * C + tid] = sum;
+  }
+}
+
 // Cc / Cs / mu64 from the partials: S = sum of the partials of the (r, c) block (upper
 // triangle; the lower one mirrors it), delta_r = (row sum of x - mu32) / HW,
 // cov = (S - HW delta_r delta_c) / (HW - 1) (+ I for the content matrices, wct_rp.py:89).
@@ -232,9 +386,15 @@ int cov_v2(const float* cF, const float* sF, const float* mu32, int n, int C, in
 #define RPST_COV_LAUNCH(NBv)                                                   \
   (vec ? (cov_syrk_kernel<NBv, true><<<grid, 512, 0, st>>>(a), 0)              \
        : (cov_syrk_kernel<NBv, false><<<grid, 512, 0, st>>>(a), 0))
+  // RPST_COV_COMPACT=0: the strided 8-wave form for C > 128 too (A/B)
+  const char* ce = getenv("RPST_COV_COMPACT");
+  const bool compact = !(ce && *ce == '0');
   if (NB == 4) RPST_COV_LAUNCH(4);
   else if (NB == 8) RPST_COV_LAUNCH(8);
-  else RPST_COV_LAUNCH(16);
+  else if (compact) {
+    if (vec) cov_syrk16_kernel<true><<<grid, 1024, 0, st>>>(a);
+    else cov_syrk16_kernel<false><<<grid, 1024, 0, st>>>(a);
+  } else RPST_COV_LAUNCH(16);
 #undef RPST_COV_LAUNCH
   if (int e = launch_status("cov_syrk_kernel")) return e;
   const int64_t tot = (int64_t)2 * n * C * C;
