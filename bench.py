@@ -602,7 +602,7 @@ def wct_roofline(summary):
             tf = a["flops"] / (avg_ms * 1e-3) / 1e12
             return {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP64_TFLOPS,
                     "unit": "TFLOP/s (fp64)", "frac": round(tf / PEAK_FP64_TFLOPS, 4),
-                    "kernel": f"cov_syrk_kernel + matfun_kernel [{name}]",
+                    "kernel": f"cov_syrk16_kernel + matfun_kernel [{name}]",
                     "launch_ms": round(avg_ms, 4), "flop_per_launch": a["flops"],
                     "traffic": pmc_lookup("wct", name, PMC_CONFIG.get(2)),
                     "flop_basis": "covariances (SYRK) 2 x C (C + 1) HW per image"}

@@ -32,11 +32,12 @@ import sys
 
 # kernels whose global reads are (predominantly) 16 B per lane: FETCH_SIZE is doubled
 WIDE_READ = ("plane_stats_kernel", "plane_apply_kernel", "rowmean_kernel", "wino4_mfma_kernel",
-             "cov_syrk_kernel<16, true>", "cov_syrk_kernel<8, true>", "cov_syrk_kernel<4, true>")
+             "cov_syrk_kernel<16, true>", "cov_syrk_kernel<8, true>", "cov_syrk_kernel<4, true>",
+             "cov_syrk16_kernel<true>")
 # the kernels of one rpst_wct_params launch on fp32 features with C <= 256 (configs[2]):
 # covariance SYRK + finish, matrix functions (gemm_f64_kernel is not listed: the decoder's
 # mix-weight GEMM runs on it)
-WCT_KERNELS = ("cov_syrk_kernel", "cov_finish_kernel", "matfun_kernel")
+WCT_KERNELS = ("cov_syrk_kernel", "cov_syrk16_kernel", "cov_finish_kernel", "matfun_kernel")
 CONV_MAIN = ("wino4_mfma_kernel", "wino_mfma_kernel", "conv_mfma_kernel", "conv3x3_narrow_kernel")
 CONV_PREFIX = ("conv", "wino", "narrow")
 
@@ -123,7 +124,7 @@ def main(fetch_dir, write_dir, order_path, out_path):
             f, w = tot(f_rows, True), tot(w_rows, False)
             kern = (f_rows or w_rows)[0][0]
             if sec == "wct":
-                kern = "cov_syrk_kernel+cov_finish_kernel+matfun_kernel"
+                kern = "cov_syrk(16)_kernel+cov_finish_kernel+matfun_kernel"
             res[sec][key] = {"kernel": kern.split("(")[0], "dispatches": len(f_rows),
                              "fetch_bytes": f, "write_bytes": w, "traffic_bytes": f + w,
                              "fetch_correction": "x2 (16-B reads)" if (
