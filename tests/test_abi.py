@@ -67,6 +67,17 @@ def test_conv2d_argument_errors(args, msg):
         _lib.call("rpst_conv2d", *args)
 
 
+@pytest.mark.parametrize("n1,n,msg", [(0, 4, "0 < n1 <= N"), (5, 4, "0 < n1 <= N"),
+                                       (2, 4, "null second input")])
+def test_conv2d_pair_argument_errors(n1, n, msg):
+    """rpst_conv2d_pair checks its split before touching the device (no GPU needed)."""
+    lib = _lib.load()
+    x2 = None if msg == "null second input" else 1
+    st = lib.rpst_conv2d_pair(1, x2, n1, 1, None, 1, n, 3, 8, 8, 16, 3, 0, 1, None)
+    assert st == -1
+    assert msg in lib.rpst_last_error().decode()
+
+
 def test_adain_workspace_error():
     lib = _lib.load()
     st = lib.rpst_adain(1, 1, 1, 2, 3, 16, ctypes.c_float(1e-5), 1, 8, None)
