@@ -37,7 +37,7 @@ namespace rpst {
 // ======================= 1. covariance of fp32 features ==================================
 
 constexpr int kCovBK = 32;       // staged k depth
-constexpr int kCovKPer = 32768;  // k per split (HW = 512^2: 8 splits)
+constexpr int kCovSplits = 8;    // K splits per matrix (HW >= 8 x 32): 8 x 2n workgroups
 #ifndef RPST_COV_UNROLL  // cov_syrk16_kernel: k sub-steps unrolled per stage (1 / 2 / 8:
 #define RPST_COV_UNROLL 2  // wct_params 12.35 / 12.08 / 13.03 ms at n 16, C 256, 512^2)
 #endif
@@ -355,7 +355,14 @@ __global__ void cov_finish_kernel(const double* __restrict__ part, const double*
 
 bool cov_v2_supported(int C) { return C >= 1 && C <= 256; }
 
-static int cov_ksplit(int64_t HW) { return (int)((HW + kCovKPer - 1) / kCovKPer); }
+// k per split: HW / 8 rounded up to whole 32-deep stages (512^2: 32768), so every shape
+// fills 8 x 2n workgroups (C = 128 at 256^2 ran 2 splits, C = 256 at 128^2 one); a function
+// of HW only, so an image's bits never depend on its batch
+static int64_t cov_kper(int64_t HW) {
+  const int64_t k = (HW + kCovSplits - 1) / kCovSplits;
+  return (k + kCovBK - 1) / kCovBK * kCovBK;
+}
+static int cov_ksplit(int64_t HW) { return (int)((HW + cov_kper(HW) - 1) / cov_kper(HW)); }
 
 size_t cov_v2_work_doubles(int n, int C, int64_t HW) {
   const int NB = cov_nb(C), nblk = NB * (NB + 1) / 2, ks = cov_ksplit(HW);
@@ -376,7 +383,7 @@ int cov_v2(const float* cF, const float* sF, const float* mu32, int n, int C, in
   a.C = C;
   a.HW = HW;
   a.ksplit = cov_ksplit(HW);
-  a.kper = kCovKPer;
+  a.kper = (int)cov_kper(HW);
   const int NB = cov_nb(C), nblk = NB * (NB + 1) / 2, PS = a.ksplit * cov_kg(NB);
   a.part = work;
   a.rsum = work + (size_t)2 * n * PS * nblk * 256;
