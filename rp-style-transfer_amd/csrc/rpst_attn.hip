@@ -462,27 +462,58 @@ __global__ __launch_bounds__(256) void fpsi_bwd_rows_kernel(const float* __restr
   if (lane == 0) dt[row] = g;
 }
 
-// dw2[n] = sum_k dt[k] Z[k][n], db1[n] = sum_k du[k][n] (thread per n, fixed order over k);
-// db2 = sum_k dt[k] (thread n == hid)
-__global__ void fpsi_colsum_kernel(const float* __restrict__ Z, const float* __restrict__ du,
-                                   const float* __restrict__ dt, float* __restrict__ dw2,
-                                   float* __restrict__ db1, float* __restrict__ db2, int64_t rows,
-                                   int hid) {
+// Column sums of the f_psi backward over all B * HW query rows, in two fixed-order passes:
+// part[(c * 3 + s) * (hid + 1) + n] over the 128-row chunk c (s = 0: sum dt Z[.][n] -> dw2,
+// s = 1: sum du[.][n] -> db1, column hid of s = 2: sum dt -> db2), then the chunks in order.
+// (The single-pass form ran 257 threads over all rows: latency-bound on two CUs.)
+constexpr int kColChunk = 128;
+__global__ __launch_bounds__(256) void fpsi_colsum_part_kernel(
+    const float* __restrict__ Z, const float* __restrict__ du, const float* __restrict__ dt,
+    float* __restrict__ part, int64_t rows, int hid) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  if (n > hid) return;
+  const int64_t k0 = (int64_t)c * kColChunk;
+  const int64_t k1 = rows < k0 + kColChunk ? rows : k0 + kColChunk;
+  float a = 0.f, b = 0.f;
+  if (n == hid) {
+    for (int64_t k = k0; k < k1; ++k) a += dt[k];
+  } else {
+    for (int64_t k = k0; k < k1; ++k) {
+      a = fmaf(dt[k], Z[k * hid + n], a);
+      b += du[k * hid + n];
+    }
+  }
+  float* p = part + (int64_t)c * 3 * (hid + 1);
+  if (n == hid) {
+    p[2 * (hid + 1) + n] = a;
+  } else {
+    p[n] = a;
+    p[(hid + 1) + n] = b;
+  }
+}
+
+__global__ void fpsi_colsum_final_kernel(const float* __restrict__ part, float* __restrict__ dw2,
+                                         float* __restrict__ db1, float* __restrict__ db2,
+                                         int chunks, int hid) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n > hid) return;
-  if (n == hid) {
-    float s = 0.f;
-    for (int64_t k = 0; k < rows; ++k) s += dt[k];
-    db2[0] = s;
-    return;
-  }
   float a = 0.f, b = 0.f;
-  for (int64_t k = 0; k < rows; ++k) {
-    a = fmaf(dt[k], Z[k * hid + n], a);
-    b += du[k * hid + n];
+  for (int c = 0; c < chunks; ++c) {
+    const float* p = part + (int64_t)c * 3 * (hid + 1);
+    if (n == hid) {
+      a += p[2 * (hid + 1) + n];
+    } else {
+      a += p[n];
+      b += p[(hid + 1) + n];
+    }
   }
-  dw2[n] = a;
-  db1[n] = b;
+  if (n == hid) {
+    db2[0] = a;
+  } else {
+    dw2[n] = a;
+    db1[n] = b;
+  }
 }
 
 // ---- AdaptiveSANet (sanet.py:12-18, 26-71, 100-138) -----------------------------------
@@ -899,8 +930,11 @@ extern "C" size_t rpst_adaptive_attention_backward_workspace_size(int B, int C, 
                                                                   int hidden) {
   if (B <= 0 || C <= 0 || HW <= 0 || hidden <= 0) return 0;
   const size_t hw2 = (size_t)B * HW * HW;
+  const size_t chunks = ((size_t)B * HW + kColChunk - 1) / kColChunk;
+  // + the per-image dW1 partials and the column-sum chunk partials
   return sizeof(float) * (3 * hw2 + 2 * (size_t)B * HW * hidden + 2 * (size_t)B * C * HW +
-                          8 * (size_t)B * HW);
+                          8 * (size_t)B * HW + (size_t)B * hidden * HW +
+                          3 * (size_t)(hidden + 1) * chunks);
 }
 
 extern "C" int rpst_adaptive_attention_backward(
@@ -938,6 +972,8 @@ extern "C" int rpst_adaptive_attention_backward(
   float* inv2 = m2 + rows;
   float* dc = inv2 + rows;
   float* dt = dc + rows;
+  float* w1part = dt + rows;                               // [B][hidden][HW]
+  float* cpart = w1part + (size_t)B * hidden * HW;         // [chunks][3][hidden + 1]
   // forward quantities: affinity, clamp (and Z), logits, softmax / relu-softmax statistics
   if (int e = affinity(content, style, Aff, cn, sn, B, C, HW, st)) return e;
   if (int e = clamp_values(Aff, w1, b1, w2, b2, hidden, mode, from, interval, Z, clamp, B, HW,
@@ -976,11 +1012,20 @@ extern "C" int rpst_adaptive_attention_backward(
   fpsi_bwd_rows_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Z, w2, b2, dc, dt, du, rows,
                                                                    hidden, mode, interval);
   if (int e = launch_status("fpsi_bwd_rows_kernel")) return e;
-  GemmArgs gw{du, Aff, dw1, {}, nullptr, nullptr, 0, hidden, HW, (int)rows, hidden, HW, HW,
-              0, 0, 0, 0};
-  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gw, 1, st);
-  if (int e = launch_status("gemm_f32_kernel(dW1=du^T A)")) return e;
-  fpsi_colsum_kernel<<<(hidden + 1 + 255) / 256, 256, 0, st>>>(Z, du, dt, dw2, db1, db2, rows,
-                                                              hidden);
-  return launch_status("fpsi_colsum_kernel");
+  // dW1 = du^T Aff per image (a batched GEMM over B: K = HW each, instead of one GEMM with
+  // K = B * HW on HW / 128 workgroups), then the B partials summed in order
+  GemmArgs gw{du, Aff, w1part, {}, nullptr, nullptr, 0, hidden, HW, HW, hidden, HW, HW,
+              (int64_t)HW * hidden, hw2, (int64_t)hidden * HW, 0};
+  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gw, B, st);
+  if (int e = launch_status("gemm_f32_kernel(dW1_b=du_b^T A_b)")) return e;
+  const int64_t nw1 = (int64_t)hidden * HW;
+  batch_sum_kernel<<<(unsigned)((nw1 + 255) / 256), 256, 0, st>>>(w1part, dw1, nw1, B);
+  if (int e = launch_status("batch_sum_kernel(dW1)")) return e;
+  const int chunks = (int)((rows + kColChunk - 1) / kColChunk);
+  fpsi_colsum_part_kernel<<<dim3((unsigned)((hidden + 1 + 255) / 256), (unsigned)chunks), 256, 0,
+                            st>>>(Z, du, dt, cpart, rows, hidden);
+  if (int e = launch_status("fpsi_colsum_part_kernel")) return e;
+  fpsi_colsum_final_kernel<<<(hidden + 1 + 255) / 256, 256, 0, st>>>(cpart, dw2, db1, db2, chunks,
+                                                                    hidden);
+  return launch_status("fpsi_colsum_final_kernel");
 }
