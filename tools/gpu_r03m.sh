@@ -7,3 +7,7 @@ cat $O/wct_shapes.log
 timeout -k 10 200 python -u tools/bench_cov.py > $O/bench_cov.log 2>&1 || { tail $O/bench_cov.log; exit 1; }
 cat $O/bench_cov.log
 bash tools/prof_pmc_configs.sh r03m_pmc 2 || exit 1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_adain -o adain -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs > $O/prof_adain.log 2>&1 || exit 1
+timeout -k 10 300 python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs > $O/bench_for_prof.json 2>/dev/null || exit 1
+echo done

@@ -124,7 +124,7 @@ def main(fetch_dir, write_dir, order_path, out_path):
             f, w = tot(f_rows, True), tot(w_rows, False)
             kern = (f_rows or w_rows)[0][0]
             if sec == "wct":
-                kern = "cov_syrk(16)_kernel+cov_finish_kernel+matfun_kernel"
+                kern = "cov_syrk16_kernel+cov_finish_kernel+matfun_kernel"
             res[sec][key] = {"kernel": kern.split("(")[0], "dispatches": len(f_rows),
                              "fetch_bytes": f, "write_bytes": w, "traffic_bytes": f + w,
                              "fetch_correction": "x2 (16-B reads)" if (

@@ -18,6 +18,6 @@ for m in ${RUNS:-"--config 2" "--config 3" "--config 4" "--model multiscale" "--
   python -c "import json;d=json.load(open('$f'));r=d['roofline'];print('$m', d['value'], d['ms_per_step'], r['kernel'], r['frac'])"
 done
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_adain -o adain -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_adain.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_adain -o adain -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs > $O/prof_adain.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_wct -o wct -- python3 $R/bench.py --config 2 --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_wct.log 2>&1 || exit 1
 echo done
