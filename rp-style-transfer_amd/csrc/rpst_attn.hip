@@ -16,6 +16,7 @@
 // are lane-contiguous; global tiles are loaded with 16-B loads along whichever dim is
 // contiguous (RK: row-major rows with k contiguous; KR: k-rows with m/n contiguous).
 // Register prefetch of tile t+1 overlaps the MFMAs of tile t.
+#include <algorithm>
 #include <cstdlib>
 
 #include "rpst_common.h"
@@ -61,6 +62,9 @@ struct GemmArgs {
   int act;                // epilogue activation: 0 none, 1 LeakyReLU(0.2)
   int M, N, K, lda, ldb, ldc;
   int64_t sA, sB, sC, sV;  // batch strides (elements); sV for the row / column vectors
+  // In-kernel split-K (BX_NONE only): grid z = batch * ks, z -> (batch z / ks, K chunk z % ks
+  // of kc elements); C advances by sC per z, so each chunk writes its own partial.
+  int ks = 1, kc = 0;
 };
 
 template <int BX>
@@ -190,11 +194,19 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   constexpr int LDA = g_ld<ALAY, BMT>(), LDB = g_ld<BLAY>();
   __shared__ float As[kGBK * LDA];
   __shared__ float Bs[kGBK * LDB];
-  const int b = blockIdx.z;
+  int b = blockIdx.z, K = g.K;
+  int64_t koA = 0, koB = 0;
+  if (g.ks > 1) {
+    const int kb = (b % g.ks) * g.kc;
+    b /= g.ks;
+    K = min(g.kc, g.K - kb);
+    koA = ALAY == LAY_RK ? kb : (int64_t)kb * g.lda;
+    koB = BLAY == LAY_RK ? kb : (int64_t)kb * g.ldb;
+  }
   const int m0 = blockIdx.y * BMT, n0 = blockIdx.x * kGBN;
-  const float* A = g.A + b * g.sA;
-  const float* B = g.B + b * g.sB;
-  float* C = g.C + b * g.sC;
+  const float* A = g.A + b * g.sA + koA;
+  const float* B = g.B + b * g.sB + koB;
+  float* C = g.C + (int64_t)blockIdx.z * g.sC;
   const int64_t voff = (int64_t)b * g.sV;
   const float* cscale = g.colscale ? g.colscale + voff : nullptr;
 
@@ -211,11 +223,11 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
       for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
 
   float ra[MW][16], rb[16];
-  const int ktiles = (g.K + kGBK - 1) / kGBK;
+  const int ktiles = (K + kGBK - 1) / kGBK;
 #pragma unroll
   for (int i = 0; i < MW; ++i)
-    g_load<ALAY, BX_NONE, VECA>(ra[i], A, g.lda, m0 + 128 * i, 0, g.M, g.K, g.rv, 0, tid);
-  g_load<BLAY, BX, VECB>(rb, B, g.ldb, n0, 0, g.N, g.K, g.rv, voff, tid);
+    g_load<ALAY, BX_NONE, VECA>(ra[i], A, g.lda, m0 + 128 * i, 0, g.M, K, g.rv, 0, tid);
+  g_load<BLAY, BX, VECB>(rb, B, g.ldb, n0, 0, g.N, K, g.rv, voff, tid);
   for (int kt = 0; kt < ktiles; ++kt) {
 #pragma unroll
     for (int i = 0; i < MW; ++i) g_store<ALAY, LDA>(As + 128 * i, ra[i], tid);
@@ -224,9 +236,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
     if (kt + 1 < ktiles) {
 #pragma unroll
       for (int i = 0; i < MW; ++i)
-        g_load<ALAY, BX_NONE, VECA>(ra[i], A, g.lda, m0 + 128 * i, (kt + 1) * kGBK, g.M, g.K,
+        g_load<ALAY, BX_NONE, VECA>(ra[i], A, g.lda, m0 + 128 * i, (kt + 1) * kGBK, g.M, K,
                                     g.rv, 0, tid);
-      g_load<BLAY, BX, VECB>(rb, B, g.ldb, n0, (kt + 1) * kGBK, g.N, g.K, g.rv, voff, tid);
+      g_load<BLAY, BX, VECB>(rb, B, g.ldb, n0, (kt + 1) * kGBK, g.N, K, g.rv, voff, tid);
     }
 #pragma unroll
     for (int kk = 0; kk < kGBK / 2; ++kk) {
@@ -306,12 +318,12 @@ static void launch_gemm(const GemmArgs& g, int batch, hipStream_t st) {
     return e && *e ? std::atoi(e) : 0;
   }();
   const int mw = mw_env == 1 ? 1 : (g.M >= 256 ? 2 : 1);
-  dim3 grid((g.N + kGBN - 1) / kGBN, (g.M + 128 * mw - 1) / (128 * mw), batch);
+  dim3 grid((g.N + kGBN - 1) / kGBN, (g.M + 128 * mw - 1) / (128 * mw), batch * g.ks);
   auto aligned = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   // 16-B loads need the contiguous dim, the leading dim and the batch stride % 4 == 0
-  const bool va = aligned(g.A) && (g.lda % 4 == 0) && (g.sA % 4 == 0) &&
+  const bool va = aligned(g.A) && (g.lda % 4 == 0) && (g.sA % 4 == 0) && (g.kc % 4 == 0) &&
                   ((ALAY == LAY_KR) ? (g.M % 4 == 0) : (g.K % 4 == 0));
-  const bool vb = aligned(g.B) && (g.ldb % 4 == 0) && (g.sB % 4 == 0) &&
+  const bool vb = aligned(g.B) && (g.ldb % 4 == 0) && (g.sB % 4 == 0) && (g.kc % 4 == 0) &&
                   ((BLAY == LAY_KR) ? (g.N % 4 == 0) : (g.K % 4 == 0));
   if (mw == 2) {
     if (va && vb) gemm_f32_kernel<ALAY, BLAY, BX, true, true, 2><<<grid, 256, 0, st>>>(g);
@@ -894,9 +906,19 @@ extern "C" int rpst_sanet_attention_backward(const float* F, const float* G, con
   return launch_status("gemm_f32_kernel(dG=F dS)");
 }
 
+// K (pixel) chunks per image of the 1x1 weight gradient: the per-image GEMM has only
+// ceil(Cout/256) x ceil(Cin/128) tiles (8 for the SANet's 512 x 512 convs, 64 workgroups at
+// N = 8), so the pixels are split until the launch has ~512 workgroups (two per CU). A
+// function of the shape only: the fixed-order partial sum stays deterministic.
+static int wgrad1x1_ks(int N, int Cin, int Cout) {
+  const int64_t tiles = (int64_t)((Cout + 255) / 256) * ((Cin + 127) / 128) * N;
+  const int64_t ks = (512 + tiles - 1) / tiles;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(ks, 16));
+}
+
 extern "C" size_t rpst_conv1x1_wgrad_workspace_size(int N, int Cin, int Cout) {
   if (N <= 0 || Cin <= 0 || Cout <= 0) return 0;
-  return sizeof(float) * (size_t)N * Cin * Cout;
+  return sizeof(float) * (size_t)N * wgrad1x1_ks(N, Cin, Cout) * Cin * Cout;
 }
 
 extern "C" int rpst_conv1x1_wgrad(const float* x, const float* dy, float* dw, float* db, int N,
@@ -912,12 +934,17 @@ extern "C" int rpst_conv1x1_wgrad(const float* x, const float* dy, float* dw, fl
   hipStream_t st = as_stream(stream);
   float* part = static_cast<float*>(workspace);
   // part[n][co][ci] = sum_p dy[n][co][p] x[n][ci][p]
+  // part[n * ks + j][co][ci] = sum over pixel chunk j of dy[n][co][p] x[n][ci][p]; chunks of
+  // kc pixels (a multiple of 64, so at most ks of them and 16-B aligned)
+  const int ksmax = wgrad1x1_ks(N, Cin, Cout);
+  const int64_t kc = std::max<int64_t>(64, ((HW + ksmax - 1) / ksmax + 63) / 64 * 64);
+  const int ks = (int)((HW + kc - 1) / kc);
   GemmArgs g{dy, x, part, {}, nullptr, nullptr, 0, Cout, Cin, (int)HW, (int)HW, (int)HW, Cin,
-             (int64_t)Cout * HW, (int64_t)Cin * HW, (int64_t)Cout * Cin, 0};
+             (int64_t)Cout * HW, (int64_t)Cin * HW, (int64_t)Cout * Cin, 0, ks, (int)kc};
   launch_gemm<LAY_RK, LAY_RK, BX_NONE>(g, N, st);
   if (int e = launch_status("gemm_f32_kernel(dW=dY X^T)")) return e;
   const int64_t per = (int64_t)Cout * Cin;
-  batch_sum_kernel<<<(unsigned)((per + 255) / 256), 256, 0, st>>>(part, dw, per, N);
+  batch_sum_kernel<<<(unsigned)((per + 255) / 256), 256, 0, st>>>(part, dw, per, N * ks);
   if (int e = launch_status("batch_sum_kernel")) return e;
   if (db) {
     channel_sum_kernel<<<(Cout + 3) / 4, 256, 0, st>>>(dy, db, N, Cout, HW);

@@ -65,6 +65,24 @@ def test_conv_wgrad(cuda, shape):
     assert rel_l2(db, bd.grad) < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(8, 512, 64, 64, 512), (2, 512, 31, 33, 512), (1, 3, 5, 7, 5),
+                                   (3, 64, 1, 1, 130), (1, 130, 63, 65, 66), (2, 256, 8, 8, 512)])
+def test_conv1x1_wgrad(cuda, shape):
+    """1x1 weight / bias gradient (rpst_conv1x1_wgrad: per-image pixel chunks on the split-K
+    GEMM, fixed-order sum) vs float64: the SANet's 512 x 512 at relu4_1 training size, ragged
+    pixel counts (a partial last chunk), a single pixel, channels that are not multiples of 4."""
+    from rpst import autograd as A
+    n, cin, h, w, cout = shape
+    x = gen(6, (n, cin, h, w))
+    g = gen(7, (n, cout, h, w))
+    dw, db = A._lin_grads(g.to(cuda), x.to(cuda))
+    ref = torch.einsum("nop,nip->oi", g.double().flatten(2), x.double().flatten(2))
+    assert rel_l2(dw.flatten(1), ref) < 1e-5
+    assert rel_l2(db, g.double().sum((0, 2, 3))) < 1e-5
+    dw2, _ = A._lin_grads(g.to(cuda), x.to(cuda))
+    assert torch.equal(dw, dw2)
+
+
 @pytest.mark.parametrize("shape", [(2, 16, 12, 20, 32), (1, 3, 9, 7, 16), (2, 64, 33, 70, 40),
                                    (1, 8, 2, 2, 8), (1, 32, 16, 64, 24), (1, 16, 5, 132, 16),
                                    (1, 32, 5, 129, 3), (2, 32, 3, 256, 32), (1, 64, 6, 140, 3)])
