@@ -112,6 +112,15 @@ int rpst_conv2d_pair(const float* input, const float* input2, int n1, const floa
                      const float* bias, float* out, int N, int Cin, int Hs, int Ws, int Cout,
                      int ksize, int pad_mode, int relu, rpst_stream_t stream);
 
+/* Conv (in_op NONE, no activation) whose output is zeroed where mask <= 0 (mask has the
+ * output's shape): the input gradient of a conv whose input is a ReLU output y, dgrad and
+ * threshold_backward(., y) in one pass (torch.autograd's ConvolutionBackward + ReluBackward
+ * under total_loss.backward(), train.py:186-189). Bit-identical to rpst_conv2d followed by
+ * rpst_relu_backward; the F(4x4) path thresholds in a second pass. */
+int rpst_conv2d_masked(const float* input, const float* packed_weight, const float* bias,
+                       const float* mask, float* out, int N, int Cin, int Hs, int Ws, int Cout,
+                       int ksize, int pad_mode, rpst_stream_t stream);
+
 /* Same conv with a caller-provided workspace (rpst_conv2d_workspace_size bytes, 0 when the
  * layer needs none). With RPST_IN_ADAIN on the F(4x4) path the workspace holds per-image
  * weights with the AdaIN scale std_s/std_c folded in along Cin and a per-(n, co) bias by
@@ -277,6 +286,14 @@ size_t rpst_reflect_pad_border_grad_workspace_size(int N, int Cin, int H, int W)
 int rpst_reflect_pad_border_grad(const float* dy, const float* w, float* dx, int N, int Cin,
                                  int Cout, int H, int W, void* workspace, size_t workspace_bytes,
                                  rpst_stream_t stream);
+/* The same, for a conv whose input is a ReLU output y (mask = y, N x Cin x H x W): the border
+ * gradient is added only where y > 0, so with dx from rpst_conv2d_masked the result equals
+ * rpst_relu_backward(dgrad + border, y) bit for bit (threshold_backward fused, train.py:186-189
+ * backward through the decoders' Conv2d -> ReLU chains). mask may be NULL. */
+int rpst_reflect_pad_border_grad_masked(const float* dy, const float* w, const float* mask,
+                                        float* dx, int N, int Cin, int Cout, int H, int W,
+                                        void* workspace, size_t workspace_bytes,
+                                        rpst_stream_t stream);
 /* conv3x3 (stride 1, zero pad 1) weight / bias gradient: x (N,Cin,H,W) the conv input, dy
  * (N,Cout,H,W) the gradient at its output -> dw (Cout,Cin,3,3), db (Cout) (db may be NULL).
  * Workspace: rpst_conv_wgrad_workspace_size(N, Cin, H, W, Cout). */

@@ -37,6 +37,9 @@ struct ConvArgs {
   // (rpst_conv2d_pair: an encoder's first conv over [content; style] without the concat)
   const float* in2;
   int in2_from;
+  // optional ReLU-backward mask: out = mask > 0 ? v : 0 (rpst_conv2d_masked, the dgrad of a
+  // conv whose input is a ReLU output: threshold_backward fused into the epilogue)
+  const float* mask;
 };
 
 // image n's input planes (block-uniform n)

@@ -246,6 +246,7 @@ __global__ __launch_bounds__(NTH, 2) void conv_mfma_kernel(ConvArgs a) {
         if (y < a.H && x < a.W) {
           const int64_t o = pbase + (int64_t)y * a.W + x;
           if (a.res) v += a.res[o];
+          if (a.mask && !(a.mask[o] > 0.f)) v = 0.f;
           a.out[o] = v;
         }
         acc[mt][nt][r] = v;
@@ -500,6 +501,7 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
       const int64_t o = ((int64_t)n * a.Cout + co) * plane + (int64_t)y * a.W + x;
       float v = activate(acc[r][co] + (a.bias ? a.bias[co] : 0.f), a.relu);
       if (a.res) v += a.res[o];
+      if (a.mask && !(a.mask[o] > 0.f)) v = 0.f;
       a.out[o] = v;
     }
   }
@@ -777,20 +779,43 @@ extern "C" int rpst_conv2d_pack(const float* weight, float* packed, int Cout, in
   return RPST_OK;
 }
 
+// out = mask > 0 ? out : 0 in place (threshold_backward after a kernel without the mask
+// epilogue)
+__global__ __launch_bounds__(256) void mask_apply_kernel(float* __restrict__ out,
+                                                         const float* __restrict__ mask,
+                                                         int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i + 3 < n && ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(mask)) & 15) == 0) {
+    float4 v = *reinterpret_cast<float4*>(out + i);
+    const float4 m = *reinterpret_cast<const float4*>(mask + i);
+    if (!(m.x > 0.f)) v.x = 0.f;
+    if (!(m.y > 0.f)) v.y = 0.f;
+    if (!(m.z > 0.f)) v.z = 0.f;
+    if (!(m.w > 0.f)) v.w = 0.f;
+    *reinterpret_cast<float4*>(out + i) = v;
+  } else {
+    for (int64_t j = i; j < n && j < i + 4; ++j)
+      if (!(mask[j] > 0.f)) out[j] = 0.f;
+  }
+}
+
 static int conv_common(const float* input, const float* aux, const float* aux2,
                        const float* packed_weight,
                        const float* bias, const float* residual, float* out, int N, int Cin,
                        int Hs, int Ws, int Cout, int ksize, int pad_mode, int in_op, int relu,
                        float2* stat_part, int* stat_P, ConvArgs* args_out, hipStream_t st,
                        float* fold_ws = nullptr, int skip_from = 0,
-                       const float* in2 = nullptr, int in2_from = 0) {
+                       const float* in2 = nullptr, int in2_from = 0,
+                       const float* mask = nullptr) {
   RPST_REQUIRE(input && packed_weight && out, "conv2d: null pointer");
   RPST_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && Hs > 0 && Ws > 0, "conv2d: bad shape");
   RPST_REQUIRE(ksize == 1 || ksize == 3, "conv2d: ksize must be 1 or 3, got %d", ksize);
   RPST_REQUIRE(pad_mode == RPST_PAD_ZERO || pad_mode == RPST_PAD_REFLECT, "conv2d: bad pad");
   RPST_REQUIRE(in_op >= RPST_IN_NONE && in_op <= RPST_IN_ADD_ADAIN, "conv2d: bad in_op");
   RPST_REQUIRE(relu >= RPST_ACT_NONE && relu <= RPST_ACT_LRELU, "conv2d: bad activation %d", relu);
+  RPST_REQUIRE(!(mask && stat_part), "conv2d: the mask epilogue has no statistics");
   ConvArgs a{};
+  a.mask = mask;
   a.skip_from = skip_from;
   a.in = input;
   a.in2 = in2;
@@ -863,6 +888,11 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
       op = RPST_IN_NONE;
     }
     if (int e = wino4_launch(a, op, st)) return e;
+    if (mask) {  // F(4x4)'s epilogue has no mask: threshold the output in a second pass
+      const int64_t n = (int64_t)N * Cout * a.H * a.W;
+      mask_apply_kernel<<<(unsigned)((n + 1023) / 1024), 256, 0, st>>>(out, mask, n);
+      if (int e = launch_status("mask_apply_kernel")) return e;
+    }
     if (stat_P) *stat_P = a.stat_P;
     if (args_out) *args_out = a;
     return RPST_OK;
@@ -946,6 +976,16 @@ extern "C" int rpst_conv2d_pair(const float* input, const float* input2, int n1,
   return conv_common(input, nullptr, nullptr, packed_weight, bias, nullptr, out, N, Cin, Hs, Ws,
                      Cout, ksize, pad_mode, RPST_IN_NONE, relu, nullptr, nullptr, nullptr,
                      as_stream(stream), nullptr, 0, n1 < N ? input2 : nullptr, n1 < N ? n1 : 0);
+}
+
+extern "C" int rpst_conv2d_masked(const float* input, const float* packed_weight,
+                                  const float* bias, const float* mask, float* out, int N,
+                                  int Cin, int Hs, int Ws, int Cout, int ksize, int pad_mode,
+                                  rpst_stream_t stream) {
+  RPST_REQUIRE(mask, "conv2d_masked: null mask");
+  return conv_common(input, nullptr, nullptr, packed_weight, bias, nullptr, out, N, Cin, Hs, Ws,
+                     Cout, ksize, pad_mode, RPST_IN_NONE, RPST_ACT_NONE, nullptr, nullptr,
+                     nullptr, as_stream(stream), nullptr, 0, nullptr, 0, mask);
 }
 
 // workspace of the F(4x4) conv with RPST_IN_ADAIN folded into per-image weights (0 for

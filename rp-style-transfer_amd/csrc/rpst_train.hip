@@ -212,8 +212,8 @@ __global__ __launch_bounds__(256) void reflect_ring_kernel(
 }
 
 __global__ __launch_bounds__(256) void reflect_fold_kernel(
-    const float* __restrict__ ring, float* __restrict__ dx, int N, int Cin, int H, int W,
-    int nrows, int r0, int r1, int ncols, int c0, int c1) {
+    const float* __restrict__ ring, float* __restrict__ dx, const float* __restrict__ mask,
+    int N, int Cin, int H, int W, int nrows, int r0, int r1, int ncols, int c0, int c1) {
   const int64_t per = (int64_t)nrows * W + (int64_t)ncols * (H - nrows);
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)N * Cin * per) return;
@@ -249,8 +249,9 @@ __global__ __launch_bounds__(256) void reflect_fold_kernel(
   // padded columns q in {0, W+1} on the interior padded row p = i + 1
   if (refl(-1, W) == j) add += rg[2 * (W + 2) + i];
   if (refl(W, W) == j) add += rg[2 * (W + 2) + H + i];
-  float* d = dx + plane * H * W + (int64_t)i * W + j;
-  *d = *d + add;
+  const int64_t o = plane * H * W + (int64_t)i * W + j;
+  if (mask && !(mask[o] > 0.f)) return;  // threshold_backward: dx stays 0 there
+  dx[o] = dx[o] + add;
 }
 
 // ---- conv weight gradient (3x3, stride 1, zero pad 1) ---------------------------------------
@@ -602,6 +603,14 @@ extern "C" size_t rpst_reflect_pad_border_grad_workspace_size(int N, int Cin, in
 extern "C" int rpst_reflect_pad_border_grad(const float* dy, const float* w, float* dx, int N,
                                             int Cin, int Cout, int H, int W, void* workspace,
                                             size_t workspace_bytes, rpst_stream_t stream) {
+  return rpst_reflect_pad_border_grad_masked(dy, w, nullptr, dx, N, Cin, Cout, H, W, workspace,
+                                             workspace_bytes, stream);
+}
+
+extern "C" int rpst_reflect_pad_border_grad_masked(const float* dy, const float* w,
+                                                   const float* mask, float* dx, int N, int Cin,
+                                                   int Cout, int H, int W, void* workspace,
+                                                   size_t workspace_bytes, rpst_stream_t stream) {
   RPST_REQUIRE(dy && w && dx && N > 0 && Cin > 0 && Cout > 0, "reflect_border_grad: bad args");
   RPST_REQUIRE(H >= 2 && W >= 2, "reflect_border_grad: ReflectionPad2d(1) needs H, W >= 2");
   if (!workspace || workspace_bytes < rpst_reflect_pad_border_grad_workspace_size(N, Cin, H, W)) {
@@ -619,7 +628,7 @@ extern "C" int rpst_reflect_pad_border_grad(const float* dy, const float* w, flo
   const int nrows = (r0 == r1) ? 1 : 2, ncols = (c0 == c1) ? 1 : 2;
   const int64_t per = (int64_t)nrows * W + (int64_t)ncols * (H - nrows);
   reflect_fold_kernel<<<blocks_for((int64_t)N * Cin * per), 256, 0, st>>>(
-      ring, dx, N, Cin, H, W, nrows, r0, r1, ncols, c0, c1);
+      ring, dx, mask, N, Cin, H, W, nrows, r0, r1, ncols, c0, c1);
   return launch_status("reflect_fold_kernel");
 }
 

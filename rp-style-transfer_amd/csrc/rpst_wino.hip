@@ -377,7 +377,15 @@ __global__ __launch_bounds__(kWinoNTH, 2) void wino_mfma_kernel(ConvArgs a) {
           y[e] += b;
           y[e] = activate(y[e], a.relu);
         }
-        float* o = a.out + (((int64_t)n * a.Cout + co) * a.H + gy) * a.W + gx;
+        const int64_t off = (((int64_t)n * a.Cout + co) * a.H + gy) * a.W + gx;
+        float* o = a.out + off;
+        if (a.mask) {
+          const float* mk = a.mask + off;
+          if (vy0 && vx0 && !(mk[0] > 0.f)) y[0] = 0.f;
+          if (vy0 && vx1 && !(mk[1] > 0.f)) y[1] = 0.f;
+          if (vy1 && vx0 && !(mk[a.W] > 0.f)) y[2] = 0.f;
+          if (vy1 && vx1 && !(mk[a.W + 1] > 0.f)) y[3] = 0.f;
+        }
         if (vec) {
           if (vy0) *reinterpret_cast<float2*>(o) = make_float2(y[0], y[1]);
           if (vy1) *reinterpret_cast<float2*>(o + a.W) = make_float2(y[2], y[3]);

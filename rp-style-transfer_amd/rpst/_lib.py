@@ -41,6 +41,7 @@ SIGNATURES = {
     "rpst_conv2d_stats_store": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I,
                                      _I, _P, _P, _F, _I, _P, _SZ, _P]),
     "rpst_conv2d": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "rpst_conv2d_masked": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_conv2d_pair": (_I, [_P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_conv2d_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),
     "rpst_conv2d_ws": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I,
@@ -57,6 +58,8 @@ SIGNATURES = {
     "rpst_maxpool2x2_ceil_backward": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "rpst_reflect_pad_border_grad_workspace_size": (_SZ, [_I, _I, _I, _I]),
     "rpst_reflect_pad_border_grad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
+    "rpst_reflect_pad_border_grad_masked": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ,
+                                                 _P]),
     "rpst_conv_wgrad_workspace_size": (_SZ, [_I, _I, _I, _I, _I]),
     "rpst_conv_wgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P]),
     "rpst_conv_wgrad_pad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _SZ, _P]),

@@ -24,7 +24,7 @@ Backward:
 """
 from __future__ import annotations
 
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -63,20 +63,36 @@ def relu_backward(g: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def conv_dgrad(g: torch.Tensor, step: plan.ConvStep) -> torch.Tensor:
+def conv_dgrad(g: torch.Tensor, step: plan.ConvStep,
+               mask: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Gradient at the conv's input (after its input operator) from g at its output
-    (pre-activation)."""
+    (pre-activation). mask: the conv's input when it is a ReLU output; the ReLU backward
+    (relu_backward(dx, mask)) is then fused into the dgrad conv and the border fold, bit for
+    bit (rpst_conv2d_masked, rpst_reflect_pad_border_grad_masked)."""
     c = step.conv
     k = c.kernel_size[0]
-    dx = ops.conv2d(g, flip_packed_weight(c), None, c.in_channels, k, pad=ops.PAD_ZERO)
+    if mask is None:
+        dx = ops.conv2d(g, flip_packed_weight(c), None, c.in_channels, k, pad=ops.PAD_ZERO)
+    else:
+        dx = ops.conv2d_masked(g, flip_packed_weight(c), c.in_channels, k, mask)
     if k == 3 and step.pad == ops.PAD_REFLECT:
         n, _, h, w = g.shape
         wd = c.weight.detach().contiguous()
         nbytes = _lib.load().rpst_reflect_pad_border_grad_workspace_size(n, c.in_channels, h, w)
         ws = _ws(nbytes, g)
-        _lib.call("rpst_reflect_pad_border_grad", g.data_ptr(), wd.data_ptr(), dx.data_ptr(),
-                  n, c.in_channels, c.out_channels, h, w, ws.data_ptr(), nbytes, _stream(g))
+        _lib.call("rpst_reflect_pad_border_grad_masked", g.data_ptr(), wd.data_ptr(),
+                  None if mask is None else mask.data_ptr(), dx.data_ptr(), n, c.in_channels,
+                  c.out_channels, h, w, ws.data_ptr(), nbytes, _stream(g))
     return dx
+
+
+def _relu_mask(steps, saved, k: int, ok: bool = True) -> Optional[torch.Tensor]:
+    """The ReLU output that step k's input gradient is thresholded by, when step k - 1 ends
+    in a plain ReLU feeding step k directly (no input operator between) and ok; else None."""
+    if not ok or k == 0 or steps[k - 1].relu != ops.ACT_RELU or steps[k].in_op != ops.IN_NONE:
+        return None
+    y = saved[k - 1][1]
+    return y if y.is_contiguous() else None
 
 
 def maxpool_backward(x: torch.Tensor, g: torch.Tensor, relu_mask: bool) -> torch.Tensor:
@@ -128,17 +144,21 @@ def _run_steps_saving(steps, x):
 
 def _rp_backward(steps, saved, g, grads: Dict[int, torch.Tensor], need_input_grad: bool):
     """Backward through an RP stack (zero-padded 3x3 convs + ReLU)."""
+    masked = False  # g already thresholded by step k's ReLU (fused into the dgrad above)
     for k in range(len(steps) - 1, -1, -1):
         s = steps[k]
         x_in, y = saved[k]
-        if s.relu:
+        if s.relu and not masked:
             g = relu_backward(g, y)
         dw, db = conv_wgrad(x_in, g, s.conv)
         grads[id(s.conv.weight)] = dw
         if db is not None:
             grads[id(s.conv.bias)] = db
+        masked = False
         if k > 0 or need_input_grad:
-            g = conv_dgrad(g, s)
+            mask = _relu_mask(steps, saved, k)
+            g = conv_dgrad(g, s, mask)
+            masked = mask is not None
     return g
 
 
@@ -191,6 +211,7 @@ class _VGGLoss:
         wts = torch.stack([w_s, w_c]).to(torch.float32).contiguous()
         vs, vsv, taps = self.steps, self.saved, self.taps
         g = None
+        masked = False
         for k in range(len(vs) - 1, -1, -1):
             x_in, y = vsv[k]
             if k in taps:
@@ -204,9 +225,12 @@ class _VGGLoss:
                           self.content4.data_ptr() if i == 3 else None, self.stats[i].data_ptr(),
                           wts.data_ptr(), g.data_ptr(), planes, hw, acc, _stream(y))
             s = vs[k]
-            if s.relu:
+            if s.relu and not masked:
                 g = relu_backward(g, y)
-            g = conv_dgrad(g, s)
+            # (a tap's loss seed is added before its ReLU backward: no fusion into a tap)
+            mask = _relu_mask(vs, vsv, k, ok=(k - 1) not in taps)
+            g = conv_dgrad(g, s, mask)
+            masked = mask is not None
             if s.in_op == ops.IN_MAXPOOL2:
                 g = maxpool_backward(x_in, g, relu_mask=False)
             elif s.in_op != ops.IN_NONE:
@@ -399,6 +423,7 @@ def _vgg_backward(steps, saved, taps, seed_fn):
     """d input from seeds at the taps: seed_fn(level, F, g) returns the tap gradient with
     the level's loss terms added into g (g None: a fresh tensor)."""
     g = None
+    masked = False
     for k in range(len(steps) - 1, -1, -1):
         x_in, y = saved[k]
         if k in taps:
@@ -406,9 +431,11 @@ def _vgg_backward(steps, saved, taps, seed_fn):
         if g is None:
             continue
         s = steps[k]
-        if s.relu:
+        if s.relu and not masked:
             g = relu_backward(g, y)
-        g = conv_dgrad(g, s)
+        mask = _relu_mask(steps, saved, k, ok=(k - 1) not in taps)
+        g = conv_dgrad(g, s, mask)
+        masked = mask is not None
         if s.in_op == ops.IN_MAXPOOL2:
             g = maxpool_backward(x_in, g, relu_mask=False)
         elif s.in_op != ops.IN_NONE:
@@ -419,10 +446,11 @@ def _vgg_backward(steps, saved, taps, seed_fn):
 def _decoder_backward(steps, saved, g, grads, need_input_grad: bool = True):
     """Decoder (sanet.py:162-192: reflect-pad conv3x3 + ReLU, nearest x2 upsample fused
     into the next conv's loader): parameter gradients into grads, returns d input."""
+    masked = False
     for k in range(len(steps) - 1, -1, -1):
         s = steps[k]
         x_in, y = saved[k]
-        if s.relu:
+        if s.relu and not masked:
             g = relu_backward(g, y)
         up = s.in_op == ops.IN_UPSAMPLE2
         if not up and s.in_op != ops.IN_NONE:
@@ -433,7 +461,9 @@ def _decoder_backward(steps, saved, g, grads, need_input_grad: bool = True):
         _acc(grads, s.conv.bias, db)
         if k == 0 and not need_input_grad:
             return None
-        g = conv_dgrad(g, s)
+        mask = _relu_mask(steps, saved, k)
+        g = conv_dgrad(g, s, mask)
+        masked = mask is not None
         if up:
             g = _upsample_backward(g)
     return g

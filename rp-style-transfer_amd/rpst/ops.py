@@ -277,6 +277,23 @@ def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], 
     return out
 
 
+def conv2d_masked(x: torch.Tensor, packed: torch.Tensor, cout: int, ksize: int,
+                  mask: torch.Tensor, pad: int = PAD_ZERO) -> torch.Tensor:
+    """out = conv_k(x), zeroed where mask <= 0 (rpst_conv2d_masked): a conv dgrad fused with
+    the ReLU backward of the layer before it (mask = that ReLU's output)."""
+    _check(x, packed, mask)
+    x, mask = _c(x), _c(mask)
+    n, cin, h, w = x.shape
+    assert tuple(mask.shape) == (n, cout, h, w)
+    out = torch.empty((n, cout, h, w), device=x.device, dtype=torch.float32)
+    with _traced(_conv_name(ksize, cin, cout, h, w, n, IN_NONE),
+                 2.0 * n * cout * h * w * cin * ksize * ksize,
+                 4.0 * (x.numel() + 2 * n * cout * h * w)):
+        _lib.call("rpst_conv2d_masked", x.data_ptr(), packed.data_ptr(), None, mask.data_ptr(),
+                  out.data_ptr(), n, cin, h, w, cout, ksize, pad, _stream(x))
+    return out
+
+
 def conv2d_skip_adain(x: torch.Tensor, content: torch.Tensor, params: torch.Tensor,
                       packed: torch.Tensor, bias: Optional[torch.Tensor], cout: int,
                       ksize: int = 3, pad: int = PAD_REFLECT, relu=ACT_LRELU,

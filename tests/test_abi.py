@@ -78,6 +78,14 @@ def test_conv2d_pair_argument_errors(n1, n, msg):
     assert msg in lib.rpst_last_error().decode()
 
 
+def test_conv2d_masked_argument_errors():
+    """rpst_conv2d_masked needs its mask, and the mask epilogue carries no statistics."""
+    lib = _lib.load()
+    st = lib.rpst_conv2d_masked(1, 1, None, None, 1, 2, 16, 8, 8, 16, 3, 0, None)
+    assert st == -1
+    assert "null mask" in lib.rpst_last_error().decode()
+
+
 def test_adain_workspace_error():
     lib = _lib.load()
     st = lib.rpst_adain(1, 1, 1, 2, 3, 16, ctypes.c_float(1e-5), 1, 8, None)

@@ -226,6 +226,33 @@ def test_conv2d_pair_matches_concat(cuda, case, conv_algo):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("case", [
+    (2, 64, 20, 72, 64, 0),    # direct / Winograd dgrad, zero pad
+    (2, 64, 20, 72, 64, 1),    # reflect pad: masked border fold
+    (1, 3, 17, 70, 16, 1),     # 16 -> 3 dgrad (narrow kernel), reflect, ragged
+    (2, 16, 9, 7, 3, 0),       # 3 -> 16 dgrad, tiny planes
+    (1, 32, 33, 40, 8, 1),
+])
+def test_conv_dgrad_masked_matches_relu_backward(cuda, case, conv_algo):
+    """rpst_conv2d_masked + rpst_reflect_pad_border_grad_masked (the ReLU backward fused into
+    a dgrad) are bit-identical to the dgrad followed by rpst_relu_backward, on every
+    algorithm (F(4x4) thresholds in a second pass)."""
+    from rpst import autograd as A
+    from rpst import ops, plan
+    n, cin, h, w_, cout, pad = case  # forward conv cin -> cout; the dgrad maps cout -> cin
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=1 if pad == 0 else 0)
+    with torch.no_grad():
+        conv.weight.copy_(gen(44, conv.weight.shape, (2.0 / (cin * 9)) ** 0.5))
+    step = plan.ConvStep(conv.to(cuda), ops.PAD_ZERO if pad == 0 else ops.PAD_REFLECT,
+                         ops.IN_NONE, ops.ACT_NONE)
+    g = gen(45, (n, cout, h, w_)).to(cuda)
+    y = torch.relu(gen(46, (n, cin, h, w_))).to(cuda)  # a ReLU output, about half zeros
+    ref = A.relu_backward(A.conv_dgrad(g, step), y)
+    out = A.conv_dgrad(g, step, mask=y)
+    assert torch.equal(out, ref)
+    assert (out[y <= 0] == 0).all()
+
+
 def test_conv2d_residual_3x3_every_algorithm(cuda, conv_algo):
     """A 3x3 conv with a residual runs on a kernel with the residual epilogue whatever
     algorithm the layer would otherwise take (the Winograd kernels have none)."""
