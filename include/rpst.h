@@ -112,6 +112,17 @@ int rpst_conv2d_pair(const float* input, const float* input2, int n1, const floa
                      const float* bias, float* out, int N, int Cin, int Hs, int Ws, int Cout,
                      int ksize, int pad_mode, int relu, rpst_stream_t stream);
 
+/* Conv whose output only feeds a 2x2 max pool (VGG relu1_2 / relu2_2 / relu3_4 -> MaxPool2d
+ * (2, 2, ceil_mode=True) -> next conv, network/base.py vgg, sanet.py:195-199 enc_2..enc_5):
+ * out (N, Cout, (H+1)/2, (W+1)/2) = max_pool2d(act(conv(in_op(input)) + bias)), the pool
+ * taken on the finished output tiles in the F(4x4) epilogue, so the full-resolution map is
+ * never written. Bit-identical to rpst_conv2d followed by rpst_maxpool2x2_ceil. Only for
+ * layers whose rpst_conv2d_algorithm is RPST_CONV_WINOGRAD4 (RPST_EINVAL otherwise: run
+ * the two calls). */
+int rpst_conv2d_pool(const float* input, const float* aux, const float* packed_weight,
+                     const float* bias, float* out, int N, int Cin, int Hs, int Ws, int Cout,
+                     int ksize, int pad_mode, int in_op, int relu, rpst_stream_t stream);
+
 /* Conv (in_op NONE, no activation) whose output is zeroed where mask <= 0 (mask has the
  * output's shape): the input gradient of a conv whose input is a ReLU output y, dgrad and
  * threshold_backward(., y) in one pass (torch.autograd's ConvolutionBackward + ReluBackward

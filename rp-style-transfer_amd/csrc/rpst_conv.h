@@ -40,6 +40,9 @@ struct ConvArgs {
   // optional ReLU-backward mask: out = mask > 0 ? v : 0 (rpst_conv2d_masked, the dgrad of a
   // conv whose input is a ReLU output: threshold_backward fused into the epilogue)
   const float* mask;
+  // F(4x4) only: out holds max_pool2d(., 2, 2, ceil_mode=True) of the result, planes of
+  // ((H + 1) / 2, (W + 1) / 2) (rpst_conv2d_pool: a conv whose output only feeds a pool)
+  int pool_out;
 };
 
 // image n's input planes (block-uniform n)

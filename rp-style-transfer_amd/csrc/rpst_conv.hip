@@ -806,7 +806,7 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
                        float2* stat_part, int* stat_P, ConvArgs* args_out, hipStream_t st,
                        float* fold_ws = nullptr, int skip_from = 0,
                        const float* in2 = nullptr, int in2_from = 0,
-                       const float* mask = nullptr) {
+                       const float* mask = nullptr, int pool_out = 0) {
   RPST_REQUIRE(input && packed_weight && out, "conv2d: null pointer");
   RPST_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && Hs > 0 && Ws > 0, "conv2d: bad shape");
   RPST_REQUIRE(ksize == 1 || ksize == 3, "conv2d: ksize must be 1 or 3, got %d", ksize);
@@ -814,8 +814,11 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   RPST_REQUIRE(in_op >= RPST_IN_NONE && in_op <= RPST_IN_ADD_ADAIN, "conv2d: bad in_op");
   RPST_REQUIRE(relu >= RPST_ACT_NONE && relu <= RPST_ACT_LRELU, "conv2d: bad activation %d", relu);
   RPST_REQUIRE(!(mask && stat_part), "conv2d: the mask epilogue has no statistics");
+  RPST_REQUIRE(!(pool_out && (stat_part || mask || residual)),
+               "conv2d: the pooled output has no statistics / mask / residual epilogue");
   ConvArgs a{};
   a.mask = mask;
+  a.pool_out = pool_out;
   a.skip_from = skip_from;
   a.in = input;
   a.in2 = in2;
@@ -878,6 +881,9 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
   // kernels only
   if (residual && (algo == RPST_CONV_WINOGRAD || algo == RPST_CONV_WINOGRAD4))
     algo = RPST_CONV_DIRECT;
+  RPST_REQUIRE(!pool_out || algo == RPST_CONV_WINOGRAD4,
+               "conv2d_pool: the pooled-output epilogue exists on the F(4x4) path only "
+               "(rpst_conv2d_algorithm == RPST_CONV_WINOGRAD4)");
   if (algo == RPST_CONV_WINOGRAD4) {
     a.wpk = packed_weight + direct_packed_floats(Cout, Cin, ksize) + wino_packed_floats(Cout, Cin);
     a.stat_part = stat_part;
@@ -986,6 +992,16 @@ extern "C" int rpst_conv2d_masked(const float* input, const float* packed_weight
   return conv_common(input, nullptr, nullptr, packed_weight, bias, nullptr, out, N, Cin, Hs, Ws,
                      Cout, ksize, pad_mode, RPST_IN_NONE, RPST_ACT_NONE, nullptr, nullptr,
                      nullptr, as_stream(stream), nullptr, 0, nullptr, 0, mask);
+}
+
+extern "C" int rpst_conv2d_pool(const float* input, const float* aux, const float* packed_weight,
+                                const float* bias, float* out, int N, int Cin, int Hs, int Ws,
+                                int Cout, int ksize, int pad_mode, int in_op, int relu,
+                                rpst_stream_t stream) {
+  RPST_REQUIRE(in_op != RPST_IN_ADD_ADAIN, "conv2d_pool: ADD_ADAIN has no pooled form");
+  return conv_common(input, aux, nullptr, packed_weight, bias, nullptr, out, N, Cin, Hs, Ws,
+                     Cout, ksize, pad_mode, in_op, relu, nullptr, nullptr, nullptr,
+                     as_stream(stream), nullptr, 0, nullptr, 0, nullptr, 1);
 }
 
 // workspace of the F(4x4) conv with RPST_IN_ADAIN folded into per-image weights (0 for

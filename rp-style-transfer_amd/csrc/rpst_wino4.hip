@@ -207,7 +207,7 @@ int wino4_rows(int Cin, int Cout) {
 // what the F(4x4) epilogue needs besides the tile (wino4_mfma_kernel's epi_ctx)
 struct EpiCtx {
   int W, H, Cout, gy0, gx0, rows, n, sidx, statP;
-  bool vec, full, bst, edge, store;
+  bool vec, full, bst, edge, store, pool;
   float inv, slope;      // slope: the activation as max(y, slope y): 0 ReLU, 0.2 LReLU, 1 none
   unsigned voff[4];      // bst: byte offset of output row yy inside a channel plane (or OOB)
   float* out;
@@ -651,7 +651,8 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
     // out-of-range offset, so no store needs a mask) when the float4 path applies to every
     // lane of the layer and one image's output fits 2^31 bytes
     const int64_t plane = (int64_t)e.H * e.W;
-    e.bst = (e.W & 3) == 0 && (int64_t)e.Cout * plane * 4 < (1LL << 31);
+    e.pool = L->pool_out != 0;
+    e.bst = !e.pool && (e.W & 3) == 0 && (int64_t)e.Cout * plane * 4 < (1LL << 31);
     e.oimg = e.out + (int64_t)e.n * e.Cout * plane;
     // images past a.skip_from: statistics only, every store out of range (dropped)
     const bool keep = L->skip_from <= 0 || e.n < L->skip_from;
@@ -724,6 +725,36 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
         const floatx4 v = {Y[yy * 4], Y[yy * 4 + 1], Y[yy * 4 + 2], Y[yy * 4 + 3]};
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro,
                                                (int)(e.voff[yy] + cofs), 0, 0);
+      }
+    } else if (e.pool) {
+      // max_pool2d(2, 2, ceil_mode) of the finished tile: tiles start on even rows and
+      // columns, so each holds whole windows; fmaxf in the stand-alone kernel's order
+      // (maxpool2_kernel), windows cut by the image edge take their in-image elements
+      if (cok && e.store) {
+        const int Ho = (e.H + 1) >> 1, Wo = (e.W + 1) >> 1;
+        float* o = e.out + (((int64_t)n * e.Cout + co) * Ho + (gy0 >> 1)) * Wo + (gx0 >> 1);
+#pragma unroll
+        for (int py = 0; py < 2; ++py) {
+          if (2 * py >= rows) continue;
+          const bool y1 = 2 * py + 1 < rows;
+          float pv[2];
+#pragma unroll
+          for (int px = 0; px < 2; ++px) {
+            const bool x1 = gx0 + 2 * px + 1 < e.W;
+            const float* t = Y + (2 * py) * 4 + 2 * px;
+            float v = t[0];
+            if (x1) v = fmaxf(v, t[1]);
+            if (y1) v = fmaxf(v, t[4]);
+            if (x1 && y1) v = fmaxf(v, t[5]);
+            pv[px] = v;
+          }
+          if (gx0 + 3 < e.W && (Wo & 1) == 0) {
+            *reinterpret_cast<float2*>(o + py * Wo) = make_float2(pv[0], pv[1]);
+          } else {
+            if (gx0 < e.W) o[py * Wo] = pv[0];
+            if (gx0 + 2 < e.W) o[py * Wo + 1] = pv[1];
+          }
+        }
       }
     } else if (cok && e.store) {
       float* o = e.out + (((int64_t)n * e.Cout + co) * e.H + gy0) * e.W + gx0;

@@ -41,6 +41,7 @@ SIGNATURES = {
     "rpst_conv2d_stats_store": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I,
                                      _I, _P, _P, _F, _I, _P, _SZ, _P]),
     "rpst_conv2d": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "rpst_conv2d_pool": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_conv2d_masked": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_conv2d_pair": (_I, [_P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_conv2d_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),

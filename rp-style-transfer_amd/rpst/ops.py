@@ -203,11 +203,12 @@ class precise_convs:
         return False
 
 
-def pool_pass_pays(x: torch.Tensor, cout: int, ksize: int) -> bool:
-    """For a conv whose input is max_pool2d(x, 2, 2, ceil_mode=True): True when the library
-    would run the pooled map's conv as F(4x4,3x3) (measured: pool pass + F(4x4) is faster
-    than the F(2x2) conv with the pool fused into its loader, profiles/r01_bench_sanet_w4*)."""
-    n, cin, h, w = x.shape
+def pool_pass_pays(x, cout: int, ksize: int) -> bool:
+    """For a conv whose input is max_pool2d(x, 2, 2, ceil_mode=True) (x a tensor or its
+    shape): True when the library would run the pooled map's conv as F(4x4,3x3) (measured:
+    pool pass + F(4x4) is faster than the F(2x2) conv with the pool fused into its loader,
+    profiles/r01_bench_sanet_w4*)."""
+    n, cin, h, w = tuple(x.shape) if isinstance(x, torch.Tensor) else tuple(x)
     return ksize == 3 and _lib.load().rpst_conv2d_algorithm(
         cout, cin, (h + 1) // 2, (w + 1) // 2, ksize, IN_NONE) == 2
 
@@ -274,6 +275,38 @@ def conv2d(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], 
                       _ptr(None if bias is None else _c(bias.detach())), _ptr(residual),
                       out.data_ptr(), n, cin, hs, ws, cout, ksize, pad, in_op, _act(relu),
                       _stream(x))
+    return out
+
+
+def conv2d_pool_fuses(x: torch.Tensor, cout: int, ksize: int, in_op: int = IN_NONE) -> bool:
+    """True when the library runs this conv on F(4x4), whose epilogue can write the output
+    max-pooled (rpst_conv2d_pool)."""
+    if os.environ.get("RPST_POOL_EPILOGUE", "") == "0":  # A/B switch: the separate pool pass
+        return False
+    n, cin, hs, ws = x.shape
+    return in_op in (IN_NONE, IN_ADAIN, IN_UPSAMPLE2) and _lib.load().rpst_conv2d_algorithm(
+        cout, cin, hs, ws, ksize, in_op) == 2
+
+
+def conv2d_pool(x: torch.Tensor, packed: torch.Tensor, bias: Optional[torch.Tensor], cout: int,
+                ksize: int, pad: int = PAD_ZERO, in_op: int = IN_NONE,
+                relu: bool = False) -> torch.Tensor:
+    """max_pool2d(conv2d(x), 2, 2, ceil_mode=True) with the pool in the F(4x4) epilogue
+    (rpst_conv2d_pool; the full-resolution output is never written). Needs
+    conv2d_pool_fuses(x, cout, ksize, in_op)."""
+    assert x.dim() == 4 and in_op in (IN_NONE, IN_UPSAMPLE2)
+    _check(x, packed, bias, None, None)
+    x = _c(x)
+    n, cin, hs, ws = x.shape
+    h, w = conv_out_hw(hs, ws, in_op)
+    out = torch.empty((n, cout, (h + 1) // 2, (w + 1) // 2), device=x.device,
+                      dtype=torch.float32)
+    with _traced(_conv_name(ksize, cin, cout, hs, ws, n, in_op),
+                 2.0 * n * cout * h * w * cin * ksize * ksize,
+                 4.0 * (x.numel() + out.numel())):
+        _lib.call("rpst_conv2d_pool", x.data_ptr(), None, packed.data_ptr(),
+                  _ptr(None if bias is None else _c(bias.detach())), out.data_ptr(), n, cin,
+                  hs, ws, cout, ksize, pad, in_op, _act(relu), _stream(x))
     return out
 
 

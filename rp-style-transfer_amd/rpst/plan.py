@@ -171,6 +171,7 @@ def run(steps: List[object], x: torch.Tensor, first_aux=None, first_in_op=None,
         raise NotImplementedError("rpst plan: first_mix needs a conv as the plan's first step")
     if first_in_op is not None and (not steps or not isinstance(steps[0], ConvStep)):
         raise NotImplementedError("rpst plan: first_in_op needs a conv as the plan's first step")
+    pooled_in = False  # step i's input was max-pooled by step i - 1's epilogue
     for i, s in enumerate(steps):
         if isinstance(s, ConvStep) and i == 0 and first_mix is not None:
             if s.in_op != ops.IN_NONE or (stats_last and len(steps) == 1):
@@ -186,11 +187,28 @@ def run(steps: List[object], x: torch.Tensor, first_aux=None, first_in_op=None,
                     raise NotImplementedError("rpst plan: first conv already has an input op")
                 in_op, aux = first_in_op, first_aux
             c = s.conv
-            if in_op == ops.IN_MAXPOOL2 and ops.pool_pass_pays(x, c.out_channels,
-                                                               c.kernel_size[0]):
+            if in_op == ops.IN_MAXPOOL2 and pooled_in:
+                in_op = ops.IN_NONE
+            elif in_op == ops.IN_MAXPOOL2 and ops.pool_pass_pays(x, c.out_channels,
+                                                                 c.kernel_size[0]):
                 # F(4x4,3x3) has no max-pool loader: a separate pool pass (one read of the
                 # source, one write of the pooled map) + F(4x4) beats the fused F(2x2)
                 x, in_op = ops.maxpool2x2_ceil(x), ops.IN_NONE
+            pooled_in = False
+            nxt = steps[i + 1] if i + 1 < len(steps) else None
+            if (isinstance(nxt, ConvStep) and nxt.in_op == ops.IN_MAXPOOL2
+                    and in_op in (ops.IN_NONE, ops.IN_UPSAMPLE2)
+                    and not (stats_last and i == len(steps) - 1)
+                    and ops.conv2d_pool_fuses(x, c.out_channels, c.kernel_size[0], in_op)):
+                h, w = ops.conv_out_hw(x.shape[2], x.shape[3], in_op)
+                y_shape = (x.shape[0], c.out_channels, h, w)
+                if ops.pool_pass_pays(y_shape, nxt.conv.out_channels, nxt.conv.kernel_size[0]):
+                    # this conv's output only feeds the next conv's pool pass: write it
+                    # pooled from the F(4x4) epilogue (never the full-resolution map)
+                    x = ops.conv2d_pool(x, packed_weight(c), c.bias, c.out_channels,
+                                        c.kernel_size[0], pad=s.pad, in_op=in_op, relu=s.relu)
+                    pooled_in = True
+                    continue
             if in_op == ops.IN_ADD_ADAIN:
                 if stats_last and i == len(steps) - 1:
                     raise NotImplementedError("rpst plan: skip-AdaIN conv with statistics")

@@ -86,6 +86,15 @@ def test_conv2d_masked_argument_errors():
     assert "null mask" in lib.rpst_last_error().decode()
 
 
+def test_conv2d_pool_needs_the_f4x4_path():
+    """rpst_conv2d_pool refuses a layer the library would not run on F(4x4) (a 3-channel
+    input conv), before any launch."""
+    lib = _lib.load()
+    st = lib.rpst_conv2d_pool(1, None, 1, None, 1, 1, 3, 16, 16, 16, 3, 0, 0, 1, None)
+    assert st == -1
+    assert "F(4x4)" in lib.rpst_last_error().decode()
+
+
 def test_adain_workspace_error():
     lib = _lib.load()
     st = lib.rpst_adain(1, 1, 1, 2, 3, 16, ctypes.c_float(1e-5), 1, 8, None)

@@ -253,6 +253,58 @@ def test_conv_dgrad_masked_matches_relu_backward(cuda, case, conv_algo):
     assert (out[y <= 0] == 0).all()
 
 
+@pytest.mark.parametrize("case", [
+    (2, 64, 40, 72, 64, 1, 0, True),     # VGG relu1_2-like, reflect
+    (1, 32, 37, 70, 48, 1, 0, True),     # odd height: ceil-mode windows cut by the edge
+    (2, 16, 33, 65, 32, 0, 0, True),     # NR = 2 block (Cin * Cout <= 512), odd width
+    (1, 64, 18, 22, 64, 0, 0, False),    # no activation
+    (1, 32, 10, 17, 32, 1, 2, True),     # nearest-upsample loader
+])
+def test_conv2d_pool_matches_conv_then_pool(cuda, case, monkeypatch):
+    """rpst_conv2d_pool (the 2x2 ceil-mode max pool taken in the F(4x4) epilogue) is
+    bit-identical to rpst_conv2d followed by rpst_maxpool2x2_ceil."""
+    from rpst import ops
+    monkeypatch.setenv("RPST_CONV_ALGO", "winograd4")
+    n, cin, h, w_, cout, pad, in_op, relu = case
+    x = gen(47, (n, cin, h, w_), 1.0, -0.2).to(cuda)
+    wt = gen(48, (cout, cin, 3, 3), (2.0 / (cin * 9)) ** 0.5).to(cuda)
+    b = gen(49, (cout,), 0.05).to(cuda)
+    pk = ops.pack_conv_weight(wt)
+    assert ops.conv2d_pool_fuses(x, cout, 3, in_op)
+    ref = ops.maxpool2x2_ceil(ops.conv2d(x, pk, b, cout, 3, pad=pad, in_op=in_op, relu=relu))
+    out = ops.conv2d_pool(x, pk, b, cout, 3, pad=pad, in_op=in_op, relu=relu)
+    assert out.shape == ref.shape
+    assert torch.equal(out, ref)
+
+
+def test_plan_pools_in_the_epilogue(cuda):
+    """A VGG block (conv, ReLU, MaxPool2d(ceil_mode), conv) runs its first conv pooled
+    (rpst_conv2d_pool) when the pooled map's conv is F(4x4): same bits as the unfused
+    plan, and no full-resolution map is materialised."""
+    from rpst import ops, plan
+    layers = [torch.nn.ReflectionPad2d(1), torch.nn.Conv2d(64, 64, 3), torch.nn.ReLU(),
+              torch.nn.MaxPool2d(2, 2, 0, ceil_mode=True), torch.nn.ReflectionPad2d(1),
+              torch.nn.Conv2d(64, 128, 3), torch.nn.ReLU()]
+    seq = torch.nn.Sequential(*layers).to(cuda).requires_grad_(False)
+    x = gen(50, (2, 64, 96, 130), 1.0, 0.1).to(cuda)
+    steps = plan.compile_layers(seq.children())
+    assert len(steps) == 2 and steps[1].in_op == ops.IN_MAXPOOL2
+    y0 = ops.conv2d(x, plan.packed_weight(steps[0].conv), steps[0].conv.bias, 64, 3, pad=1,
+                    relu=True)
+    want = plan.run([steps[1]], y0)
+    if not ops.pool_pass_pays(y0, 128, 3):
+        pytest.skip("the pooled conv is not F(4x4) at this shape")
+    calls = []
+    real = ops.conv2d_pool
+    try:
+        ops.conv2d_pool = lambda *a, **k: calls.append(1) or real(*a, **k)
+        got = plan.run(steps, x)
+    finally:
+        ops.conv2d_pool = real
+    assert calls == [1]
+    assert torch.equal(got, want)
+
+
 def test_conv2d_residual_3x3_every_algorithm(cuda, conv_algo):
     """A 3x3 conv with a residual runs on a kernel with the residual epilogue whatever
     algorithm the layer would otherwise take (the Winograd kernels have none)."""
