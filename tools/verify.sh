@@ -20,4 +20,5 @@ done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_adain -o adain -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs > $O/prof_adain.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_wct -o wct -- python3 $R/bench.py --config 2 --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_wct.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_sanet -o sanet -- python3 $R/bench.py --config 3 --steps 5 --warmup 2 --no-cpu-baseline --no-configs > $O/prof_sanet.log 2>&1 || exit 1
 echo done
