@@ -677,6 +677,38 @@ static int clamp_values(const float* A, const float* w1, const float* b1, const 
   return launch_status("clamp_head_kernel");
 }
 
+// The clamp values without the affinity matrix: f_psi's first Linear only ever sees
+// A = cn^T sn through Z = A W1^T, and Z = cn^T (sn W1^T) (sanet.py:45-66, 110): T = sn W1^T
+// (C x hid per image, K = HW), then Z = cn^T T + b1 (K = C): 2 x 2 C hid HW FLOP per image
+// instead of 2 HW^2 (C + hid), and the B x HW x HW affinity is never written or read (the
+// same sums in another association: ~1e-7 relative from the two-GEMM form).
+// T: B * C * hid floats of scratch.
+static int clamp_values_factored(const float* cn, const float* sn, const float* w1,
+                                 const float* b1, const float* w2, const float* b2, int hid,
+                                 int mode, float from, float interval, float* T, float* Z,
+                                 float* clamp, int B, int C, int HW, hipStream_t st) {
+  GemmArgs gt{sn, w1, T, {}, nullptr, nullptr, 0, C, hid, HW, HW, HW, hid,
+              (int64_t)C * HW, 0, (int64_t)C * hid, 0};
+  launch_gemm<LAY_RK, LAY_RK, BX_NONE>(gt, B, st);
+  if (int e = launch_status("gemm_f32_kernel(T=sn W1^T)")) return e;
+  GemmArgs gz{cn, T, Z, {}, nullptr, b1, 1, HW, hid, C, HW, hid, hid,
+              (int64_t)C * HW, (int64_t)C * hid, (int64_t)HW * hid, 0};
+  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gz, B, st);
+  if (int e = launch_status("gemm_f32_kernel(Z=cn^T T)")) return e;
+  const int64_t rows = (int64_t)B * HW;
+  clamp_head_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Z, w2, b2, clamp, rows, hid,
+                                                               mode, from, interval);
+  return launch_status("clamp_head_kernel");
+}
+
+static int col_norms(const float* c, const float* s, float* cn, float* sn, int B, int C, int HW,
+                     hipStream_t st) {
+  const int64_t pos = (int64_t)B * HW;
+  colnorm_kernel<<<(unsigned)((pos + 255) / 256), 256, 0, st>>>(c, cn, B, C, HW);
+  colnorm_kernel<<<(unsigned)((pos + 255) / 256), 256, 0, st>>>(s, sn, B, C, HW);
+  return launch_status("colnorm_kernel");
+}
+
 static int affinity(const float* c, const float* s, float* out, float* cn, float* sn, int B,
                     int C, int HW, hipStream_t st) {
   const int64_t pos = (int64_t)B * HW;
@@ -786,9 +818,14 @@ extern "C" int rpst_aea_clamp(const float* x, const float* fx, const float* w1,
   return launch_status("aea_apply_kernel");
 }
 
+// the logits' region first holds T = sn W1^T (C x hidden per image): whichever is larger
+static size_t sq_or_t(int B, int C, int HW, int hidden) {
+  return (size_t)B * std::max((size_t)HW * HW, (size_t)C * hidden);
+}
+
 extern "C" size_t rpst_adaptive_attention_workspace_size(int B, int C, int HW, int hidden) {
   if (B <= 0 || C <= 0 || HW <= 0 || hidden <= 0) return 0;
-  return sizeof(float) * ((size_t)B * HW * HW + (size_t)B * HW * hidden +
+  return sizeof(float) * (sq_or_t(B, C, HW, hidden) + (size_t)B * HW * hidden +
                           2 * (size_t)B * C * HW + 5 * (size_t)B * HW);
 }
 
@@ -812,8 +849,8 @@ extern "C" int rpst_adaptive_attention(const float* F, const float* G, const flo
     return RPST_EWORKSPACE;
   }
   hipStream_t st = as_stream(stream);
-  float* S = static_cast<float*>(workspace);  // affinity first, then the logits
-  float* Z = S + (size_t)B * HW * HW;
+  float* S = static_cast<float*>(workspace);  // T = sn W1^T first, then the logits
+  float* Z = S + sq_or_t(B, C, HW, hidden);
   float* cn = Z + (size_t)B * HW * hidden;
   float* sn = cn + (size_t)B * C * HW;
   float* rmax = sn + (size_t)B * C * HW;
@@ -821,10 +858,11 @@ extern "C" int rpst_adaptive_attention(const float* F, const float* G, const flo
   float* clamp = rinv + (size_t)B * HW;
   float* m2 = clamp + (size_t)B * HW;
   float* inv2 = m2 + (size_t)B * HW;
-  // 1. clamp values from the cosine affinity of the raw features (sanet.py:110, 45 / 66)
-  if (int e = affinity(content, style, S, cn, sn, B, C, HW, st)) return e;
-  if (int e = clamp_values(S, w1, b1, w2, b2, hidden, mode, from, interval, Z, clamp, B, HW,
-                           st))
+  // 1. clamp values from the cosine affinity of the raw features (sanet.py:110, 45 / 66), the
+  //    affinity folded into f_psi's first Linear (T in the logits' buffer, not yet written)
+  if (int e = col_norms(content, style, cn, sn, B, C, HW, st)) return e;
+  if (int e = clamp_values_factored(cn, sn, w1, b1, w2, b2, hidden, mode, from, interval, S, Z,
+                                    clamp, B, C, HW, st))
     return e;
   // 2. logits S = F^T G and softmax row statistics (sanet.py:114-117)
   const int64_t fhw = (int64_t)C * HW;
@@ -971,8 +1009,10 @@ extern "C" size_t rpst_adaptive_attention_backward_workspace_size(int B, int C, 
   if (B <= 0 || C <= 0 || HW <= 0 || hidden <= 0) return 0;
   const size_t hw2 = (size_t)B * HW * HW;
   const size_t chunks = ((size_t)B * HW + kColChunk - 1) / kColChunk;
-  // + the per-image dW1 partials and the column-sum chunk partials
-  return sizeof(float) * (3 * hw2 + 2 * (size_t)B * HW * hidden + 2 * (size_t)B * C * HW +
+  // (the first region holds T and then R, C x hidden per image, never the affinity) + the
+  // per-image dW1 partials and the column-sum chunk partials
+  return sizeof(float) * (sq_or_t(B, C, HW, hidden) + 2 * hw2 + 2 * (size_t)B * HW * hidden +
+                          2 * (size_t)B * C * HW +
                           8 * (size_t)B * HW + (size_t)B * hidden * HW +
                           3 * (size_t)(hidden + 1) * chunks);
 }
@@ -998,8 +1038,8 @@ extern "C" int rpst_adaptive_attention_backward(
   }
   hipStream_t st = as_stream(stream);
   const int64_t hw2 = (int64_t)HW * HW, fhw = (int64_t)C * HW, rows = (int64_t)B * HW;
-  float* Aff = static_cast<float*>(workspace);
-  float* S = Aff + (size_t)B * hw2;
+  float* Aff = static_cast<float*>(workspace);  // T, then R (C x hidden per image)
+  float* S = Aff + sq_or_t(B, C, HW, hidden);
   float* dQ = S + (size_t)B * hw2;
   float* Z = dQ + (size_t)B * hw2;
   float* du = Z + (size_t)rows * hidden;
@@ -1014,10 +1054,11 @@ extern "C" int rpst_adaptive_attention_backward(
   float* dt = dc + rows;
   float* w1part = dt + rows;                               // [B][hidden][HW]
   float* cpart = w1part + (size_t)B * hidden * HW;         // [chunks][3][hidden + 1]
-  // forward quantities: affinity, clamp (and Z), logits, softmax / relu-softmax statistics
-  if (int e = affinity(content, style, Aff, cn, sn, B, C, HW, st)) return e;
-  if (int e = clamp_values(Aff, w1, b1, w2, b2, hidden, mode, from, interval, Z, clamp, B, HW,
-                           st))
+  // forward quantities: clamp (and Z) as the forward forms them (the affinity folded into
+  // f_psi's first Linear; T in the Aff region), logits, softmax / relu-softmax statistics
+  if (int e = col_norms(content, style, cn, sn, B, C, HW, st)) return e;
+  if (int e = clamp_values_factored(cn, sn, w1, b1, w2, b2, hidden, mode, from, interval, Aff,
+                                    Z, clamp, B, C, HW, st))
     return e;
   GemmArgs g1{F, G, S, {}, nullptr, nullptr, 0, HW, HW, C, HW, HW, HW, fhw, fhw, hw2, 0};
   launch_gemm<LAY_KR, LAY_KR, BX_NONE>(g1, B, st);
@@ -1052,12 +1093,17 @@ extern "C" int rpst_adaptive_attention_backward(
   fpsi_bwd_rows_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Z, w2, b2, dc, dt, du, rows,
                                                                    hidden, mode, interval);
   if (int e = launch_status("fpsi_bwd_rows_kernel")) return e;
-  // dW1 = du^T Aff per image (a batched GEMM over B: K = HW each, instead of one GEMM with
-  // K = B * HW on HW / 128 workgroups), then the B partials summed in order
-  GemmArgs gw{du, Aff, w1part, {}, nullptr, nullptr, 0, hidden, HW, HW, hidden, HW, HW,
-              (int64_t)HW * hidden, hw2, (int64_t)hidden * HW, 0};
+  // dW1 = du^T A per image with A = cn^T sn never formed: R = cn du (C x hidden, K = HW),
+  // then dW1_b = R^T sn (K = C), then the B partials summed in order
+  float* R = Aff;
+  GemmArgs gr{cn, du, R, {}, nullptr, nullptr, 0, C, hidden, HW, HW, hidden, hidden,
+              fhw, (int64_t)HW * hidden, (int64_t)C * hidden, 0};
+  launch_gemm<LAY_RK, LAY_KR, BX_NONE>(gr, B, st);
+  if (int e = launch_status("gemm_f32_kernel(R_b=cn_b du_b)")) return e;
+  GemmArgs gw{R, sn, w1part, {}, nullptr, nullptr, 0, hidden, HW, C, hidden, HW, HW,
+              (int64_t)C * hidden, fhw, (int64_t)hidden * HW, 0};
   launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gw, B, st);
-  if (int e = launch_status("gemm_f32_kernel(dW1_b=du_b^T A_b)")) return e;
+  if (int e = launch_status("gemm_f32_kernel(dW1_b=R_b^T sn_b)")) return e;
   const int64_t nw1 = (int64_t)hidden * HW;
   batch_sum_kernel<<<(unsigned)((nw1 + 255) / 256), 256, 0, st>>>(w1part, dw1, nw1, B);
   if (int e = launch_status("batch_sum_kernel(dW1)")) return e;
