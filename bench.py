@@ -75,6 +75,8 @@ def build_model(kind, dev):
         m = net.AdaptiveSAModel(ADAPTIVE_CONFIG, copy.deepcopy(net.vgg), 0, 512)
     elif kind == "train":
         m = net.AdaINRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
+    elif kind == "forward":
+        m = net.AdaINRPNet(cfg, copy.deepcopy(net.vgg))
     elif kind == "train_wct":
         m = net.WCTRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
     elif kind == "train_sanet":
@@ -136,12 +138,15 @@ WORKLOADS = {
                       "on the adaptive transform and decoder (SURVEY 8(f) ranks 2-3)",
     "train_source": "SourceNet training iteration: forward() losses + total_loss.backward() + "
                     "Adam step on the decoder (SURVEY 8(f) ranks 2-3)",
+    "forward": "AdaINRPNet.forward() under torch.no_grad(): stylised image + VGG relu1_1-4_1 "
+               "style / content losses, rp_blocks=5 hidden_dim=16 (SURVEY 8(d) config #2, "
+               "adain_rp.py:110-138)",
     "selftest": "CPU stand-in per-image function (launcher / timing / gather test only)",
 }
 DEFAULT_BATCH = {"adain": 32, "wct": 16, "sanet": 32, "multiscale": 32, "source": 32,
                  "adaptive": 32, "train": 8, "train_wct": 8, "train_sanet": 8,
                  "train_multiscale": 8, "train_source": 8, "train_adaptive": 8,
-                 "selftest": 4}
+                 "forward": 32, "selftest": 4}
 # CPU-baseline sample per workload (BASELINE.md plan: B=2 at 512^2, B=1 for WCT)
 CPU_SAMPLE_BATCH = {"wct": 1, "train": 1, "train_wct": 1, "train_sanet": 1,
                     "train_multiscale": 1, "train_source": 1, "train_adaptive": 1}
@@ -212,6 +217,9 @@ def cpu_baseline(kind, size, reps=3, batch=None):
     elif kind == "train":
         m = net.AdaINRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
         fn = lambda c, s, sd: R.adain_rp_grads(c, s, sd, 5, 1.0, 1.0)  # noqa: E731
+    elif kind == "forward":
+        m = net.AdaINRPNet(cfg, copy.deepcopy(net.vgg))
+        fn = lambda c, s, sd: R.adain_rp_forward(c, s, sd, 5, 1.0, 10.0)  # noqa: E731
     elif kind == "train_wct":
         m = net.WCTRPNet(dict(cfg, style_weight=1.0), copy.deepcopy(net.vgg))
         fn = lambda c, s, sd: R.wct_rp_grads(c, s, sd, 5, 1.0, 1.0)  # noqa: E731
@@ -492,7 +500,12 @@ def run_workload(kind, size, batch, gbatch, gather, micro, steps, warmup, world,
     # the D2H gather of chunk i runs on a copy stream while chunk i + 1 computes
     copy_stream = torch.cuda.Stream(dev) if (cuda and host is not None) else None
 
-    if kind not in TRAIN_KINDS:
+    if kind == "forward":
+        def step():
+            with torch.no_grad():
+                _, tot = model(content, style)
+            return tot
+    elif kind not in TRAIN_KINDS:
         def step():
             out = None
             for s0 in range(0, B, mb):
@@ -532,7 +545,7 @@ def run_workload(kind, size, batch, gbatch, gather, micro, steps, warmup, world,
         order = {"steps": steps, "warmup": warmup, "per_step": names[:len(names) // max(steps, 1)]}
     ops.TRACE = None
     last_chunk = B - mb * ((B - 1) // mb)
-    assert torch.isfinite(out).all() and (kind.startswith("train") or
+    assert torch.isfinite(out).all() and (kind.startswith("train") or kind == "forward" or
                                           out.shape == (last_chunk,) + shape[1:])
 
     per_rank = [dt_rank]

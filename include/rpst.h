@@ -218,9 +218,13 @@ int rpst_add_upsample_nearest2x(const float* a, const float* b, float* out, int 
  * O[b] = H[b] softmax_rows(F[b]^T G[b])^T  for F, G, H, O of shape (B, C, HW):
  *   S = F^T G (HW x HW, no 1/sqrt(C) scale), row softmax over keys, O = H S^T.
  * The 1x1 convs f/g/h/out_conv and mean_variance_norm run through rpst_conv2d /
- * rpst_mean_variance_norm. Workspace: rpst_sanet_attention_workspace_size(B, HW)
- * (S is materialised: B*HW*HW floats). */
+ * rpst_mean_variance_norm. C in {64, 128, 256, 512} with HW % 4 == 0 runs flash-style (S
+ * is never written: the keys stream through a double-buffered LDS ring with an online
+ * softmax; no workspace); other shapes materialise S (B*HW*HW floats).
+ * Workspace: rpst_sanet_attention_workspace_size_c(B, C, HW) (0 on the flash path);
+ * rpst_sanet_attention_workspace_size(B, HW) is the materialised-S size (always enough). */
 size_t rpst_sanet_attention_workspace_size(int B, int HW);
+size_t rpst_sanet_attention_workspace_size_c(int B, int C, int HW);
 int rpst_sanet_attention(const float* F, const float* G, const float* H, float* O, int B,
                          int C, int HW, void* workspace, size_t workspace_bytes,
                          rpst_stream_t stream);
@@ -418,6 +422,15 @@ int rpst_whiten_and_color_f64(const double* cF, const double* sF, double* out, i
                               int64_t HW, double* residual, void* workspace,
                               size_t workspace_bytes, rpst_stream_t stream);
 
+/* whiten_and_color(cF, sF, 'original') (Li et al., wct_rp.py:96-101): out =
+ * matrix_sqrt(Cs) matrix_inv_sqrt(Cc + I) (cF - mu_c) + mu_s, both matrix functions in the
+ * reference's SVD form (as rpst_matrix_power_psd_f64, including the 1e-5 truncation), with
+ * Cc, Cs the covariances of wct_rp.py:89-94 (the content one + I). Same shapes and workspace
+ * as rpst_whiten_and_color_f64. */
+int rpst_whiten_and_color_original_f64(const double* cF, const double* sF, double* out, int C,
+                                       int64_t HW, void* workspace, size_t workspace_bytes,
+                                       rpst_stream_t stream);
+
 /* ---- a9: WCTRPNet.fuse(content_feats, style_feats)  network/wct_rp.py:157-166 --------
  * content, style, out: (n, C, HW) fp32. Per image: widen to fp64, whiten_and_color, round
  * to fp32 — all n images in one set of launches. residual: 2n doubles or NULL (as a8, per
@@ -435,6 +448,21 @@ int rpst_wct_fuse(const float* content, const float* style, float* out, int n, i
 int rpst_wct_params(const float* content, const float* style, const float* means, double* T,
                     double* offset, int n, int C, int64_t HW, double* residual, void* workspace,
                     size_t workspace_bytes, rpst_stream_t stream);
+
+/* Per-image status of the last rpst_wct_fuse / rpst_wct_params call on `workspace` (same n,
+ * C, HW), copied asynchronously on `stream` into status (n ints, device memory): 0 = valid,
+ * otherwise a bit mask of RPST_WCT_NOCONV (a Newton-Schulz iteration did not converge:
+ * non-finite features) and RPST_WCT_TIMEOUT (a group barrier of the persistent matrix-function
+ * launch timed out, e.g. its workgroups were not all resident beside other work). Any non-zero
+ * status comes with NaN in that image's T / offset / output — never a silently wrong finite
+ * value. Read it at the caller's next natural synchronisation.
+ * rpst_whiten_and_color_status: the same for the last rpst_whiten_and_color_f64 call. */
+#define RPST_WCT_NOCONV 1
+#define RPST_WCT_TIMEOUT 4
+int rpst_wct_status(const void* workspace, int n, int C, int64_t HW, int* status,
+                    rpst_stream_t stream);
+int rpst_whiten_and_color_status(const void* workspace, int C, int64_t HW, int* status,
+                                 rpst_stream_t stream);
 
 /* out = act(conv(pad(T_n x + c_n)) + bias) per image n: the WCT colour transform fused into
  * the consumer conv. F(4x4) layers fold T_n into per-image weights W T_n (fp64, rounded

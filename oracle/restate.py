@@ -286,8 +286,9 @@ def matrix_inv_sqrt(A: Tensor) -> Tensor:
     return _psd_power(A, -0.5)
 
 
-def whiten_and_color(cF: Tensor, sF: Tensor) -> Tensor:
-    """WCTRPNet.whiten_and_color(method='closed-form') (wct_rp.py:82-114), fp64."""
+def whiten_and_color(cF: Tensor, sF: Tensor, method: str = 'closed-form') -> Tensor:
+    """WCTRPNet.whiten_and_color (wct_rp.py:82-114), fp64: 'closed-form' (Lu et al.,
+    :102-111) or 'original' (Li et al., :96-101)."""
     n = cF.shape[1]
     c_mean = cF.mean(1, keepdim=True)
     cF = cF - c_mean
@@ -295,6 +296,9 @@ def whiten_and_color(cF: Tensor, sF: Tensor) -> Tensor:
     s_mean = sF.mean(1, keepdim=True)
     sF = sF - s_mean
     cs = (sF @ sF.t()).div(sF.shape[1] - 1)
+    if method == 'original':  # wct_rp.py:96-101
+        return matrix_sqrt(cs) @ (matrix_inv_sqrt(cc) @ cF) + s_mean
+    assert method == 'closed-form'
     c_sqrt = matrix_sqrt(cc)
     c_isqrt = matrix_inv_sqrt(cc)
     middle = matrix_sqrt(c_sqrt @ cs @ c_sqrt)

@@ -23,10 +23,13 @@ int cov_v2(const float* cF, const float* sF, const float* mu32, int n, int C, in
 // WCT: T_b = Ic Mid Ic with Sc, Ic = (Cc_b + 1e-4 I)^(+-1/2), Mid = (Sc Cs_b Sc + 1e-4 I)^(1/2)
 // (wct_rp.py:104-109) and offset_b = mu_s - T_b mu_c; residual (2n, may be null): the final
 // Newton-Schulz residuals of the two square roots. A matrix whose iteration did not converge
-// (non-finite input) gets NaN in T and offset.
+// (non-finite input), or whose group barriers timed out, gets NaN in T and offset; its flags
+// word (RPST_WCT_NOCONV / RPST_WCT_TIMEOUT) is copied out by matfun_wct_status.
 size_t matfun_wct_work_doubles(int n, int C);
 int matfun_wct(const double* Cc, const double* Cs, const double* mu64, double* T, double* offset,
                double* residual, int n, int C, double* work, hipStream_t st);
+int matfun_wct_status(double* work, int n, int C, int* status, hipStream_t st);
+int matfun_wct_clear_status(double* work, int n, int C, hipStream_t st);
 
 // Power: out = (A + 1e-4 I)^(1/2) (inverse = 0) or ^(-1/2), exactly the reference's SVD form
 // V diag(s^p) V^T truncated at s < 1e-5 (wct_rp.py:7-40): Newton-Schulz for symmetric inputs

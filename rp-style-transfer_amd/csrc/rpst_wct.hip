@@ -538,7 +538,7 @@ struct WctLayout {
   bool v2;  // fp32 features with C <= 256: cov_syrk_kernel (rpst_wct_mat.hip)
   int64_t HW;
   // offsets in doubles
-  size_t mu_c, mu_s, mu32, part, cc, cs, tm, off, tf, mf;
+  size_t mu_c, mu_s, mu32, part, cc, cs, tm, off, tf, mf, orig;
   size_t total;
 };
 
@@ -565,6 +565,10 @@ static WctLayout wct_layout(int n, int C, int64_t HW, bool src_f32) {
   L.off = o; o += (size_t)n * C;
   L.tf = o; o += cc / 2 + (size_t)n * C + 2;  // fp32 transform operands (wct_run)
   L.mf = o; o += matfun_wct_work_doubles(n, C);
+  // whiten_and_color(method='original') (fp64 features, n = 1): (Cc + 1e-4 I)^(-1/2) and
+  // (Cs + 1e-4 I)^(1/2) in SVD form, then the matrix-power workspace
+  L.orig = o;
+  if (!src_f32) o += (size_t)2 * n * C * C + matfun_power_work_doubles(C, n);
   L.total = o;
   return L;
 }
@@ -585,13 +589,14 @@ __global__ void narrow_means_kernel(const double* __restrict__ m, float* __restr
 
 // WCT matrices of every image (wct_rp.py:85-109): fp64 means (mu_c, mu_s in the workspace),
 // covariances, then T = Ic Mid Ic and offset = mu_s - T mu_c from the persistent matfun
-// launch. SRC is SRC_F32C (fp32 features) or SRC_F64C (fp64). means: optional fp32 (2n x C)
+// launch (original: T = (Cs + 1e-4 I)^(1/2) (Cc + 1e-4 I)^(-1/2) in the reference's SVD form,
+// Li et al., wct_rp.py:96-101; offset unused). SRC is SRC_F32C (fp32 features) or SRC_F64C (fp64). means: optional fp32 (2n x C)
 // row means (content rows then style rows), used to centre; residual (2n, optional): final
 // Newton-Schulz residuals of (Cc + 1e-4 I) and of Mid's argument. T / offset: n x C x C / n x C.
 template <int SRC>
 static int wct_matrices(const void* cF, const void* sF, const float* means, int n, int C,
                         int64_t HW, const WctLayout& L, double* ws, double* T, double* offset,
-                        double* residual, hipStream_t st) {
+                        double* residual, hipStream_t st, bool original = false) {
   double *mu_c = ws + L.mu_c, *part = ws + L.part;
   double *Cc = ws + L.cc, *Cs = ws + L.cs;
   const int64_t cnt = (int64_t)2 * n * C;
@@ -655,6 +660,31 @@ static int wct_matrices(const void* cF, const void* sF, const float* means, int 
                                           1.0 / (double)(HW - 1), 0.0, n);
     if (int e = launch_status("cov_reduce_kernel")) return e;
   }
+  if (original) {
+    // 3'. Li et al.: cF_inv_sqrt = matrix_inv_sqrt(Cc), sF_sqrt = matrix_sqrt(Cs) (each the
+    //     SVD form with the 1e-5 truncation: Newton-Schulz, Jacobi where it could differ),
+    //     T = sF_sqrt cF_inv_sqrt; sF_sqrt (cF_inv_sqrt cF) of wct_rp.py:101 is the same
+    //     product up to fp64 association. No barrier-timeout state is left in L.mf: flagged
+    //     matrices are recomputed by the Jacobi kernel.
+    double* Ai = ws + L.orig;
+    double* Bs = Ai + (size_t)n * C * C;
+    double* pw = Bs + (size_t)n * C * C;
+    if (int e = matfun_power(Cc, Ai, C, n, 1, nullptr, pw, st)) return e;
+    if (int e = matfun_power(Cs, Bs, C, n, 0, nullptr, pw, st)) return e;
+    if (int e = matfun_wct_clear_status(ws + L.mf, n, C, st)) return e;
+    G64Args g{};
+    g.A = Bs;
+    g.B = Ai;
+    g.C = T;
+    g.alpha = 1.0;
+    g.M = g.N = g.K = C;
+    g.lda = g.ldb = g.ldc = C;
+    g.sA = g.sB = g.sC = (int64_t)C * C;
+    g.ksplit = 1;
+    dim3 grid((unsigned)((C + 63) / 64), (unsigned)((C + 63) / 64), n);
+    gemm64<64, SRC_F64, SRC_F64, B_KN, OUT_F64>(g, grid, st);
+    return launch_status("gemm_f64_kernel(original T)");
+  }
   // 3. Sc, Ic = (Cc + 1e-4 I)^(+-1/2); Mid = (Sc Cs Sc + 1e-4 I)^(1/2); T = Ic Mid Ic;
   //    offset = mu_s - T mu_c: one persistent launch
   return matfun_wct(Cc, Cs, mu_c, T, offset, residual, n, C, ws + L.mf, st);
@@ -663,11 +693,12 @@ static int wct_matrices(const void* cF, const void* sF, const float* means, int 
 // Shared WCT body: the matrices, then out = T (cF - mu_c) + mu_s.
 template <int SRC, int OUTM>
 static int wct_run(const void* cF, const void* sF, void* out, int n, int C, int64_t HW,
-                   void* workspace, double* residual, hipStream_t st) {
+                   void* workspace, double* residual, hipStream_t st, bool original = false) {
   const WctLayout L = wct_layout(n, C, HW, SRC == SRC_F32C);
   double* ws = static_cast<double*>(workspace);
   double *mu_c = ws + L.mu_c, *mu_s = ws + L.mu_s, *Tm = ws + L.tm;
-  if (int e = wct_matrices<SRC>(cF, sF, nullptr, n, C, HW, L, ws, Tm, ws + L.off, residual, st))
+  if (int e = wct_matrices<SRC>(cF, sF, nullptr, n, C, HW, L, ws, Tm, ws + L.off, residual, st,
+                                original))
     return e;
 
   // out = T (cF - mu_c) + mu_s; fp32 features -> fp32 MFMA (RPST_WCT_T_F64=1: fp64)
@@ -787,6 +818,39 @@ extern "C" int rpst_whiten_and_color_f64(const double* cF, const double* sF, dou
   }
   return wct_run<SRC_F64C, OUT_F64_BIAS>(cF, sF, out, 1, C, HW, workspace, residual,
                                          as_stream(stream));
+}
+
+extern "C" int rpst_whiten_and_color_original_f64(const double* cF, const double* sF,
+                                                  double* out, int C, int64_t HW, void* workspace,
+                                                  size_t workspace_bytes, rpst_stream_t stream) {
+  RPST_REQUIRE(cF && sF && out, "whiten_and_color(original): null pointer");
+  RPST_REQUIRE(C > 0 && C <= 1024 && HW > 1 && HW <= 0x7fffffffLL,
+               "whiten_and_color(original): bad shape");
+  if (!workspace || workspace_bytes < rpst_wct_workspace_size(1, C, HW)) {
+    set_error("whiten_and_color(original): workspace too small");
+    return RPST_EWORKSPACE;
+  }
+  return wct_run<SRC_F64C, OUT_F64_BIAS>(cF, sF, out, 1, C, HW, workspace, nullptr,
+                                         as_stream(stream), true);
+}
+
+extern "C" int rpst_wct_status(const void* workspace, int n, int C, int64_t HW, int* status,
+                               rpst_stream_t stream) {
+  RPST_REQUIRE(workspace && status, "wct_status: null pointer");
+  RPST_REQUIRE(n > 0 && C > 0 && C <= 1024 && HW > 1, "wct_status: bad shape");
+  // rpst_wct_fuse / rpst_wct_params lay the workspace out for fp32 features
+  const WctLayout L = wct_layout(n, C, HW, true);
+  double* ws = static_cast<double*>(const_cast<void*>(workspace));
+  return matfun_wct_status(ws + L.mf, n, C, status, as_stream(stream));
+}
+
+extern "C" int rpst_whiten_and_color_status(const void* workspace, int C, int64_t HW, int* status,
+                                            rpst_stream_t stream) {
+  RPST_REQUIRE(workspace && status, "whiten_and_color_status: null pointer");
+  RPST_REQUIRE(C > 0 && C <= 1024 && HW > 1, "whiten_and_color_status: bad shape");
+  const WctLayout L = wct_layout(1, C, HW, false);
+  double* ws = static_cast<double*>(const_cast<void*>(workspace));
+  return matfun_wct_status(ws + L.mf, 1, C, status, as_stream(stream));
 }
 
 extern "C" size_t rpst_matrix_power_workspace_size(int n, int batch) {

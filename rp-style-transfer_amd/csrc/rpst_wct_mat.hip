@@ -438,11 +438,16 @@ struct MfArgs {
   double* scratch;   // per group: kMfBufs n x n
   double* red;       // per group: [2][kRedSlots][P]
   unsigned* bar;     // per group barrier counter, zero at launch
+  // debug knob (RPST_MATFUN_DEBUG_SKIP=1, tests only): workgroup P - 1 of group 0 never arrives
+  // at its barriers, as if it were not resident; the spin bound shrinks so the test is quick
+  int dbg_skip;
 };
 constexpr int kMfBufs = 11;
 
 struct MfCtx {
   int n, P, p, ti, tj;
+  bool skip;         // dbg_skip: this workgroup does not arrive at barriers
+  unsigned spin_cap;
   unsigned* bar;
   unsigned* abort;  // launch-wide: set by a timed-out barrier, every later barrier passes
   unsigned phase;
@@ -464,15 +469,18 @@ __device__ __forceinline__ void mf_sync(MfCtx& c) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (c.P > 1) {
-      __hip_atomic_fetch_add(c.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!c.skip) __hip_atomic_fetch_add(c.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned target = c.phase * (unsigned)c.P;
       unsigned spins = 0;
       while (__hip_atomic_load(c.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(2);
         // ~0.25 s: far beyond any phase (a matrix function takes ~1 ms); on a timeout the
-        // matrix is flagged and every later barrier of the launch passes, so it drains
+        // matrix is flagged and every later barrier of the launch gives up after 1024 spins,
+        // flagging the matrix it belongs to, so the launch drains. Every flagged matrix is
+        // overwritten with NaN after the launch (mf_poison_kernel): a barrier that did not
+        // synchronise never yields a finite result
         if ((++spins & 1023u) == 0 &&
-            (spins > (1u << 22) ||
+            (spins > c.spin_cap ||
              __hip_atomic_load(c.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
           __hip_atomic_fetch_or(c.flag, FL_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(c.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -675,6 +683,8 @@ __global__ __launch_bounds__(256) void matfun_kernel(MfArgs a) {
   c.p = p;
   c.ti = p / a.tpd;
   c.tj = p % a.tpd;
+  c.skip = a.dbg_skip && g == 0 && p == a.P - 1;
+  c.spin_cap = a.dbg_skip ? (1u << 14) : (1u << 22);
   c.bar = a.bar + g;
   c.abort = a.bar + a.G;
   c.phase = 0;
@@ -846,12 +856,43 @@ __global__ __launch_bounds__(1024) void jacobi_power_kernel(const double* __rest
   }
 }
 
+// MF_WCT: T and offset of every matrix whose barriers timed out (FL_TIMEOUT: some barrier of
+// its group did not synchronise, so its partials may be stale) become NaN. One block per
+// flagged-or-not matrix; unflagged ones exit at once.
+__global__ __launch_bounds__(256) void mf_poison_kernel(const int* __restrict__ flags,
+                                                        double* __restrict__ T,
+                                                        double* __restrict__ offset, int n) {
+  const int b = blockIdx.x;
+  if (!(flags[b] & FL_TIMEOUT)) return;
+  const double nan = __builtin_nan("");
+  const int64_t nn = (int64_t)n * n;
+  for (int64_t e = threadIdx.x; e < nn; e += 256) T[(int64_t)b * nn + e] = nan;
+  for (int e = threadIdx.x; e < n; e += 256) offset[(int64_t)b * n + e] = nan;
+}
+
 // ======================= host side =======================================================
 
+// workgroups of matfun_kernel the device holds at once (occupancy x CUs; 256 when unknown,
+// e.g. no device in a CPU-only process sizing a workspace)
+static int mf_resident_cap() {
+  static const int cap = [] {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, matfun_kernel, 256, 0) != hipSuccess ||
+        cus <= 0 || per <= 0) {
+      (void)hipGetLastError();
+      return 256;
+    }
+    return cus * per;
+  }();
+  return cap;
+}
+
+// layout geometry (the workspace is sized for G = 256 / P groups, whatever the device)
 static void mf_geometry(int n, int batch, int& tpd, int& P, int& G) {
   tpd = (n + kMT - 1) / kMT;
   P = tpd * tpd;
-  // at most 256 workgroups (41 KiB of LDS each): every group's workgroups are co-resident
   G = 256 / P;
   if (G < 1) G = 1;
   if (G > batch) G = batch;
@@ -865,22 +906,68 @@ static size_t mf_work_doubles(int n, int batch) {
          (size_t)(batch + 1) / 2 + 2;
 }
 
+// per-matrix flags of the last launch on this workspace (layout of mf_launch)
+static int* mf_flags(double* work, int n, int batch) {
+  int tpd, P, G;
+  mf_geometry(n, batch, tpd, P, G);
+  return reinterpret_cast<int*>(
+      reinterpret_cast<unsigned*>(work + (size_t)G * kMfBufs * n * n + (size_t)G * 2 * kRedSlots * P) +
+      G + 1);
+}
+
 static int mf_launch(MfArgs a, double* work, hipStream_t st) {
-  mf_geometry(a.n, a.batch, a.tpd, a.P, a.G);
+  int Gl;
+  mf_geometry(a.n, a.batch, a.tpd, a.P, Gl);
   a.scratch = work;
-  a.red = a.scratch + (size_t)a.G * kMfBufs * a.n * a.n;
-  a.bar = reinterpret_cast<unsigned*>(a.red + (size_t)a.G * 2 * kRedSlots * a.P);
-  a.flags = reinterpret_cast<int*>(a.bar + a.G + 1);
-  if (hipMemsetAsync(a.bar, 0, sizeof(unsigned) * (a.G + 1) + sizeof(int) * a.batch, st) !=
+  a.red = a.scratch + (size_t)Gl * kMfBufs * a.n * a.n;
+  a.bar = reinterpret_cast<unsigned*>(a.red + (size_t)Gl * 2 * kRedSlots * a.P);
+  a.flags = reinterpret_cast<int*>(a.bar + Gl + 1);
+  // groups that the device can hold at once: the group barriers need every workgroup of a
+  // group resident (a smaller device, or a grid the occupancy does not cover, gets fewer
+  // groups looping over more matrices)
+  const int cap = mf_resident_cap();
+  if (cap < a.P) {
+    set_error("matfun: %d workgroups per matrix but only %d resident on this device", a.P, cap);
+    return RPST_EINVAL;
+  }
+  a.G = Gl < cap / a.P ? Gl : cap / a.P;
+  {
+    const char* e = getenv("RPST_MATFUN_DEBUG_SKIP");
+    a.dbg_skip = (e && *e && atoi(e) != 0 && a.P > 1) ? 1 : 0;
+  }
+  // barrier counters (the layout's Gl of them) + abort word + flags
+  if (hipMemsetAsync(a.bar, 0, sizeof(unsigned) * (Gl + 1) + sizeof(int) * a.batch, st) !=
       hipSuccess) {
     set_error("matfun: workspace reset failed");
     return RPST_EHIP;
   }
   matfun_kernel<<<a.G * a.P, 256, 0, st>>>(a);
-  return launch_status("matfun_kernel");
+  if (int e = launch_status("matfun_kernel")) return e;
+  if (a.mode == MF_WCT) {
+    mf_poison_kernel<<<a.batch, 256, 0, st>>>(a.flags, a.T, a.offset, a.n);
+    return launch_status("mf_poison_kernel");
+  }
+  return RPST_OK;
+}
+
+int matfun_wct_status(double* work, int n, int C, int* status, hipStream_t st) {
+  if (hipMemcpyAsync(status, mf_flags(work, C, n), sizeof(int) * (size_t)n,
+                     hipMemcpyDeviceToDevice, st) != hipSuccess) {
+    set_error("wct_status: copy failed");
+    return RPST_EHIP;
+  }
+  return RPST_OK;
 }
 
 size_t matfun_wct_work_doubles(int n, int C) { return mf_work_doubles(C, n); }
+
+int matfun_wct_clear_status(double* work, int n, int C, hipStream_t st) {
+  if (hipMemsetAsync(mf_flags(work, C, n), 0, sizeof(int) * (size_t)n, st) != hipSuccess) {
+    set_error("wct: status reset failed");
+    return RPST_EHIP;
+  }
+  return RPST_OK;
+}
 
 int matfun_wct(const double* Cc, const double* Cs, const double* mu64, double* T, double* offset,
                double* residual, int n, int C, double* work, hipStream_t st) {
@@ -922,11 +1009,7 @@ int matfun_power(const double* A, double* out, int n, int batch, int inverse, do
   a.residual = residual;
   if (int e = mf_launch(a, work, st)) return e;
   double* jw = work + mf_work_doubles(n, batch);
-  int tpd, P, G;
-  mf_geometry(n, batch, tpd, P, G);
-  const int* flags = reinterpret_cast<const int*>(
-      reinterpret_cast<unsigned*>(work + (size_t)G * kMfBufs * n * n + (size_t)G * 2 * kRedSlots * P) +
-      G + 1);
+  const int* flags = mf_flags(work, n, batch);
   jacobi_power_kernel<<<batch, 1024, 0, st>>>(A, out, flags, n, inverse, jw);
   return launch_status("jacobi_power_kernel");
 }

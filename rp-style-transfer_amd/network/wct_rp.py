@@ -24,6 +24,10 @@ from .base import (BaseNet, build_decrease_depth_rp_blocks, build_increase_depth
 
 # RPST_FUSE_WCT=0 disables the fused path (A/B measurements, debugging)
 FUSED_WCT = os.environ.get("RPST_FUSE_WCT", "1") != "0"
+# RPST_WCT_CHECK=1: read the per-image WCT status after each launch (one host sync) and raise
+# on an invalid image (non-convergence, or a timed-out persistent launch) instead of letting
+# its NaN output through; off by default (the inference path never synchronises)
+CHECK_WCT = os.environ.get("RPST_WCT_CHECK", "0") == "1"
 
 
 def wct_rp_fused(encoder, decoder, content, style):
@@ -36,10 +40,14 @@ def wct_rp_fused(encoder, decoder, content, style):
     assert content.size() == style.size()
     feats, mean, _ = plan.run(plan.compile_layers(encoder.children()), content, x2=style,
                               stats_last=True)
-    T, c, res = ops.wct_params(feats[:n], feats[n:], means=mean.reshape(2 * n, -1))
+    T, c, res, st = ops.wct_params(feats[:n], feats[n:], means=mean.reshape(2 * n, -1),
+                                   status=True)
     out = plan.run(plan.compile_layers(decoder.children()), feats[:n], first_mix=(T, c))
-    # res: the Newton-Schulz residuals (2n), on the device; no host sync here: an image whose
-    # iteration did not converge (non-finite features) has NaN T and c, so its output is NaN
+    # st: per-image status on the device; no host sync unless RPST_WCT_CHECK=1: an image whose
+    # iteration did not converge (non-finite features), or whose persistent launch timed out,
+    # has NaN T and c, so its output is NaN
+    if CHECK_WCT:
+        ops.check_wct_status(st, "WCTRPNet.test")
     return out
 
 
@@ -83,9 +91,13 @@ class WCTRPNet(BaseNet):
         self.mse_loss = nn.MSELoss()
 
     def whiten_and_color(self, cF, sF, method='closed-form'):
-        """cF, sF: (C, HW) fp64 device tensors -> (C, HW) fp64."""
-        assert method == 'closed-form', "only the closed-form (Lu et al.) branch is used"
-        return ops.whiten_and_color(cF, sF)
+        """cF, sF: (C, HW) fp64 device tensors -> (C, HW) fp64; method 'closed-form' (Lu et
+        al., wct_rp.py:102-111) or 'original' (Li et al., :96-101)."""
+        if CHECK_WCT:
+            out, st = ops.whiten_and_color(cF, sF, method=method, status=True)
+            ops.check_wct_status(st, "WCTRPNet.whiten_and_color")
+            return out
+        return ops.whiten_and_color(cF, sF, method=method)
 
     def encode_with_intermediate(self, input):
         results = [input]
@@ -124,6 +136,10 @@ class WCTRPNet(BaseNet):
 
     def fuse(self, content_feats, style_feats):
         """Per-image closed-form WCT, all images of the batch in one set of launches."""
+        if CHECK_WCT:
+            out, st = ops.wct_fuse(content_feats, style_feats, status=True)
+            ops.check_wct_status(st, "WCTRPNet.fuse")
+            return out
         return ops.wct_fuse(content_feats, style_feats)
 
     def forward(self, content, style, alpha=1.0):

@@ -52,6 +52,7 @@ SIGNATURES = {
     "rpst_upsample_nearest2x": (_I, [_P, _P, _I, _I, _I, _I, _P]),
     "rpst_add_upsample_nearest2x": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
     "rpst_sanet_attention_workspace_size": (_SZ, [_I, _I]),
+    "rpst_sanet_attention_workspace_size_c": (_SZ, [_I, _I, _I]),
     "rpst_sanet_attention": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
     "rpst_conv_weight_flip": (_I, [_P, _P, _I, _I, _I, _P]),
     "rpst_relu_backward": (_I, [_P, _P, _P, _I64, _P]),
@@ -98,6 +99,9 @@ SIGNATURES = {
     "rpst_whiten_and_color_f64": (_I, [_P, _P, _P, _I, _I64, _P, _P, _SZ, _P]),
     "rpst_wct_fuse": (_I, [_P, _P, _P, _I, _I, _I64, _P, _P, _SZ, _P]),
     "rpst_wct_params": (_I, [_P, _P, _P, _P, _P, _I, _I, _I64, _P, _P, _SZ, _P]),
+    "rpst_wct_status": (_I, [_P, _I, _I, _I64, _P, _P]),
+    "rpst_whiten_and_color_original_f64": (_I, [_P, _P, _P, _I, _I64, _P, _SZ, _P]),
+    "rpst_whiten_and_color_status": (_I, [_P, _I, _I64, _P, _P]),
     "rpst_conv2d_mix_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),
     "rpst_conv2d_mix": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _SZ,
                              _P]),

@@ -306,7 +306,8 @@ class _WCTRPStep(torch.autograd.Function):
             n = content.shape[0]
             feats = plan.run(plan.compile_layers(model.rp_shared_encoder.children()),
                              torch.cat([content, style], dim=0))
-            t = ops.wct_fuse(feats[:n], feats[n:])
+            # per-image WCT status (device): train.py checks it after the step's loss sync
+            t, model._wct_status = ops.wct_fuse(feats[:n], feats[n:], status=True)
             dec_steps = plan.compile_layers(model.rp_decoder.children())
             stylized, dec_saved = _run_steps_saving(dec_steps, t)
             loss = _VGGLoss(model, stylized, content, style, cw, sw)

@@ -13,9 +13,9 @@ test driver does around `network.test()` (test.py:117-150, datasets/base.py:51-1
              x*255+0.5 clamped to uint8 (test.py:139-149); PNG encoding by PIL on host
              threads.
 
-`Pipeline` overlaps the three: batch k+1 decodes on the thread pool while batch k runs
-on the GPU; pinned host buffers and a copy stream carry the pixels; PNG encoding of
-batch k runs on the writer threads behind a HIP event.
+`Pipeline` overlaps the three: batch k+1 decodes (one task per image) into a pinned buffer
+while batch k runs on the GPU; a copy stream carries the pixels; the PNG encodes of batch k
+(one task per file) start behind a HIP event while batch k+1 computes.
 """
 from __future__ import annotations
 
@@ -89,9 +89,10 @@ def load_image(path: str, size: int) -> np.ndarray:
         return np.asarray(im, dtype=np.uint8).copy()
 
 
-def save_png(arr: np.ndarray, path: str) -> None:
+def save_png(arr: np.ndarray, path: str, level: int = 6) -> None:
+    """torchvision.utils.save_image's file write: PIL PNG (zlib level 6 by default)."""
     from PIL import Image
-    Image.fromarray(arr).save(path)
+    Image.fromarray(arr).save(path, compress_level=level)
 
 
 # ---- GPU pixel conversions -------------------------------------------------------------
@@ -141,25 +142,37 @@ class Pipeline:
     """Stylise a paired dataset batch by batch and write `{cn}-{sn}.png` and
     `{cn}-{sn}-cat.png` (test.py:128-150) into out_dir.
 
-    stylize(content, style) -> stylized runs on `device` (e.g. a model's `test`)."""
+    stylize(content, style) -> stylized runs on `device` (e.g. a model's `test`).
+
+    Host work is per image on thread pools (PIL releases the GIL in decode, resize and
+    zlib): batch k + 1 decodes straight into a pinned buffer while batch k runs on the GPU,
+    and the PNG encodes of batch k are queued as soon as its pixels are back on the host (a
+    HIP event on the copy stream), one task per file. png_level: zlib level of the PNGs
+    (PIL's default 6 is what torchvision.save_image writes; the pixels are identical at any
+    level, lower levels encode faster)."""
 
     def __init__(self, stylize: Callable[[torch.Tensor, torch.Tensor], torch.Tensor],
                  device, img_size: int, batch_size: int = 1, num_workers: int = 4,
-                 cat: bool = True):
+                 cat: bool = True, png_level: int = 6):
         self.stylize = stylize
         self.device = torch.device(device)
         self.img_size = img_size
         self.batch_size = max(1, batch_size)
         self.workers = max(1, num_workers)
         self.cat = cat
+        self.png_level = png_level
 
-    def _decode(self, dataset, idx: List[int]):
+    def _decode_start(self, pool, dataset, idx: List[int]):
+        """Queue the decodes of one batch (one task per image) into a pinned buffer."""
         items = [dataset.item(i) for i in idx]
-        pix = np.empty((2, len(idx), self.img_size, self.img_size, 3), dtype=np.uint8)
-        for j, it in enumerate(items):
-            pix[0, j] = load_image(it[0], self.img_size)
-            pix[1, j] = load_image(it[1], self.img_size)
-        return items, torch.from_numpy(pix).pin_memory()
+        pinned = torch.empty((2, len(idx), self.img_size, self.img_size, 3), dtype=torch.uint8,
+                             pin_memory=True)
+        pix = pinned.numpy()
+
+        def load(k, j, path):
+            pix[k, j] = load_image(path, self.img_size)
+        futs = [pool.submit(load, k, j, it[k]) for j, it in enumerate(items) for k in (0, 1)]
+        return items, pinned, futs
 
     def run(self, dataset, out_dir: str, log: Optional[Callable[[str], None]] = None) -> int:
         os.makedirs(out_dir, exist_ok=True)
@@ -168,15 +181,17 @@ class Pipeline:
         if not batches:
             return 0
         copy_stream = torch.cuda.Stream(self.device)
-        written = 0
         with ThreadPoolExecutor(self.workers) as readers, \
                 ThreadPoolExecutor(self.workers) as writers, torch.no_grad():
-            pending = [readers.submit(self._decode, dataset, batches[0])]
+            pending = [self._decode_start(readers, dataset, batches[0])]
             saves = []
+            back = None  # (event, items, host buffers) of the previous batch
             for k in range(len(batches)):
                 if k + 1 < len(batches):  # decode the next batch while this one runs
-                    pending.append(readers.submit(self._decode, dataset, batches[k + 1]))
-                items, pinned = pending.pop(0).result()
+                    pending.append(self._decode_start(readers, dataset, batches[k + 1]))
+                items, pinned, futs = pending.pop(0)
+                for f in futs:
+                    f.result()
                 with torch.cuda.stream(copy_stream):
                     dev_u8 = pinned.to(self.device, non_blocking=True)
                 compute = torch.cuda.current_stream(self.device)
@@ -195,18 +210,28 @@ class Pipeline:
                         h.copy_(o, non_blocking=True)
                     done = torch.cuda.Event()
                     done.record(copy_stream)
-                saves.append(writers.submit(self._write, done, items, host, out_dir, log))
-            for f in saves:
-                written += f.result()
-        return written
+                # the previous batch's pixels are back by now (its work was queued first):
+                # queue its encodes while this batch computes
+                if back is not None:
+                    saves += self._write_start(writers, *back, out_dir, log)
+                back = (done, items, host)
+            saves += self._write_start(writers, *back, out_dir, log)
+            return sum(f.result() for f in saves)
 
-    @staticmethod
-    def _write(done, items, host, out_dir, log) -> int:
+    def _write_start(self, pool, done, items, host, out_dir, log):
         done.synchronize()
+        level = self.png_level
+
+        def save(arr, path, name):
+            save_png(arr, path, level)
+            if log and name:
+                log(f"Proceed {name}.")
+            return 1 if name else 0
+        futs = []
         for j, (_, _, cn, sn, _, _) in enumerate(items):
-            save_png(host[0][j].numpy(), os.path.join(out_dir, f"{cn}-{sn}.png"))
+            futs.append(pool.submit(save, host[0][j].numpy(),
+                                    os.path.join(out_dir, f"{cn}-{sn}.png"), f"{cn}-{sn}"))
             if len(host) > 1:
-                save_png(host[1][j].numpy(), os.path.join(out_dir, f"{cn}-{sn}-cat.png"))
-            if log:
-                log(f"Proceed {cn}-{sn}.")
-        return len(items)
+                futs.append(pool.submit(save, host[1][j].numpy(),
+                                        os.path.join(out_dir, f"{cn}-{sn}-cat.png"), None))
+        return futs

@@ -437,10 +437,11 @@ def sanet_attention(F: torch.Tensor, G: torch.Tensor, H: torch.Tensor) -> torch.
     hw = h * w
     out = torch.empty_like(F)
     lib = _lib.load()
-    per_img = lib.rpst_sanet_attention_workspace_size(1, hw)
-    chunk = max(1, min(B, SANET_WS_CAP // max(per_img, 1)))
-    ws_bytes = lib.rpst_sanet_attention_workspace_size(chunk, hw)
-    ws = torch.empty(ws_bytes, device=F.device, dtype=torch.uint8)
+    # flash path (S never written): no workspace, the whole batch in one launch
+    per_img = lib.rpst_sanet_attention_workspace_size_c(1, C, hw)
+    chunk = B if per_img == 0 else max(1, min(B, SANET_WS_CAP // per_img))
+    ws_bytes = lib.rpst_sanet_attention_workspace_size_c(chunk, C, hw)
+    ws = torch.empty(max(ws_bytes, 16), device=F.device, dtype=torch.uint8)
     for b0 in range(0, B, chunk):
         nb = min(chunk, B - b0)
         with _traced(f"sanet_attention C{C} HW{hw} N{nb}", 4.0 * nb * hw * hw * C, 0.0):
@@ -523,7 +524,9 @@ def adaptive_attention(F: torch.Tensor, G: torch.Tensor, H: torch.Tensor,
     ws = torch.empty(ws_bytes, device=F.device, dtype=torch.uint8)
     for b0 in range(0, B, chunk):
         nb = min(chunk, B - b0)
-        flops = nb * (6.0 * hw * hw * C + 2.0 * hw * hw * hid)
+        # S = F^T G and O = H Q^T (4 HW^2 C) + f_psi's first Linear without the affinity:
+        # T = sn W1^T, Z = cn^T T (4 C hid HW); DESIGN.md §1 f3
+        flops = nb * (4.0 * hw * hw * C + 4.0 * C * hid * hw)
         with _traced(f"adaptive_attention C{C} HW{hw} N{nb}", flops, 0.0):
             _lib.call("rpst_adaptive_attention", F[b0].data_ptr(), G[b0].data_ptr(),
                       H[b0].data_ptr(), content[b0].data_ptr(), style[b0].data_ptr(),
@@ -556,25 +559,67 @@ def matrix_power_psd(A: torch.Tensor, p: float) -> torch.Tensor:
     return out
 
 
-def whiten_and_color(cF: torch.Tensor, sF: torch.Tensor) -> torch.Tensor:
-    """WCTRPNet.whiten_and_color closed-form (wct_rp.py:82-114): (C,HW) fp64 -> fp64."""
+def whiten_and_color(cF: torch.Tensor, sF: torch.Tensor, method: str = 'closed-form',
+                     status: bool = False):
+    """WCTRPNet.whiten_and_color (wct_rp.py:82-114): (C,HW) fp64 -> fp64. method
+    'closed-form' (Lu et al., :102-111) or 'original' (Li et al., :96-101: matrix_sqrt(Cs)
+    matrix_inv_sqrt(Cc) in the reference's SVD form). status=True also returns the (1,)
+    int32 device status word (rpst_whiten_and_color_status; always 0 for 'original', whose
+    Jacobi fallback recomputes any matrix Newton-Schulz could not take)."""
     assert cF.dim() == 2 and cF.shape == sF.shape
+    assert method in ('closed-form', 'original'), method
     _check(cF, sF, dtype=torch.float64)
     cF, sF = _c(cF), _c(sF)
     C, hw = cF.shape
     out = torch.empty_like(cF)
-    res = torch.empty(2, device=cF.device, dtype=torch.float64)
     nbytes = _lib.load().rpst_wct_workspace_size(1, C, hw)
     ws = torch.empty(nbytes, device=cF.device, dtype=torch.uint8)
-    _lib.call("rpst_whiten_and_color_f64", cF.data_ptr(), sF.data_ptr(), out.data_ptr(), C, hw,
-              res.data_ptr(), ws.data_ptr(), nbytes, _stream(cF))
-    return out
+    if method == 'original':
+        _lib.call("rpst_whiten_and_color_original_f64", cF.data_ptr(), sF.data_ptr(),
+                  out.data_ptr(), C, hw, ws.data_ptr(), nbytes, _stream(cF))
+    else:
+        res = torch.empty(2, device=cF.device, dtype=torch.float64)
+        _lib.call("rpst_whiten_and_color_f64", cF.data_ptr(), sF.data_ptr(), out.data_ptr(), C,
+                  hw, res.data_ptr(), ws.data_ptr(), nbytes, _stream(cF))
+    if not status:
+        return out
+    st = torch.empty(1, device=cF.device, dtype=torch.int32)
+    if method == 'original':
+        st.zero_()
+    else:
+        _lib.call("rpst_whiten_and_color_status", ws.data_ptr(), C, hw, st.data_ptr(),
+                  _stream(cF))
+    return out, st
 
 
-def wct_fuse(content: torch.Tensor, style: torch.Tensor) -> torch.Tensor:
+WCT_NOCONV = 1   # include/rpst.h RPST_WCT_NOCONV
+WCT_TIMEOUT = 4  # include/rpst.h RPST_WCT_TIMEOUT
+
+
+def check_wct_status(status: torch.Tensor, what: str = "wct") -> None:
+    """Host check of a WCT status vector (synchronises on it): raises RuntimeError naming
+    the images whose matrices did not converge or whose persistent launch timed out (their
+    outputs are NaN, never silently wrong). For callers that want failures surfaced (tests,
+    train.py with RPST_WCT_CHECK=1); the inference path itself never synchronises."""
+    st = status.cpu()
+    bad = torch.nonzero(st).flatten().tolist()
+    if bad:
+        why = {i: "+".join(w for f, w in ((WCT_TIMEOUT, "timeout"), (WCT_NOCONV, "no-convergence"))
+                           if int(st[i]) & f) for i in bad}
+        raise RuntimeError(f"{what}: invalid WCT matrices for images {why} (outputs are NaN)")
+
+
+def _wct_status(ws: torch.Tensor, n: int, C: int, hw: int, dev) -> torch.Tensor:
+    st = torch.empty(n, device=dev, dtype=torch.int32)
+    _lib.call("rpst_wct_status", ws.data_ptr(), n, C, hw, st.data_ptr(), _stream(st))
+    return st
+
+
+def wct_fuse(content: torch.Tensor, style: torch.Tensor, status: bool = False):
     """WCTRPNet.fuse (wct_rp.py:157-166): (n,C,h,w) fp32 -> fp32, fp64 internals. The matrix
     functions iterate on the device (no host synchronisation); an image whose Newton-Schulz
-    iteration cannot converge (non-finite features) comes out NaN."""
+    iteration cannot converge (non-finite features) or whose persistent launch timed out comes
+    out NaN. status=True also returns the (n,) int32 per-image status (rpst_wct_status)."""
     assert content.dim() == 4 and content.shape == style.shape
     _check(content, style)
     content, style = _c(content), _c(style)
@@ -586,12 +631,16 @@ def wct_fuse(content: torch.Tensor, style: torch.Tensor) -> torch.Tensor:
     with _traced(f"wct_fuse C{C} {h * w}px N{n}", 6.0 * n * C * C * h * w, 0.0):
         _lib.call("rpst_wct_fuse", content.data_ptr(), style.data_ptr(), out.data_ptr(), n, C,
                   h * w, res.data_ptr(), ws.data_ptr(), nbytes, _stream(content))
+    if status:
+        return out, _wct_status(ws, n, C, h * w, content.device)
     return out
 
 
-def wct_params(content: torch.Tensor, style: torch.Tensor, means: Optional[torch.Tensor] = None):
+def wct_params(content: torch.Tensor, style: torch.Tensor, means: Optional[torch.Tensor] = None,
+               status: bool = False):
     """The closed-form WCT matrices of every image without the product (wct_rp.py:85-109):
-    returns (T (n,C,C) fp64, offset c = mu_s - T mu_c (n,C) fp64, residual (2n,) fp64).
+    returns (T (n,C,C) fp64, offset c = mu_s - T mu_c (n,C) fp64, residual (2n,) fp64), plus
+    the (n,) int32 status with status=True (rpst_wct_status: 0 valid; NaN T / c otherwise).
     means: optional (2n, C) fp32 row means, content rows first (the encoder epilogue's)."""
     assert content.dim() == 4 and content.shape == style.shape
     _check(content, style, means)
@@ -609,6 +658,8 @@ def wct_params(content: torch.Tensor, style: torch.Tensor, means: Optional[torch
         _lib.call("rpst_wct_params", content.data_ptr(), style.data_ptr(), _ptr(means),
                   T.data_ptr(), c.data_ptr(), n, C, h * w, res.data_ptr(), ws.data_ptr(), nbytes,
                   _stream(content))
+    if status:
+        return T, c, res, _wct_status(ws, n, C, h * w, content.device)
     return T, c, res
 
 

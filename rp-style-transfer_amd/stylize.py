@@ -81,6 +81,9 @@ def main(argv=None) -> int:
     ap.add_argument("--synthetic-weights", type=int, default=None, metavar="SEED",
                     help="use rpst.synth weights instead of vgg / checkpoints")
     ap.add_argument("--device", default="cuda:0")
+    ap.add_argument("--png-compress-level", type=int, default=6,
+                    help="zlib level of the written PNGs (6 = torchvision save_image's; the "
+                         "pixels are identical at every level, 1 encodes ~3x faster)")
     args = ap.parse_args(argv)
     with open(args.config) as f:
         opt = yaml.safe_load(f)
@@ -98,7 +101,8 @@ def main(argv=None) -> int:
 
     with torch.cuda.device(device):
         n = Pipeline(stylize, device, opt["img_size"], opt.get("batch_size", 1),
-                     opt.get("num_workers", 4)).run(dataset, str(out_dir), log=logger.info)
+                     opt.get("num_workers", 4), png_level=args.png_compress_level).run(
+                         dataset, str(out_dir), log=logger.info)
     logger.info(f"stylised {n} pairs into {out_dir}")
     return 0
 

@@ -139,6 +139,7 @@ def main(argv=None) -> int:
     import yaml
 
     import stylize
+    from rpst import ops
     from rpst.imageio import DATASETS, Pipeline
     from rpst.shard import GradientAllReduce
 
@@ -193,6 +194,10 @@ def main(argv=None) -> int:
         if rank != 0:
             continue
         scalars = {k: float(v.detach()) for k, v in loss_dict.items()}
+        if getattr(network, "_wct_status", None) is not None:
+            # WCTRPNet: an image whose fp64 matrices failed (non-convergence, or a timed-out
+            # persistent launch) would train on a NaN feature; surface it (the step is synced)
+            ops.check_wct_status(network._wct_status, f"iteration {i}")
         elapsed = round(time.time() - start, 2)
         log.write(json.dumps({"iteration": _begin(network) + i, "elapsed": elapsed,
                               **scalars}) + "\n")

@@ -254,6 +254,40 @@ def gen_wct_edge(net):
     np.savez_compressed(os.path.join(HERE, "wct_edge.npz"), **out)
 
 
+def wct_original_inputs():
+    """Inputs of gen_wct_original (regenerated by the tests): whiten_and_color(method=
+    'original') (Li et al., wct_rp.py:96-101) on small ReLU features, one with a dead style
+    channel (singular style covariance: matrix_sqrt's SVD form at the 1e-4 floor), and at
+    C = 256 on conditioned features (stored as probe products)."""
+    from rpst import synth
+    cases = []
+    for i, (cdim, hw) in enumerate([(16, 256), (64, 1024), (32, 100)]):
+        cf = rand_feat(600 + i, (cdim, hw), scale=2.0, offset=0.3, relu=True).astype(np.float64)
+        sf = rand_feat(700 + i, (cdim, hw), scale=1.5, offset=0.5, relu=True).astype(np.float64)
+        if i == 2:
+            sf[5] = 0.0
+        cases.append((cf, sf, None))
+    cdim, hw = 256, 2048
+    cf = synth.conditioned_features(960, cdim, hw, 1.5)
+    sf = synth.conditioned_features(961, cdim, hw, 3.0)
+    ph = 2.0 * synth.uniform01(960, "hwprobe", hw * 4).reshape(hw, 4) - 1.0
+    cases.append((cf, sf, ph))
+    return cases
+
+
+def gen_wct_original(net):
+    m = net.WCTRPNet(rp_config(2), copy.deepcopy(net.vgg))
+    out = {}
+    for i, (cf, sf, ph) in enumerate(wct_original_inputs()):
+        wc = m.whiten_and_color(t(cf), t(sf), method='original').numpy()
+        if ph is None:
+            out[f"wc{i}"] = wc
+        else:
+            out[f"wcP{i}"] = wc @ ph
+            out[f"wcCols{i}"] = wc[:, :32].copy()
+    np.savez_compressed(os.path.join(HERE, "wct_original.npz"), **out)
+
+
 def gen_sanet(net):
     from network.sanet import SANet, Transform, mean_variance_norm
     out = {}
@@ -649,7 +683,7 @@ GENERATORS = {"keys": gen_keys, "stats": gen_stats, "adain_rp": gen_adain_rp,
               "grads_wct": gen_grads_wct, "wct_large": gen_wct_large,
               "grads_sam": gen_grads_sam, "grads_src": gen_grads_src,
               "grads_ms": gen_grads_ms, "wct_edge": gen_wct_edge,
-              "grads_adaptive": gen_grads_adaptive}
+              "grads_adaptive": gen_grads_adaptive, "wct_original": gen_wct_original}
 
 
 def main():

@@ -112,6 +112,57 @@ def test_adaptive_attention_peaked(cuda, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", [(2, 512, 32, 32), (2, 48, 8, 10)])
+def test_factored_clamp_production_shape(cuda, mode, shape):
+    """The factored AEA clamp (Z = cn^T (sn W1^T), dW1 = (cn du)^T sn: the B x HW x HW
+    affinity never formed) at a production shape (C = 512, HW = 1024, hid = 64) and at a
+    ragged hidden width (HW = 80 -> hid = 5), forward clamp and backward dW1 / db1 / dW2 / db2
+    against the float64 two-GEMM form (affinity formed, torch autograd)."""
+    import network as net
+    from rpst import _lib, ops
+    B, C, h, w = shape
+    hw = h * w
+    mod = net.AEAModule(hw) if mode == "aea" else net.AEALReluModule(hw)
+    synth_(mod, 11)
+    hid = mod.f_psi[0].out_features
+    assert hid == hw // 16
+    sd = {k: v.double().clone().requires_grad_(True) for k, v in state_dict_of(mod).items()}
+    F = gen(21, (B, C, h, w), 0.2)
+    G = gen(22, (B, C, h, w), 0.2)
+    H = gen(23, (B, C, h, w), 1.0)
+    c = gen(24, (B, C, h, w), 1.0, 0.2, relu=True)
+    s = gen(25, (B, C, h, w), 1.0, 0.2, relu=True)
+    dO = gen(26, (B, C, h, w), 1.0)
+    S = torch.bmm(F.view(B, C, -1).permute(0, 2, 1).double(), G.view(B, C, -1).double())
+    A = R.cal_affinity_matrix(c.double(), s.double())
+    Q, clamp = R.aea(A, torch.softmax(S, -1), sd, "", mode)
+    O = torch.bmm(H.view(B, C, -1).double(), Q.permute(0, 2, 1))
+    (O * dO.view(B, C, -1).double()).sum().backward()
+    mod = mod.to(cuda)
+    args = [x.to(cuda) for x in (F, G, H, c, s)]
+    with torch.no_grad():
+        out, cl, _, _ = ops.adaptive_attention(*args, mod.f_psi, mod.mode, 50.0, 0.4, 0.5,
+                                               keep_claims=True)
+    assert rel_l2(cl, clamp.detach()) < 1e-6, rel_l2(cl, clamp.detach())
+    assert rel_l2(out, O.detach().view(B, C, h, w)) < 1e-5
+    w1, b1, w2, b2, hid2 = ops._mlp_params(mod.f_psi)
+    assert hid2 == hid
+    dF, dG, dH = (torch.empty_like(a) for a in args[:3])
+    dw1, db1, dw2, db2 = (torch.empty_like(x) for x in (w1, b1, w2, b2))
+    nbytes = _lib.load().rpst_adaptive_attention_backward_workspace_size(B, C, hw, hid)
+    ws = torch.empty(nbytes, device=cuda, dtype=torch.uint8)
+    _lib.call("rpst_adaptive_attention_backward", *(a.data_ptr() for a in args),
+              w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(), hid, mod.mode, 50.0,
+              0.4, 0.5, dO.to(cuda).data_ptr(), dF.data_ptr(), dG.data_ptr(), dH.data_ptr(),
+              dw1.data_ptr(), db1.data_ptr(), dw2.data_ptr(), db2.data_ptr(), B, C, hw,
+              ws.data_ptr(), nbytes, ops._stream(args[0]))
+    for got, key in ((dw1, "f_psi.0.weight"), (db1, "f_psi.0.bias"), (dw2, "f_psi.2.weight"),
+                     (db2, "f_psi.2.bias")):
+        ref = sd[key].grad
+        assert rel_l2(got.view_as(ref), ref) < 1e-4, (key, rel_l2(got.view_as(ref), ref))
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_adaptive_transform_golden(cuda, golden, mode):
     import network as net
     g = golden("adaptive")

@@ -110,6 +110,54 @@ def test_sanet_attention_large_logits(cuda):
     assert rel_l2(out, ref) < 1e-5
 
 
+def _attn_ref64(F, G, H, rows=None):
+    """float64 O = H softmax(F^T G)^T (sanet.py:86-94), optionally for a subset of queries."""
+    B, C = F.shape[:2]
+    Fq = F.view(B, C, -1).double()
+    if rows is not None:
+        Fq = Fq[:, :, rows]
+    S = torch.bmm(Fq.permute(0, 2, 1), G.view(B, C, -1).double())
+    return torch.bmm(H.view(B, C, -1).double(), torch.softmax(S, -1).permute(0, 2, 1))
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 12, 15), (1, 128, 9, 20), (3, 256, 8, 8),
+                                   (2, 512, 16, 17), (1, 40, 6, 6)])
+def test_sanet_attention_flash_shapes(cuda, shape):
+    """Flash-style attention (S never written) on ragged key / query counts (HW % 16 != 0,
+    HW < 64), every supported C, and a C that takes the materialised-S path (40), against
+    float64; the two paths agree within fp32 rounding."""
+    from rpst import _lib, ops
+    B, C, h, w = shape
+    F = gen(31, shape, 0.6)
+    G = gen(32, shape, 0.6)
+    H = gen(33, shape, 1.0)
+    ref = _attn_ref64(F, G, H).view(shape)
+    out = ops.sanet_attention(F.to(cuda), G.to(cuda), H.to(cuda))
+    assert rel_l2(out, ref) < 1e-5, rel_l2(out, ref)
+    flash = _lib.load().rpst_sanet_attention_workspace_size_c(B, C, h * w) == 0
+    assert flash == (C in (64, 128, 256, 512) and (h * w) % 4 == 0)
+
+
+def test_sanet_attention_relu4_1_at_1024(cuda):
+    """The relu4_1 shape of a 1024x1024 image (HW = 16384, C = 512): the flash path needs no
+    B x HW x HW workspace (1 GiB per image materialised); checked on 256 queries against
+    float64."""
+    from rpst import _lib, ops
+    shape = (1, 512, 128, 128)
+    assert _lib.load().rpst_sanet_attention_workspace_size_c(1, 512, 128 * 128) == 0
+    F = gen(41, shape, 0.2)
+    G = gen(42, shape, 0.2)
+    H = gen(43, shape, 1.0)
+    torch.cuda.synchronize()
+    before = torch.cuda.max_memory_allocated()
+    out = ops.sanet_attention(F.to(cuda), G.to(cuda), H.to(cuda))
+    torch.cuda.synchronize()
+    assert torch.cuda.max_memory_allocated() - before < (1 << 28)  # far below 1 GiB of S
+    rows = torch.arange(0, 16384, 64)
+    ref = _attn_ref64(F, G, H, rows)
+    assert rel_l2(out.view(1, 512, -1)[:, :, rows.to(cuda)], ref) < 1e-5
+
+
 def test_samodel_vs_oracle_64(cuda):
     import network as net
     from rpst import synth
@@ -255,6 +303,75 @@ def test_whiten_and_color_dead_channel_512(cuda, golden):
     assert np.isfinite(wc).all()
     assert rel_l2(wc @ ph, g["wcP"]) < 1e-9, rel_l2(wc @ ph, g["wcP"])
     assert rel_l2(wc[:, :32], g["wcCols"]) < 1e-9, rel_l2(wc[:, :32], g["wcCols"])
+
+
+def test_whiten_and_color_original_golden(cuda, golden):
+    """whiten_and_color(method='original') (Li et al., wct_rp.py:96-101) through
+    rpst_whiten_and_color_original_f64 against the reference (tests/golden/wct_original.npz):
+    small ReLU features, a dead style channel, and C = 256 on conditioned features."""
+    import os
+    import sys
+    import network as net
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from gen_golden import wct_original_inputs
+    g = golden("wct_original")
+    m = net.WCTRPNet(rp_config(2), copy.deepcopy(net.vgg))
+    for i, (cf, sf, ph) in enumerate(wct_original_inputs()):
+        wc = m.whiten_and_color(t(cf).to(cuda), t(sf).to(cuda), method='original').cpu().numpy()
+        assert np.isfinite(wc).all(), i
+        if ph is None:
+            assert rel_l2(wc, g[f"wc{i}"]) < 1e-10, (i, rel_l2(wc, g[f"wc{i}"]))
+        else:
+            assert rel_l2(wc @ ph, g[f"wcP{i}"]) < 1e-10, (i, rel_l2(wc @ ph, g[f"wcP{i}"]))
+            assert rel_l2(wc[:, :32], g[f"wcCols{i}"]) < 1e-10, i
+
+
+def test_wct_status_clean(cuda):
+    """A normal batch reports status 0 for every image (rpst_wct_status)."""
+    from rpst import ops
+    c = gen(61, (4, 128, 16, 24), 1.0, 0.5, relu=True).to(cuda)
+    s = gen(62, (4, 128, 16, 24), 1.5, 0.3, relu=True).to(cuda)
+    _, _, _, st = ops.wct_params(c, s, status=True)
+    assert st.cpu().tolist() == [0, 0, 0, 0]
+    out, st2 = ops.wct_fuse(c, s, status=True)
+    assert st2.cpu().tolist() == [0, 0, 0, 0] and torch.isfinite(out).all()
+    ops.check_wct_status(st)  # no raise
+
+
+def test_wct_barrier_timeout_is_nan_not_wrong(cuda, monkeypatch):
+    """Forced barrier timeout in the persistent matrix-function launch (debug knob
+    RPST_MATFUN_DEBUG_SKIP: one workgroup of group 0 never arrives, as if not resident): the
+    matrices of that group come back NaN with RPST_WCT_TIMEOUT in their status, and every
+    other image is either flagged and NaN or unflagged and bit-identical to a clean run --
+    never finite and wrong."""
+    from rpst import ops
+    n = 8
+    c = gen(63, (n, 128, 16, 20), 1.0, 0.5, relu=True).to(cuda)
+    s = gen(64, (n, 128, 16, 20), 1.5, 0.3, relu=True).to(cuda)
+    T0, c0, _, st0 = ops.wct_params(c, s, status=True)
+    assert st0.cpu().tolist() == [0] * n
+    monkeypatch.setenv("RPST_MATFUN_DEBUG_SKIP", "1")
+    T1, c1, _, st1 = ops.wct_params(c, s, status=True)
+    fused, st2 = ops.wct_fuse(c, s, status=True)
+    monkeypatch.delenv("RPST_MATFUN_DEBUG_SKIP")
+    torch.cuda.synchronize()
+    for st, what in ((st1, "params"), (st2, "fuse")):
+        st = st.cpu()
+        assert int(st[0]) & ops.WCT_TIMEOUT, (what, st.tolist())
+    st1 = st1.cpu()
+    for b in range(n):
+        if int(st1[b]):
+            assert torch.isnan(T1[b]).all() and torch.isnan(c1[b]).all(), b
+        else:
+            assert torch.equal(T1[b], T0[b]) and torch.equal(c1[b], c0[b]), b
+    assert torch.isnan(fused[0]).all()
+    for b in range(n):
+        assert torch.isnan(fused[b]).all() if int(st2[b]) else torch.isfinite(fused[b]).all()
+    with pytest.raises(RuntimeError, match="timeout"):
+        ops.check_wct_status(st1)
+    # the next call on a clean launch is valid again
+    T2, _, _, st3 = ops.wct_params(c, s, status=True)
+    assert st3.cpu().tolist() == [0] * n and torch.equal(T2, T0)
 
 
 def test_wct_large_mean_features(cuda):

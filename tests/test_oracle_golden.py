@@ -138,6 +138,22 @@ def test_wct_edge_reference(golden):
     assert 5e3 < float(g["style_cov_max_eig"]) < 2e4
 
 
+def test_wct_original_reference(golden):
+    """whiten_and_color(method='original') (Li et al., wct_rp.py:96-101) of the oracle against
+    the reference (gen_golden.gen_wct_original), including a dead style channel and C = 256."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from gen_golden import wct_original_inputs
+    g = golden("wct_original")
+    for i, (cf, sf, ph) in enumerate(wct_original_inputs()):
+        wc = R.whiten_and_color(t(cf), t(sf), method='original').numpy()
+        if ph is None:
+            assert rel_l2(wc, g[f"wc{i}"]) < 1e-12, i
+        else:
+            assert rel_l2(wc @ ph, g[f"wcP{i}"]) < 1e-11, i
+            assert rel_l2(wc[:, :32], g[f"wcCols{i}"]) < 1e-11, i
+
+
 def test_wct_rp_test(golden):
     import network as net
     g = golden("wct")

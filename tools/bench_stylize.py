@@ -1,0 +1,131 @@
+"""Throughput of the test driver's host pipeline (stylize.py -> rpst.imageio.Pipeline, the
+counterpart of test.py:117-150) against bare AdaINRPNet.test() on resident tensors.
+
+Writes N synthetic photo-like PNG pairs at 512x512 (smooth gradients, sinusoids and mild
+noise, so zlib sees image-like data) into a scratch directory, then times on one GPU:
+  test_img_s      AdaINRPNet.test() at batch B on tensors already in HBM (bench.py's step)
+  pipeline_img_s  Pipeline.run over the N pairs: PNG decode + resize on host threads, H2D of
+                  uint8 pixels, ToTensor on the GPU, test(), save_image's pixel path on the
+                  GPU, D2H, PNG encode of {cn}-{sn}.png and the 3-up -cat.png on host threads
+  decode / encode host rates with the same thread counts, alone (the host-side bound)
+at PNG zlib level 6 (torchvision.save_image's) and 1 (same pixels, faster encode).
+
+    python tools/bench_stylize.py [--pairs 128] [--batch 32] [--workers 8]
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rp-style-transfer_amd"))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def photo_like(seed, size):
+    r = np.random.default_rng(seed)
+    y, x = np.mgrid[0:size, 0:size].astype(np.float32) / size
+    img = np.empty((size, size, 3), np.float32)
+    for c in range(3):
+        a, b, f1, f2 = r.uniform(0.2, 0.8), r.uniform(-0.5, 0.5), r.uniform(1, 6), r.uniform(1, 6)
+        img[..., c] = a + b * x + 0.2 * np.sin(2 * np.pi * (f1 * x + r.uniform())) * np.cos(
+            2 * np.pi * (f2 * y + r.uniform()))
+    img += r.normal(0, 0.02, img.shape).astype(np.float32)
+    return (np.clip(img, 0, 1) * 255 + 0.5).astype(np.uint8)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--workers", type=int, default=8)
+    args = ap.parse_args()
+    import network as net
+    from rpst import synth
+    from rpst.imageio import PairedDataset, Pipeline, load_image, save_png
+    dev = torch.device("cuda:0")
+    root = tempfile.mkdtemp(prefix="rpst_stylize_", dir="/tmp")
+    try:
+        for d in ("content", "style"):
+            os.makedirs(os.path.join(root, d))
+        with ThreadPoolExecutor(args.workers) as pool:
+            list(pool.map(lambda i: save_png(photo_like(i, args.size),
+                                             os.path.join(root, "content", f"im{i:04d}.png")),
+                          range(args.pairs)))
+            list(pool.map(lambda i: save_png(photo_like(10_000 + i, args.size),
+                                             os.path.join(root, "style", f"im{i:04d}.png")),
+                          range(args.pairs)))
+        ds = PairedDataset(root)
+        paths = [p for i in range(len(ds)) for p in ds.item(i)[:2]]
+        rec = {"pairs": args.pairs, "batch": args.batch, "image": f"{args.size}x{args.size}",
+               "workers": args.workers, "host_cpus": os.cpu_count(),
+               "omp_threads": os.environ.get("OMP_NUM_THREADS")}
+        # host-side rates alone
+        with ThreadPoolExecutor(args.workers) as pool:
+            t0 = time.perf_counter()
+            imgs = list(pool.map(lambda p: load_image(p, args.size), paths))
+            rec["decode_pairs_s"] = round(args.pairs / (time.perf_counter() - t0), 1)
+            cat = np.zeros((args.size + 4, 3 * (args.size + 2) + 2, 3), np.uint8)
+            out = os.path.join(root, "enc")
+            os.makedirs(out)
+            for lvl in (6, 1):
+                t0 = time.perf_counter()
+                futs = [pool.submit(save_png, imgs[2 * i], os.path.join(out, f"{i}.png"), lvl)
+                        for i in range(args.pairs)]
+                futs += [pool.submit(save_png, cat, os.path.join(out, f"{i}c.png"), lvl)
+                         for i in range(args.pairs)]
+                for f in futs:
+                    f.result()
+                rec[f"encode_pairs_s_level{lvl}"] = round(args.pairs / (time.perf_counter() - t0), 1)
+        # bare test() on resident tensors
+        cfg = {"rp_blocks": 5, "hidden_dim": 16, "content_weight": 1.0, "style_weight": 10.0,
+               "resume": False}
+        import copy
+        m = net.AdaINRPNet(cfg, copy.deepcopy(net.vgg))
+        synth.synth_module_(m, 0)
+        m = m.to(dev)
+        c = torch.from_numpy(synth.image(1000, (args.batch, 3, args.size, args.size))).to(dev)
+        s = torch.from_numpy(synth.image(2000, (args.batch, 3, args.size, args.size))).to(dev)
+        for _ in range(2):
+            m.test(c, s)
+        torch.cuda.synchronize()
+        reps = max(1, args.pairs // args.batch)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            m.test(c, s)
+        torch.cuda.synchronize()
+        rec["test_img_s"] = round(reps * args.batch / (time.perf_counter() - t0), 1)
+        del c, s
+        # the pipeline, end to end (a warm-up pass over one batch first)
+        for lvl in (6, 1):
+            pipe = Pipeline(m.test, dev, args.size, args.batch, args.workers, png_level=lvl)
+            warm = PairedDataset(root)
+            warm.content_names = warm.content_names[:args.batch]
+            pipe.run(warm, os.path.join(root, f"warm{lvl}"))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            n = pipe.run(ds, os.path.join(root, f"out{lvl}"))
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            assert n == args.pairs
+            rec[f"pipeline_img_s_level{lvl}"] = round(n / dt, 1)
+        rec["pipeline_vs_test_level6"] = round(rec["pipeline_img_s_level6"] / rec["test_img_s"], 3)
+        rec["pipeline_vs_test_level1"] = round(rec["pipeline_img_s_level1"] / rec["test_img_s"], 3)
+        # the host bound: decode and encode share the CPUs (2 x workers threads)
+        for lvl in (6, 1):
+            d, e = rec["decode_pairs_s"], rec[f"encode_pairs_s_level{lvl}"]
+            rec[f"host_bound_pairs_s_level{lvl}"] = round(1.0 / (1.0 / d + 1.0 / e), 1)
+        print(json.dumps(rec), flush=True)
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
