@@ -274,6 +274,13 @@ int rpst_u8hwc_to_f32nchw(const uint8_t* in, float* out, int N, int H, int W,
 int rpst_f32nchw_to_u8_tile(const float* in, uint8_t* canvas, int N, int H, int W,
                             int canvas_h, int canvas_w, int y0, int x0, rpst_stream_t stream);
 
+/* PNG "Up" filter of N 8-bit images of H rows x rowbytes bytes (e.g. rpst_f32nchw_to_u8_tile's
+ * canvases, rowbytes = 3 W): out (N, H, rowbytes + 1) = per row the filter-type byte 2 then
+ * (row y - row y-1) mod 256 (row -1 = 0), i.e. the PNG IDAT scanlines before zlib, so the host
+ * side of save_image (test.py:139-149) is only the deflate (rpst.imageio.write_png). */
+int rpst_png_filter_up(const uint8_t* in, uint8_t* out, int N, int H, int rowbytes,
+                       rpst_stream_t stream);
+
 /* ---- f2: training backward  AdaINRPNet.forward adain_rp.py:110-138 +
  * total_loss.backward() train.py:186-189. Conv dgrad runs on rpst_conv2d with weights from
  * rpst_conv_weight_flip (packed by rpst_conv2d_pack); reflect-padded convs then add

@@ -49,9 +49,44 @@ __global__ __launch_bounds__(256) void f32_to_u8_tile_kernel(const float* __rest
   }
 }
 
+// PNG "Up" filter (PNG spec 9.2, filter type 2) of N images of H rows x rowbytes bytes:
+// out row y = [2, (row y - row y-1) mod 256 ...] (row -1 = 0), so the host only runs zlib over
+// the filtered scanlines (rpst.imageio.write_png). One thread per 4 output bytes of a row.
+__global__ __launch_bounds__(256) void png_filter_up_kernel(const uint8_t* __restrict__ in,
+                                                            uint8_t* __restrict__ out, int64_t rows,
+                                                            int H, int rowbytes) {
+  const int ob = rowbytes + 1;
+  const int per_row = (ob + 3) >> 2;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= rows * per_row) return;
+  const int64_t r = t / per_row;
+  const int j0 = (int)(t - r * per_row) * 4;
+  const bool first = (r % H) == 0;
+  const uint8_t* cur = in + r * rowbytes;
+  const uint8_t* prev = cur - rowbytes;
+  uint8_t* o = out + r * ob;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int j = j0 + e;
+    if (j >= ob) break;
+    o[j] = j == 0 ? (uint8_t)2 : (uint8_t)(cur[j - 1] - (first ? 0 : prev[j - 1]));
+  }
+}
+
 }  // namespace rpst
 
 using namespace rpst;
+
+extern "C" int rpst_png_filter_up(const uint8_t* in, uint8_t* out, int N, int H, int rowbytes,
+                                  rpst_stream_t stream) {
+  RPST_REQUIRE(in && out, "png_filter_up: null pointer");
+  RPST_REQUIRE(N > 0 && H > 0 && rowbytes > 0, "png_filter_up: bad shape");
+  const int64_t rows = (int64_t)N * H, threads = rows * ((rowbytes + 1 + 3) / 4);
+  RPST_REQUIRE((threads + 255) / 256 <= 0x7fffffffLL, "png_filter_up: too large");
+  png_filter_up_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, as_stream(stream)>>>(
+      in, out, rows, H, rowbytes);
+  return launch_status("png_filter_up_kernel");
+}
 
 extern "C" int rpst_u8hwc_to_f32nchw(const uint8_t* in, float* out, int N, int H, int W,
                                      rpst_stream_t stream) {

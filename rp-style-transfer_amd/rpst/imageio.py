@@ -10,8 +10,8 @@ test driver does around `network.test()` (test.py:117-150, datasets/base.py:51-1
   ToTensor   on the GPU (`rpst_u8hwc_to_f32nchw`): uint8 pixels cross PCIe, 3 B/pixel
   save_image on the GPU (`rpst_f32nchw_to_u8_tile`): make_grid(nrow=3, padding=2,
              pad_value=0) of [content, style, stylized] and the single stylised image,
-             x*255+0.5 clamped to uint8 (test.py:139-149); PNG encoding by PIL on host
-             threads.
+             x*255+0.5 clamped to uint8 (test.py:139-149), then the PNG scanline filter
+             (`rpst_png_filter_up`); the host threads only deflate and write (write_png).
 
 `Pipeline` overlaps the three: batch k+1 decodes (one task per image) into a pinned buffer
 while batch k runs on the GPU; a copy stream carries the pixels; the PNG encodes of batch k
@@ -20,6 +20,7 @@ while batch k runs on the GPU; a copy stream carries the pixels; the PNG encodes
 from __future__ import annotations
 
 import os
+import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -95,7 +96,38 @@ def save_png(arr: np.ndarray, path: str, level: int = 6) -> None:
     Image.fromarray(arr).save(path, compress_level=level)
 
 
+def write_png(path: str, filtered: np.ndarray, level: int = 6) -> None:
+    """PNG file (8-bit RGB) from scanlines already filtered on the GPU (png_filter_up: one
+    filter-type byte + 3 W bytes per row): signature, IHDR, one IDAT = zlib(filtered, level),
+    IEND. zlib and crc32 release the GIL, so writer threads run in parallel. The pixels read
+    back are exactly the canvas's (PNG is lossless at every level and filter)."""
+    import struct
+    import zlib
+    h, ob = filtered.shape
+    w = (ob - 1) // 3
+
+    def chunk(kind: bytes, data: bytes) -> bytes:
+        return (struct.pack(">I", len(data)) + kind + data +
+                struct.pack(">I", zlib.crc32(data, zlib.crc32(kind)) & 0xffffffff))
+    ihdr = struct.pack(">IIBBBBB", w, h, 8, 2, 0, 0, 0)
+    idat = zlib.compress(memoryview(np.ascontiguousarray(filtered)).cast("B"), level)
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"IDAT", idat) +
+                chunk(b"IEND", b""))
+
+
 # ---- GPU pixel conversions -------------------------------------------------------------
+def png_filter_up(u8: torch.Tensor) -> torch.Tensor:
+    """(N, H, W, 3) uint8 on the GPU -> (N, H, 1 + 3 W) PNG scanlines with the Up filter
+    (rpst_png_filter_up), ready for write_png's deflate."""
+    assert u8.dim() == 4 and u8.shape[-1] == 3 and u8.dtype == torch.uint8 and u8.is_cuda
+    u8 = u8.contiguous()
+    n, h, w, _ = u8.shape
+    out = torch.empty((n, h, 1 + 3 * w), device=u8.device, dtype=torch.uint8)
+    _lib.call("rpst_png_filter_up", u8.data_ptr(), out.data_ptr(), n, h, 3 * w, _stream(u8))
+    return out
+
+
 def to_tensor(u8: torch.Tensor) -> torch.Tensor:
     """(N, H, W, 3) uint8 on the GPU -> (N, 3, H, W) fp32 in [0, 1] (transforms.ToTensor)."""
     assert u8.dim() == 4 and u8.shape[-1] == 3 and u8.dtype == torch.uint8 and u8.is_cuda
@@ -153,12 +185,13 @@ class Pipeline:
 
     def __init__(self, stylize: Callable[[torch.Tensor, torch.Tensor], torch.Tensor],
                  device, img_size: int, batch_size: int = 1, num_workers: int = 4,
-                 cat: bool = True, png_level: int = 6):
+                 cat: bool = True, png_level: int = 6, encode_workers: Optional[int] = None):
         self.stylize = stylize
         self.device = torch.device(device)
         self.img_size = img_size
         self.batch_size = max(1, batch_size)
         self.workers = max(1, num_workers)
+        self.encode_workers = max(1, encode_workers or num_workers)
         self.cat = cat
         self.png_level = png_level
 
@@ -181,8 +214,12 @@ class Pipeline:
         if not batches:
             return 0
         copy_stream = torch.cuda.Stream(self.device)
+        # host seconds of the driving thread per phase (bench_stylize.py reports them)
+        st = self.stats = {"wait_decode": 0.0, "launch": 0.0, "wait_d2h": 0.0,
+                           "wait_encode": 0.0}
+        clock = time.perf_counter
         with ThreadPoolExecutor(self.workers) as readers, \
-                ThreadPoolExecutor(self.workers) as writers, torch.no_grad():
+                ThreadPoolExecutor(self.encode_workers) as writers, torch.no_grad():
             pending = [self._decode_start(readers, dataset, batches[0])]
             saves = []
             back = None  # (event, items, host buffers) of the previous batch
@@ -190,8 +227,11 @@ class Pipeline:
                 if k + 1 < len(batches):  # decode the next batch while this one runs
                     pending.append(self._decode_start(readers, dataset, batches[k + 1]))
                 items, pinned, futs = pending.pop(0)
+                t0 = clock()
                 for f in futs:
                     f.result()
+                t1 = clock()
+                st["wait_decode"] += t1 - t0
                 with torch.cuda.stream(copy_stream):
                     dev_u8 = pinned.to(self.device, non_blocking=True)
                 compute = torch.cuda.current_stream(self.device)
@@ -202,6 +242,8 @@ class Pipeline:
                 outs = [to_uint8(stylized)]
                 if self.cat:
                     outs.append(grid_uint8([content, style, stylized]))
+                # PNG scanline filtering on the GPU too: the host only deflates
+                outs = [png_filter_up(o) for o in outs]
                 host = [torch.empty(o.shape, dtype=torch.uint8, pin_memory=True) for o in outs]
                 copy_stream.wait_stream(compute)
                 with torch.cuda.stream(copy_stream):
@@ -210,20 +252,26 @@ class Pipeline:
                         h.copy_(o, non_blocking=True)
                     done = torch.cuda.Event()
                     done.record(copy_stream)
+                t2 = clock()
+                st["launch"] += t2 - t1
                 # the previous batch's pixels are back by now (its work was queued first):
                 # queue its encodes while this batch computes
                 if back is not None:
                     saves += self._write_start(writers, *back, out_dir, log)
+                st["wait_d2h"] += clock() - t2
                 back = (done, items, host)
+            t3 = clock()
             saves += self._write_start(writers, *back, out_dir, log)
-            return sum(f.result() for f in saves)
+            n = sum(f.result() for f in saves)
+            st["wait_encode"] += clock() - t3
+            return n
 
     def _write_start(self, pool, done, items, host, out_dir, log):
         done.synchronize()
         level = self.png_level
 
         def save(arr, path, name):
-            save_png(arr, path, level)
+            write_png(path, arr, level)
             if log and name:
                 log(f"Proceed {name}.")
             return 1 if name else 0

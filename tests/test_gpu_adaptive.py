@@ -145,7 +145,8 @@ def test_factored_clamp_production_shape(cuda, mode, shape):
                                                keep_claims=True)
     assert rel_l2(cl, clamp.detach()) < 1e-6, rel_l2(cl, clamp.detach())
     assert rel_l2(out, O.detach().view(B, C, h, w)) < 1e-5
-    w1, b1, w2, b2, hid2 = ops._mlp_params(mod.f_psi)
+    with torch.no_grad():
+        w1, b1, w2, b2, hid2 = ops._mlp_params(mod.f_psi)
     assert hid2 == hid
     dF, dG, dH = (torch.empty_like(a) for a in args[:3])
     dw1, db1, dw2, db2 = (torch.empty_like(x) for x in (w1, b1, w2, b2))

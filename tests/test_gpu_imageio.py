@@ -39,6 +39,26 @@ def test_save_image_pixels_bit_exact(cuda):
         np.testing.assert_array_equal(grid[b], ref)
 
 
+def test_png_filter_up_and_writer_round_trip(cuda, tmp_path):
+    """rpst_png_filter_up is the PNG spec's Up filter bit for bit, and write_png's files decode
+    (PIL) to exactly the canvas at zlib levels 0, 1 and 6."""
+    from PIL import Image
+    from rpst.imageio import png_filter_up, write_png
+    rng = np.random.default_rng(3)
+    u8 = rng.integers(0, 256, size=(2, 17, 29, 3), dtype=np.uint8)
+    f = png_filter_up(torch.from_numpy(u8).to(cuda)).cpu().numpy()
+    x = u8.reshape(2, 17, 29 * 3).astype(np.int16)
+    ref = np.empty((2, 17, 1 + 29 * 3), np.uint8)
+    ref[:, :, 0] = 2
+    ref[:, 0, 1:] = x[:, 0]
+    ref[:, 1:, 1:] = (x[:, 1:] - x[:, :-1]) & 255
+    np.testing.assert_array_equal(f, ref)
+    for lvl in (0, 1, 6):
+        p = str(tmp_path / f"r{lvl}.png")
+        write_png(p, f[1], lvl)
+        np.testing.assert_array_equal(np.asarray(Image.open(p).convert("RGB")), u8[1])
+
+
 def _write_pairs(root, sizes):
     from PIL import Image
     rng = np.random.default_rng(7)

@@ -35,4 +35,23 @@ for i in range(int(g["n"])):
     m.zero_grad(); _, t = m(torch.from_numpy(g[f"content{i}"]).to(cuda), torch.from_numpy(g[f"style{i}"]).to(cuda)); t.backward()
     nm = dict(m.named_parameters())
     out[f"wct{i}"] = max(rel_l2(nm[str(k)].grad, g[f"grad{i}:{k}"]) for k in g[f"names{i}"])
+# SAModel (grads_sam): probe errors scaled to the test's bar (1e-4; 2e-3 for the softmax-side
+# f / g gradients, tests/test_gpu_train.py), so <= 1e-4 passes like the other cases
+g = load("grads_sam")
+SAM_CFG = {"content_weight": 1.0, "style_weight": 3.0, "l_identity1_weight": 50.0,
+           "l_identity2_weight": 1.0}
+for i in range(int(g["n"])):
+    c = torch.from_numpy(g[f"content{i}"]).to(cuda)
+    m = net.SAModel(dict(SAM_CFG), copy.deepcopy(net.vgg), 0, c.shape[-1])
+    m.decoder = copy.deepcopy(m.decoder); synth_(m, int(g[f"seed{i}"])); m = m.to(cuda)
+    m.zero_grad(); _, t = m(c, torch.from_numpy(g[f"style{i}"]).to(cuda)); t.backward()
+    nm = dict(m.named_parameters())
+    worst = 0.0
+    for k in g[f"names{i}"]:
+        k = str(k)
+        if k.endswith(".g.bias"):
+            continue
+        tol = 2e-3 if k.split(".")[-2] in ("f", "g") else 1e-4
+        worst = max(worst, probe_err(grad_probe(k, nm[k].grad), g[f"gprobe{i}:{k}"], nm[k].grad.numel()) / tol * 1e-4)
+    out[f"sam{i}"] = worst
 print(os.environ.get("RPST_TRAIN_PRECISE", "1"), json.dumps({k: float("%.3g" % v) for k, v in out.items()}))
