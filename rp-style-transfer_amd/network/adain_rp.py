@@ -120,9 +120,13 @@ class AdaINRPNet(BaseNet):
             return adain_rp_losses(self, content, style)
         content_feat, style_feat = encode_both(self.rp_shared_encoder, content, style)
         stylized = self.rp_decoder(AdaIN(content_feat, style_feat))
-        down_stylized_feats = self.encode_with_intermediate(stylized)
-        down_style_feats = self.encode_with_intermediate(style)
-        down_content_feats = self.encode_with_intermediate(content)
+        # the three VGG passes (adain_rp.py:123-125) as one pass over [stylized; style;
+        # content]: the same per-image results (the kernels are batch-invariant bit for bit,
+        # tests/test_gpu_timed.py), one launch sequence and 3x the grid at relu4_1's 64^2
+        n = content.shape[0]
+        feats = self.encode_with_intermediate(torch.cat([stylized, style, content], dim=0))
+        down_stylized_feats, down_style_feats, down_content_feats = (
+            [f[j * n:(j + 1) * n] for f in feats] for j in range(3))
         loss_s = self.calc_style_loss(down_stylized_feats[0], down_style_feats[0])
         for i in range(1, 4):
             loss_s += self.calc_style_loss(down_stylized_feats[i], down_style_feats[i])

@@ -182,11 +182,13 @@ class _VGGLoss:
             vgg_saved += sv
             taps.append(len(vgg_steps) - 1)
         if targets is None:
+            # the targets are constants of the step (no gradient flows into them): F(4x4)
             ref = torch.cat([style, content], dim=0)
             targets = []
-            for i in range(4):
-                ref = getattr(model, f"enc_{i + 1}")(ref)
-                targets.append(ref)
+            with ops.precise_convs(on=False):
+                for i in range(4):
+                    ref = getattr(model, f"enc_{i + 1}")(ref)
+                    targets.append(ref)
         stats, loss_s = [], []
         for i, k in enumerate(taps):
             F = vgg_saved[k][1]
@@ -242,12 +244,12 @@ class _VGGLoss:
 class _AdaINRPStep(torch.autograd.Function):
     @staticmethod
     def forward(ctx, content, style, model, cw, sw, *params):
-        with ops.precise_convs():
+        with ops.precise_convs("adain"):
             return _AdaINRPStep._forward(ctx, content, style, model, cw, sw, *params)
 
     @staticmethod
     def backward(ctx, g_total, g_ls, g_lc):
-        with ops.precise_convs():  # the autograd engine runs this on its own thread
+        with ops.precise_convs("adain"):  # the autograd engine runs this on its own thread
             return _AdaINRPStep._backward(ctx, g_total, g_ls, g_lc)
 
     @staticmethod
@@ -302,10 +304,11 @@ class _WCTRPStep(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, content, style, model, cw, sw, *params):
-        with ops.precise_convs():
+        with ops.precise_convs("wct"):
             n = content.shape[0]
-            feats = plan.run(plan.compile_layers(model.rp_shared_encoder.children()),
-                             torch.cat([content, style], dim=0))
+            with ops.precise_convs(on=False):  # fuse() detaches: a constant of the step
+                feats = plan.run(plan.compile_layers(model.rp_shared_encoder.children()),
+                                 torch.cat([content, style], dim=0))
             # per-image WCT status (device): train.py checks it after the step's loss sync
             t, model._wct_status = ops.wct_fuse(feats[:n], feats[n:], status=True)
             dec_steps = plan.compile_layers(model.rp_decoder.children())
@@ -316,7 +319,7 @@ class _WCTRPStep(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_total, g_ls, g_lc):
-        with ops.precise_convs():
+        with ops.precise_convs("wct"):
             g = ctx.loss.backward(g_total, g_ls, g_lc)
             grads: Dict[int, torch.Tensor] = {}
             _rp_backward(ctx.dec_steps, ctx.dec_saved, g, grads, need_input_grad=False)
@@ -607,18 +610,19 @@ def _transform_backward(tr, saved, g, grads):
 class _SAModelStep(torch.autograd.Function):
     @staticmethod
     def forward(ctx, content, style, model, cfg, *params):
-        with ops.precise_convs():
+        with ops.precise_convs("sanet"):
             return _SAModelStep._forward(ctx, content, style, model, cfg, *params)
 
     @staticmethod
     def backward(ctx, g_total, g_ls, g_lc, g_l1, g_l2):
-        with ops.precise_convs():
+        with ops.precise_convs("sanet"):
             return _SAModelStep._backward(ctx, g_total, g_ls, g_lc, g_l1, g_l2)
 
     @staticmethod
     def _forward(ctx, content, style, model, cfg, *params):
         n = content.shape[0]
-        feats = model.encode_with_intermediate(torch.cat([style, content], dim=0))
+        with ops.precise_convs(on=False):  # frozen VGG of the inputs: constants of the step
+            feats = model.encode_with_intermediate(torch.cat([style, content], dim=0))
         sf = [f[:n].contiguous() for f in feats]
         cf = [f[n:].contiguous() for f in feats]
         dec_steps = plan.compile_layers(model.decoder.children())
@@ -798,12 +802,13 @@ class _SourceNetStep(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, content, style, model, cw, sw, *params):
-        with ops.precise_convs():
+        with ops.precise_convs("source"):
             n = content.shape[0]
             ref, targets = torch.cat([style, content], dim=0), []
-            for i in range(4):
-                ref = getattr(model, f"enc_{i + 1}")(ref)
-                targets.append(ref)
+            with ops.precise_convs(on=False):  # frozen VGG of the inputs: constants
+                for i in range(4):
+                    ref = getattr(model, f"enc_{i + 1}")(ref)
+                    targets.append(ref)
             t = ops.adaptive_instance_normalization(targets[3][n:], targets[3][:n])
             dec_steps = plan.compile_layers(model.decoder.children())
             stylized, dec_saved = _run_steps_saving(dec_steps, t)
@@ -814,7 +819,7 @@ class _SourceNetStep(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_total, g_ls, g_lc):
-        with ops.precise_convs():
+        with ops.precise_convs("source"):
             g = ctx.loss.backward(g_total, g_ls, g_lc)
             grads: Dict[int, torch.Tensor] = {}
             _decoder_backward(ctx.dec_steps, ctx.dec_saved, g, grads, need_input_grad=False)
@@ -836,7 +841,7 @@ class _MultiScaleStep(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, content, style, model, cw, sw, *params):
-        with ops.precise_convs():
+        with ops.precise_convs("multiscale"):
             n = content.shape[0]
             x, enc, levels = torch.cat([content, style], dim=0), [], []
             for blk in model.rp_shared_encoder:
@@ -865,7 +870,7 @@ class _MultiScaleStep(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_total, g_ls, g_lc):
-        with ops.precise_convs():
+        with ops.precise_convs("multiscale"):
             g = ctx.loss.backward(g_total, g_ls, g_lc)
             grads: Dict[int, torch.Tensor] = {}
             L = len(ctx.enc)

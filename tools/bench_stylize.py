@@ -131,8 +131,13 @@ def main():
         del c, s
         # the pipeline, end to end (a warm-up pass over one batch first)
         for lvl in levels:
-            pipe = Pipeline(m.test, dev, args.size, args.batch, args.workers, png_level=lvl,
-                            encode_workers=args.encode_workers)
+            # the thread split follows the bound: deflate-heavy levels get most threads for
+            # encoding; stored PNGs (level 0) are decode-bound, so the split is even there
+            dw, ew = (args.workers, args.encode_workers) if lvl > 0 else (
+                (args.workers + args.encode_workers) // 2,) * 2
+            rec[f"pipeline_threads_level{lvl}"] = [dw, ew]
+            pipe = Pipeline(m.test, dev, args.size, args.batch, dw, png_level=lvl,
+                            encode_workers=ew)
             warm = PairedDataset(root)
             warm.content_names = warm.content_names[:args.batch]
             pipe.run(warm, os.path.join(root, f"warm{lvl}"))

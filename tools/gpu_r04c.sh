@@ -1,13 +1,15 @@
 #!/bin/bash
-# Round 4: 8-wave flash attention (RPST_SANET_FLASH=2) tests + timing vs the 4-wave form and the
-# two-GEMM path; GPU PNG filter tests; the stylize pipeline line
+# Round 4: flash attention variants (1 pipelined 4-wave = default, 2 8-wave, 3 plain 4-wave,
+# 0 two-GEMM) tests + timing; GPU PNG filter tests; stylize pipeline line; training precision A/B
 set -o pipefail
 O=gpurun_out/r04c; mkdir -p $O
-RPST_SANET_FLASH=2 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_models.py -k "attention" > $O/tests_flash2.log 2>&1 || { tail -40 $O/tests_flash2.log; exit 1; }
-grep -E "passed|failed" $O/tests_flash2.log | tail -2
+for f in 1 2; do
+  RPST_SANET_FLASH=$f timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_models.py -k "attention" > $O/tests_flash$f.log 2>&1 || { tail -40 $O/tests_flash$f.log; exit 1; }
+  echo "flash=$f $(grep -E 'passed|failed' $O/tests_flash$f.log | tail -1)"
+done
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_imageio.py > $O/tests_io.log 2>&1 || { tail -40 $O/tests_io.log; exit 1; }
-grep -E "passed|failed" $O/tests_io.log | tail -2
-for f in 2 1 0; do
+grep -E "passed|failed" $O/tests_io.log | tail -1
+for f in 1 2 3 0; do
   RPST_SANET_FLASH=$f timeout -k 10 120 python tools/bench_attn.py --reps 5 > $O/attn_flash$f.json 2>&1 || { tail $O/attn_flash$f.json; exit 1; }
   echo "flash=$f $(tail -1 $O/attn_flash$f.json)"
 done
