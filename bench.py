@@ -642,11 +642,14 @@ def sub_record(cfg_index, meas, kind, size, world, steps, with_cpu):
             if name.startswith("sanet_attention"):
                 avg = a["ms"] / a["launches"]
                 tf = a["flops"] / (avg * 1e-3) / 1e12
+                from rpst import _lib
+                flash = _lib.load().rpst_sanet_attention_workspace_size_c(32, 512, 4096) == 0
                 rec["roofline_attention"] = {
                     "bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP32_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(tf / PEAK_FP32_TFLOPS, 4),
-                    "kernel": f"gemm_f32_kernel + rowstats_kernel [{name}]",
-                    "launch_ms": round(avg, 4)}
+                    "kernel": ("sanet_flash_kernel (S never written)" if flash else
+                               "gemm_f32_kernel + rowstats_kernel") + f" [{name}]",
+                    "launch_ms": round(avg, 4), "flop_basis": "4 HW^2 C per image"}
                 break
     rec["cpu_baseline"] = cpu_baseline(kind, size) if with_cpu else None
     return rec

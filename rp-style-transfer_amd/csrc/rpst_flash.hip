@@ -70,6 +70,22 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
   const int prow = lane >> 2, pseg = lane & 3;
   const unsigned voffG = (unsigned)(prow * HW + 4 * pseg) * 4u;
   const unsigned voffH = (unsigned)(prow * HW + 4 * (pseg ^ ((lane >> 4) & 3))) * 4u;
+  // one DMA piece (jj < PPW: G piece jj, else H piece jj - PPW) of key block k0 / 16; a
+  // step's 2 PPW pieces are spread one per MFMA group (scores: NQ / SG = 2 PPW groups) so each
+  // issue hides in an MFMA gap instead of stalling a clustered run of them
+  auto piece = [&](int jj, int k0g, float* gs, int k0h, float* hs) {
+    const bool isg = jj < PPW;
+    const int j = wave * PPW + (isg ? jj : jj - PPW);
+    if (isg) {
+      if (k0g >= 0)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (attn_lds_ptr_t)(gs + 256 * j), 16, (int)voffG,
+                                                 (16 * j * HW + k0g) * 4, 0, 0);
+    } else if (k0h >= 0) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rH, (attn_lds_ptr_t)(hs + 256 * j), 16, (int)voffH,
+                                               (16 * j * HW + k0h) * 4, 0, 0);
+    }
+  };
+  static_assert(NQ / 8 == 2 * PPW, "one DMA piece per MFMA group of scores()");
   auto issue_g = [&](int k0, float* gs) {
 #pragma unroll
     for (int jj = 0; jj < PPW; ++jj) {
@@ -107,7 +123,7 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
   // double buffering: a wave is alone on its SIMD, so an LDS read the next MFMA waits on
   // leaves the matrix pipe idle for its whole latency)
   constexpr int SG = 8;  // S k-steps per group
-  auto scores = [&](int kb, const float* gs, auto&& after_first_reads) {
+  auto scores = [&](int kb, const float* gs, auto&& group_dma) {
     (void)kb;
     // S^T = G_tile^T Q: two accumulation chains (the 16x16x4 dependent latency is 40 cycles)
     floatx4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
@@ -117,9 +133,9 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
       for (int e = 0; e < SG; ++e) a[e] = gs[(4 * (SG * t + e) + g) * kFBN + lq];
     };
     ld(ga[0], 0);
-    after_first_reads();  // e.g. the next key block's DMA, while the first reads are in flight
 #pragma unroll
     for (int t = 0; t < NQ / SG; ++t) {
+      group_dma(t);  // DMA piece t of the next key blocks
       if (t + 1 < NQ / SG) ld(ga[(t + 1) & 1], t + 1);
       __builtin_amdgcn_sched_barrier(0);  // the reads issue before this group's MFMAs
 #pragma unroll
@@ -189,12 +205,8 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's key tile kb has landed
       __builtin_amdgcn_s_barrier();                     // ... for every wave; the other
       // (the other buffers are free: step kb - 1 is done everywhere)
-      softmax(kb, scores(kb, gs, [&]() {
-        if (kb + 1 < nk) {
-          issue_g((kb + 1) * kFBN, gn);
-          issue_h((kb + 1) * kFBN, hn);
-        }
-      }));
+      const int k1 = kb + 1 < nk ? (kb + 1) * kFBN : -1;
+      softmax(kb, scores(kb, gs, [&](int t) { piece(t, k1, gn, k1, hn); }));
       update(hs);
     };
     for (int kb = 0; kb < nk; kb += 2) {
@@ -209,13 +221,10 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
     auto step = [&](int kb, const float* gs, const float* hprev, float* gn, float* hcur) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // G(kb), H(kb - 1) have landed
       __builtin_amdgcn_s_barrier();
-      auto dma = [&]() {
-        if (kb + 1 < nk) issue_g((kb + 1) * kFBN, gn);
-        if (kb < nk) issue_h(kb * kFBN, hcur);
-      };
+      const int kg = kb + 1 < nk ? (kb + 1) * kFBN : -1, kh = kb < nk ? kb * kFBN : -1;
       floatx4 sc = {0.f, 0.f, 0.f, 0.f};
-      if (kb < nk) sc = scores(kb, gs, dma);
-      else dma();
+      if (kb < nk) sc = scores(kb, gs, [&](int t) { piece(t, kg, gn, kh, hcur); });
+      // (the last iteration has no scores and no DMA left: kg, kh < 0)
       if (kb >= 1) update(hprev);
       if (kb < nk) softmax(kb, sc);
     };

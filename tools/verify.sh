@@ -12,11 +12,15 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -2 $O/smoke.log
 timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail $O/bench_default.err; exit 1; }
 cat $O/bench_default.json
-for m in ${RUNS:-"--config 2" "--config 3" "--config 4" "--model multiscale" "--model source" "--model adaptive" "--model train" "--model train_wct" "--model train_sanet" "--model train_multiscale" "--model train_source" "--model train_adaptive"}; do
+for m in ${RUNS:-"--config 2" "--config 3" "--config 4" "--model forward" "--model multiscale" "--model source" "--model adaptive" "--model train" "--model train_wct" "--model train_sanet" "--model train_multiscale" "--model train_source" "--model train_adaptive"}; do
   f=$O/bench_$(echo $m | tr -d ' -').json
   timeout -k 10 400 python bench.py $m --no-cpu-baseline > $f 2> $f.err || { tail $f.err; exit 1; }
   python -c "import json;d=json.load(open('$f'));r=d['roofline'];print('$m', d['value'], d['ms_per_step'], r['kernel'], r['frac'])"
 done
+timeout -k 10 120 python tools/bench_attn.py --reps 5 > $O/attn.json 2>&1 || { tail $O/attn.json; exit 1; }
+tail -1 $O/attn.json
+timeout -k 10 300 python tools/bench_stylize.py --pairs 128 --batch 32 > $O/stylize.json 2> $O/stylize.err || { tail $O/stylize.err; exit 1; }
+cat $O/stylize.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_adain -o adain -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs > $O/prof_adain.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_wct -o wct -- python3 $R/bench.py --config 2 --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_wct.log 2>&1 || exit 1
