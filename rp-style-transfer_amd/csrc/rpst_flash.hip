@@ -29,6 +29,11 @@ namespace rpst {
 // masked to -inf; queries past HW are not stored. HW % 4 == 0 (16-B rows) and C in
 // {64, 128, 256, 512}; other shapes take the two-GEMM path below.
 constexpr int kFBM = 64, kFBN = 16;
+// timing-only builds (results wrong; tools/build_variants.sh rpst_flash.hip "x:-DRPST_FLDBG=n"):
+// 1 no softmax (P = S), 2 no DMA waits / barriers, 4 no DMA, 8 no O update
+#ifndef RPST_FLDBG
+#define RPST_FLDBG 0
+#endif
 
 __device__ __forceinline__ int attn_xcd_swizzle(int b, int nwg) {
   // bijective: consecutive logical ids land on one XCD (b % 8 = hardware XCD of block b)
@@ -74,6 +79,7 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
   // step's 2 PPW pieces are spread one per MFMA group (scores: NQ / SG = 2 PPW groups) so each
   // issue hides in an MFMA gap instead of stalling a clustered run of them
   auto piece = [&](int jj, int k0g, float* gs, int k0h, float* hs) {
+    if (RPST_FLDBG & 4) return;
     const bool isg = jj < PPW;
     const int j = wave * PPW + (isg ? jj : jj - PPW);
     if (isg) {
@@ -149,6 +155,11 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
   // online softmax over this lane's keys kb * 16 + 4 g + r for query lq: O rescaled to the
   // new running max (lazily), p = exp(S - m)
   auto softmax = [&](int kb, const floatx4& sc) {
+    if (RPST_FLDBG & 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p[r] = sc[r];
+      return;
+    }
     const int kbase = kb * kFBN + 4 * g;
     float sv[4], mx = -INFINITY;
 #pragma unroll
@@ -177,6 +188,7 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
   // groups of UG, the H reads of group u + 1 issued before group u's MFMAs
   constexpr int UG = NMB >= 4 ? 4 : NMB;
   auto update = [&](const float* hs) {
+    if (RPST_FLDBG & 8) return;
     float4 hb[2][UG];
     auto ld = [&](float4 (&h)[UG], int u) {
 #pragma unroll
@@ -219,8 +231,10 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
     // shuffle / exp latency sits behind the update's MFMAs. H lags G by one block: H(kb) is
     // loaded in iteration kb into the buffer of H(kb - 2) and consumed in iteration kb + 1.
     auto step = [&](int kb, const float* gs, const float* hprev, float* gn, float* hcur) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // G(kb), H(kb - 1) have landed
-      __builtin_amdgcn_s_barrier();
+      if (!(RPST_FLDBG & 2)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // G(kb), H(kb - 1) have landed
+        __builtin_amdgcn_s_barrier();
+      }
       const int kg = kb + 1 < nk ? (kb + 1) * kFBN : -1, kh = kb < nk ? kb * kFBN : -1;
       floatx4 sc = {0.f, 0.f, 0.f, 0.f};
       if (kb < nk) sc = scores(kb, gs, [&](int t) { piece(t, kg, gn, kh, hcur); });

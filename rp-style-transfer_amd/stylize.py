@@ -84,6 +84,11 @@ def main(argv=None) -> int:
     ap.add_argument("--png-compress-level", type=int, default=6,
                     help="zlib level of the written PNGs (6 = torchvision save_image's; the "
                          "pixels are identical at every level, 1 encodes ~3x faster)")
+    ap.add_argument("--png-strategy", default="rle", choices=["default", "filtered", "huffman", "rle"],
+                    help="zlib strategy of the written PNGs (rle: ~6x faster than the default "
+                         "match search at level 6, ~1.5 %% larger files, identical pixels)")
+    ap.add_argument("--encode-workers", type=int, default=8,
+                    help="PNG writer threads (decode threads: the config's num_workers)")
     args = ap.parse_args(argv)
     with open(args.config) as f:
         opt = yaml.safe_load(f)
@@ -101,7 +106,8 @@ def main(argv=None) -> int:
 
     with torch.cuda.device(device):
         n = Pipeline(stylize, device, opt["img_size"], opt.get("batch_size", 1),
-                     opt.get("num_workers", 4), png_level=args.png_compress_level).run(
+                     opt.get("num_workers", 4), png_level=args.png_compress_level,
+                     png_strategy=args.png_strategy, encode_workers=args.encode_workers).run(
                          dataset, str(out_dir), log=logger.info)
     logger.info(f"stylised {n} pairs into {out_dir}")
     return 0

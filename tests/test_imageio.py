@@ -75,7 +75,8 @@ def test_stylize_rejects_out_of_scope_networks():
 
 def test_write_png_round_trip(tmp_path):
     """write_png (the pipeline's writer for GPU-filtered scanlines) decodes to the pixels at
-    every zlib level; the scanlines here are Up-filtered on the host like rpst_png_filter_up."""
+    every zlib level and strategy; the scanlines here are Up-filtered on the host like
+    rpst_png_filter_up."""
     from PIL import Image
     from rpst.imageio import write_png
     a = np.random.default_rng(5).integers(0, 256, (21, 34, 3)).astype(np.uint8)
@@ -84,7 +85,8 @@ def test_write_png_round_trip(tmp_path):
     f[:, 0] = 2
     f[0, 1:] = x[0]
     f[1:, 1:] = (x[1:] - x[:-1]) & 255
-    for lvl in (0, 1, 9):
-        p = str(tmp_path / f"w{lvl}.png")
-        write_png(p, f, lvl)
+    for lvl, strat in ((0, "default"), (1, "default"), (9, "default"), (6, "rle"),
+                       (6, "huffman"), (6, "filtered")):
+        p = str(tmp_path / f"w{lvl}{strat}.png")
+        write_png(p, f, lvl, strat)
         np.testing.assert_array_equal(np.asarray(Image.open(p).convert("RGB")), a)

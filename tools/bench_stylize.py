@@ -8,11 +8,12 @@ noise, so zlib sees image-like data) into a scratch directory, then times on one
                   uint8 pixels, ToTensor on the GPU, test(), save_image's pixel path on the
                   GPU, D2H, PNG encode of {cn}-{sn}.png and the 3-up -cat.png on host threads
   decode / encode host rates with the same thread counts, alone (the host-side bound)
-at PNG zlib level 6 (torchvision.save_image's), 1 and 0 (stored): the same pixels, faster
-deflate. The PNG scanline filter runs on the GPU (rpst_png_filter_up), so the host threads
-only decode, deflate and write.
+for three PNG encodings of the same pixels: zlib level 6 with the default strategy
+(torchvision.save_image's), level 6 with Z_RLE (stylize.py's default) and level 0 (stored).
+The PNG scanline filter runs on the GPU (rpst_png_filter_up), so the host threads only
+decode, deflate and write.
 
-    python tools/bench_stylize.py [--pairs 128] [--batch 32] [--workers 4] [--encode-workers 12]
+    python tools/bench_stylize.py [--pairs 512] [--batch 32] [--workers 4] [--encode-workers 12]
 """
 import argparse
 import json
@@ -55,7 +56,7 @@ def up_filter(img):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--pairs", type=int, default=128)
+    ap.add_argument("--pairs", type=int, default=512)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--workers", type=int, default=4, help="decode threads")
@@ -69,7 +70,7 @@ def main():
     try:
         for d in ("content", "style"):
             os.makedirs(os.path.join(root, d))
-        with ThreadPoolExecutor(args.workers) as pool:
+        with ThreadPoolExecutor(args.workers + args.encode_workers) as pool:
             list(pool.map(lambda i: save_png(photo_like(i, args.size),
                                              os.path.join(root, "content", f"im{i:04d}.png")),
                           range(args.pairs)))
@@ -85,7 +86,7 @@ def main():
         # host-side rates alone: decode on --workers threads; deflate + write of the GPU-filtered
         # scanlines (write_png) on --encode-workers threads, for one stylised image and its
         # 3-up -cat image per pair (here: filtered on the host from the decoded photos)
-        levels = (6, 1, 0)
+        encs = {"l6": (6, "default"), "rle": (6, "rle"), "l0": (0, "default")}
         with ThreadPoolExecutor(args.workers) as pool:
             t0 = time.perf_counter()
             imgs = list(pool.map(lambda p: load_image(p, args.size), paths))
@@ -101,15 +102,17 @@ def main():
         out = os.path.join(root, "enc")
         os.makedirs(out)
         with ThreadPoolExecutor(args.encode_workers) as pool:
-            for lvl in levels:
+            for name, (lvl, strat) in encs.items():
                 t0 = time.perf_counter()
-                futs = [pool.submit(write_png, os.path.join(out, f"{i}.png"), single[i % 16], lvl)
-                        for i in range(args.pairs)]
-                futs += [pool.submit(write_png, os.path.join(out, f"{i}c.png"), cat[i % 16], lvl)
-                         for i in range(args.pairs)]
+                futs = [pool.submit(write_png, os.path.join(out, f"{i}.png"), single[i % 16], lvl,
+                                    strat) for i in range(args.pairs)]
+                futs += [pool.submit(write_png, os.path.join(out, f"{i}c.png"), cat[i % 16], lvl,
+                                     strat) for i in range(args.pairs)]
                 for f in futs:
                     f.result()
-                rec[f"encode_pairs_s_level{lvl}"] = round(args.pairs / (time.perf_counter() - t0), 1)
+                rec[f"encode_pairs_s_{name}"] = round(args.pairs / (time.perf_counter() - t0), 1)
+                rec[f"png_bytes_per_pair_{name}"] = (os.path.getsize(os.path.join(out, "0.png")) +
+                                                     os.path.getsize(os.path.join(out, "0c.png")))
         # bare test() on resident tensors
         cfg = {"rp_blocks": 5, "hidden_dim": 16, "content_weight": 1.0, "style_weight": 10.0,
                "resume": False}
@@ -130,32 +133,33 @@ def main():
         rec["test_img_s"] = round(reps * args.batch / (time.perf_counter() - t0), 1)
         del c, s
         # the pipeline, end to end (a warm-up pass over one batch first)
-        for lvl in levels:
-            # the thread split follows the bound: deflate-heavy levels get most threads for
-            # encoding; stored PNGs (level 0) are decode-bound, so the split is even there
-            dw, ew = (args.workers, args.encode_workers) if lvl > 0 else (
+        for name, (lvl, strat) in encs.items():
+            # the thread split follows the bound: the default match search at level 6 gets
+            # most threads for encoding; rle and stored PNGs are decode-bound: an even split
+            dw, ew = (args.workers, args.encode_workers) if name == "l6" else (
                 (args.workers + args.encode_workers) // 2,) * 2
-            rec[f"pipeline_threads_level{lvl}"] = [dw, ew]
+            rec[f"pipeline_threads_{name}"] = [dw, ew]
             pipe = Pipeline(m.test, dev, args.size, args.batch, dw, png_level=lvl,
-                            encode_workers=ew)
+                            encode_workers=ew, png_strategy=strat)
             warm = PairedDataset(root)
             warm.content_names = warm.content_names[:args.batch]
-            pipe.run(warm, os.path.join(root, f"warm{lvl}"))
+            pipe.run(warm, os.path.join(root, f"warm{name}"))
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            n = pipe.run(ds, os.path.join(root, f"out{lvl}"))
+            n = pipe.run(ds, os.path.join(root, f"out{name}"))
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             assert n == args.pairs
-            rec[f"pipeline_img_s_level{lvl}"] = round(n / dt, 1)
-            rec[f"pipeline_host_s_level{lvl}"] = {k: round(v, 3) for k, v in pipe.stats.items()}
-            rec[f"pipeline_wall_s_level{lvl}"] = round(dt, 3)
-        for lvl in levels:
-            rec[f"pipeline_vs_test_level{lvl}"] = round(
-                rec[f"pipeline_img_s_level{lvl}"] / rec["test_img_s"], 3)
-            # host bound: decode and deflate run on their own thread pools
-            rec[f"host_bound_pairs_s_level{lvl}"] = min(rec["decode_pairs_s"],
-                                                        rec[f"encode_pairs_s_level{lvl}"])
+            rec[f"pipeline_img_s_{name}"] = round(n / dt, 1)
+            rec[f"pipeline_host_s_{name}"] = {k: round(v, 3) for k, v in pipe.stats.items()}
+            rec[f"pipeline_wall_s_{name}"] = round(dt, 3)
+            shutil.rmtree(os.path.join(root, f"out{name}"), ignore_errors=True)
+        for name in encs:
+            rec[f"pipeline_vs_test_{name}"] = round(rec[f"pipeline_img_s_{name}"] / rec["test_img_s"], 3)
+            # host bound: decode and deflate run on their own thread pools (rates measured
+            # above with --workers decode / --encode-workers deflate threads)
+            rec[f"host_bound_pairs_s_{name}"] = min(rec["decode_pairs_s"],
+                                                    rec[f"encode_pairs_s_{name}"])
         print(json.dumps(rec), flush=True)
     finally:
         shutil.rmtree(root, ignore_errors=True)

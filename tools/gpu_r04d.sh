@@ -3,6 +3,11 @@
 # then the round-4 PMC traffic + SQ counter tables of configs[1] (tools/prof_pmc.sh)
 set -o pipefail
 O=gpurun_out/r04d; mkdir -p $O
+# every algorithm (direct tile variants, F(2x2), F(4x4)) on the small layers
+for only in 16-\>32 32-\>64 64-\>32 32-\>16; do
+  timeout -k 10 180 python tools/bench_conv.py --layers adain --rounds 2 --only "$only" > $O/algo.log 2>&1 || { tail $O/algo.log; exit 1; }
+  tail -1 $O/algo.log
+done
 for only in 16-\>32 32-\>64 64-\>32 32-\>16; do
   for cs in 1 2; do
     for half in 512 2048 0; do
