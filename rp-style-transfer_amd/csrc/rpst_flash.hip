@@ -43,6 +43,26 @@ __device__ __forceinline__ int attn_xcd_swizzle(int b, int nwg) {
 
 typedef __attribute__((address_space(3))) void* attn_lds_ptr_t;
 
+// max over the four lanes l, l ^ 16, l ^ 32, l ^ 48 (one query's four key groups): the gfx950
+// row-swap permutes (VALU, no LDS round trip as ds_bpermute)
+__device__ __forceinline__ float rows4_max(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto a = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  v = fmaxf(__builtin_bit_cast(float, a[0]), __builtin_bit_cast(float, a[1]));
+  const unsigned w = __builtin_bit_cast(unsigned, v);
+  const auto b = __builtin_amdgcn_permlane16_swap(w, w, false, false);
+  return fmaxf(__builtin_bit_cast(float, b[0]), __builtin_bit_cast(float, b[1]));
+}
+__device__ __forceinline__ float rows4_sum(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto a = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  v = __builtin_bit_cast(float, a[0]) + __builtin_bit_cast(float, a[1]);
+  const unsigned w = __builtin_bit_cast(unsigned, v);
+  const auto b = __builtin_amdgcn_permlane16_swap(w, w, false, false);
+  return __builtin_bit_cast(float, b[0]) + __builtin_bit_cast(float, b[1]);
+}
+constexpr float kLog2e = 1.4426950408889634f;
+
 template <int C, bool PIPE>
 __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __restrict__ F,
                                                              const float* __restrict__ G,
@@ -167,14 +187,16 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
       sv[r] = kbase + r < HW ? sc[r] : -INFINITY;
       mx = fmaxf(mx, sv[r]);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = m_run == -INFINITY ? 0.f : expf(m_run - m_new);
+    const float m_new = fmaxf(m_run, rows4_max(mx));
+    // exp(x - m) as v_exp_f32 (base 2) of fma(x, log2 e, -m log2 e): one rounding before
+    // the hardware exp instead of expf's range-reduced software sequence; masked keys
+    // (-inf) give 0
+    const float mL = m_new * kLog2e;
+    const float alpha = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(fmaf(m_run, kLog2e, -mL));
     float ps = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      p[r] = expf(sv[r] - m_new);
+      p[r] = __builtin_amdgcn_exp2f(fmaf(sv[r], kLog2e, -mL));
       ps += p[r];
     }
     l_run = fmaf(l_run, alpha, ps);
@@ -248,8 +270,7 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
     }
   }
   // the row sum over the four lane groups holding a query's keys; O / l
-  l_run += __shfl_xor(l_run, 16, 64);
-  l_run += __shfl_xor(l_run, 32, 64);
+  l_run = rows4_sum(l_run);
   if (q < HW) {
     const float inv = 1.f / l_run;
     float* Ob = O + b * plane + q;

@@ -53,6 +53,12 @@ constexpr int kW4CK = 8;                   // input channels per chunk
 #ifndef RPST_W4_HP
 #define RPST_W4_HP 2
 #endif
+// the last co tile of a block exchanges its output-transform partials through every ring
+// stage in turn, without the barrier that guards the reuse of one stage between passes:
+// RPST_W4_WIDEEPI=0 restores the one-stage exchange everywhere (A/B)
+#ifndef RPST_W4_WIDEEPI
+#define RPST_W4_WIDEEPI 1
+#endif
 #ifndef RPST_W4_ORDER  // spatial block order (w4_tile)
 #define RPST_W4_ORDER 0
 #endif
@@ -442,12 +448,15 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
   auto issue_w = [&](int g, bool live, float* st) {
     if (!(DBG & 2)) {
       const int wv = launder(wave);
+      live = __builtin_amdgcn_readfirstlane((int)live) != 0;  // selects the LDS target (M0)
       const int sw = live ? (ct0 * K4 + g) * kW4SW * 4 + wv * 1024 : 0;  // piece wv's bytes
 #pragma unroll
       for (int i = 0; i < Geo::WPI; ++i) {
         const bool real = wv + NW * i < 18;
+        // dead pieces (past the last step) land in the dummy target: the last co tile's
+        // epilogue reuses every stage
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rsrc_or_zero(w_img, wbytes, live && real), (lds_ptr_t)(real ? st + Geo::SPATCH + wv * 256 + NW * 256 * i : dummy), 16, lane * 16,
+            rsrc_or_zero(w_img, wbytes, live && real), (lds_ptr_t)(real && live ? st + Geo::SPATCH + wv * 256 + NW * 256 * i : dummy), 16, lane * 16,
             real ? sw + NW * 1024 * i : 0, 0, 0);
       }
     }
@@ -456,6 +465,7 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
     {
       if (DBG & 1) return;
       const int wv = launder(wave);
+      live = __builtin_amdgcn_readfirstlane((int)live) != 0;  // selects the LDS target (M0)
       const int c = 4 * ks + wv / NH;
       const bool ok = live && c < a.Cin;
       const auto r = rsrc_or_zero(in_img, oob, ok);
@@ -466,12 +476,12 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
         for (int i = 0; i < kWide; ++i) {
           const int p = kWide * (wv % NH) + i;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              r, (lds_ptr_t)(p < Geo::DMA4 ? xs + 256 * p : dummy), 16, (int)poff[i], so, 0, 0);
+              r, (lds_ptr_t)(live && p < Geo::DMA4 ? xs + 256 * p : dummy), 16, (int)poff[i], so, 0, 0);
         }
       } else {
 #pragma unroll
         for (int i = 0; i < kSlow; ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(xs + 64 * (kSlow * (wv % NH) + i)),
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(live ? xs + 64 * (kSlow * (wv % NH) + i) : dummy),
                                                    4, (int)poff[i], so, 0, 0);
       }
     }
@@ -804,10 +814,16 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
   };
   // PH = ph: the half this wave finishes is channel half PH; it hands the other half's
   // partial tile to its partner wave
-  auto epilogue_ph = [&](auto PHc, int ct, float* xs) {
+  // last (the block's last co tile; RPST_W4_WIDEEPI): no live DMA is left (dead pieces land
+  // in `dummy`), so pass r goes through ring stage r % S and no pass waits for the previous
+  // one's reads before writing (5 barriers per epilogue instead of 8)
+  auto epilogue_ph = [&](auto PHc, int ct, float* xs, bool last) {
     constexpr int PH = decltype(PHc)::value;
     lds_barrier();  // every wave is done reading the stage
-    float* xb = xs + wr * 2048;
+    auto xbuf = [&](int r) -> float* {
+      float* st = !last ? xs : (r % S == 0 ? smem0 : (r % S == 1 ? smem1 : (r % S == 2 ? smem2 : smem3)));
+      return st + wr * 2048;
+    };
     const EpiCtx e = epi_ctx();
     const int co0 = ct * kW4BM + 16 * PH + 4 * k;
     // PH = 0 adds the biases of both channel halves (its own and the partner's partial),
@@ -826,6 +842,7 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+      float* xb = xbuf(r);
       float own[16];
       {
         float give[16];
@@ -847,13 +864,14 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
         own[4 * g4 + 3] += o4.w;
       }
       finish(e, co0 + r, own);
-      if (r < 3) lds_barrier();  // the next pass overwrites the exchange region
+      if (r < 3 && !last) lds_barrier();  // the next pass overwrites the exchange region
     }
   };
-  auto epilogue = [&](int ct, float* xs) {
-    if (ph) epilogue_ph(std::integral_constant<int, 1>{}, ct, xs);
-    else epilogue_ph(std::integral_constant<int, 0>{}, ct, xs);
+  auto epilogue = [&](int ct, float* xs, bool last) {
+    if (ph) epilogue_ph(std::integral_constant<int, 1>{}, ct, xs, last);
+    else epilogue_ph(std::integral_constant<int, 0>{}, ct, xs, last);
   };
+
 
   // ---- pipeline: ring of 4 stages, K step g in stage g % 4, issued 3 steps ahead --------
   // Every step issues one group of `per` pieces per wave, also past the last step (those
@@ -899,7 +917,9 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
     compute(cur, d, hw, hp);
     ks3 = ks3 + 1 == K4 ? 0 : ks3 + 1;
     if (ks == K4 - 1) {
-      if (!(DBG & 32)) epilogue(ct, cur);
+      if (!(DBG & 32)) {
+        epilogue(ct, cur, RPST_W4_WIDEEPI && ct == ct0 + nct - 1);
+      }
 #pragma unroll
       for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     }

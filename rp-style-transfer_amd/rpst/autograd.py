@@ -621,7 +621,12 @@ class _SAModelStep(torch.autograd.Function):
     @staticmethod
     def _forward(ctx, content, style, model, cfg, *params):
         n = content.shape[0]
-        with ops.precise_convs(on=False):  # frozen VGG of the inputs: constants of the step
+        # frozen VGG of the inputs: constants of the step, on F(4x4) -- except for the
+        # AdaptiveSAModel, whose 'aea' clamp (a slope-50 sigmoid of a peaked softmax)
+        # amplifies their ~1e-5 difference past its loss bar (profiles/r04f: style loss
+        # 2.85e-4 against 2.73e-4)
+        adaptive = _is_adaptive(model.transform.sanet4_1)
+        with ops.precise_convs(on=adaptive):
             feats = model.encode_with_intermediate(torch.cat([style, content], dim=0))
         sf = [f[:n].contiguous() for f in feats]
         cf = [f[n:].contiguous() for f in feats]

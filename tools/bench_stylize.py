@@ -136,7 +136,7 @@ def main():
         for name, (lvl, strat) in encs.items():
             # the thread split follows the bound: the default match search at level 6 gets
             # most threads for encoding; rle and stored PNGs are decode-bound: an even split
-            dw, ew = (args.workers, args.encode_workers) if name == "l6" else (
+            dw, ew = (args.workers, args.encode_workers) if name != "l0" else (
                 (args.workers + args.encode_workers) // 2,) * 2
             rec[f"pipeline_threads_{name}"] = [dw, ew]
             pipe = Pipeline(m.test, dev, args.size, args.batch, dw, png_level=lvl,

@@ -18,3 +18,7 @@ for only in 16-\>32 32-\>64 64-\>32 32-\>16; do
 done
 SKIP_TESTS=1 bash tools/prof_pmc.sh r04d_pmc > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
 tail -25 $O/prof.log
+# where the F(4x4) time goes per layer: timing-only builds (RPST_W4DBG: 8 no input transform,
+# 16 no barriers, 32 no epilogue, 3 no DMA, 48 neither barriers nor epilogue)
+LIBS="w0 w8 w16 w32 w3 w48" bash tools/ab_libs.sh r04d_attr > $O/attr.log 2>&1 || { tail $O/attr.log; exit 1; }
+cat $O/attr.log
