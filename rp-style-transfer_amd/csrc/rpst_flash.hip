@@ -44,22 +44,38 @@ __device__ __forceinline__ int attn_xcd_swizzle(int b, int nwg) {
 typedef __attribute__((address_space(3))) void* attn_lds_ptr_t;
 
 // max over the four lanes l, l ^ 16, l ^ 32, l ^ 48 (one query's four key groups): the gfx950
-// row-swap permutes (VALU, no LDS round trip as ds_bpermute)
-__device__ __forceinline__ float rows4_max(float v) {
+// row-swap permutes (VALU, no LDS round trip as ds_bpermute). A swap of a register with a
+// copy of itself leaves (lo, lo) in one and (hi, hi) in the other. The two results are made
+// opaque: this compiler folds a combination of them into the first one (max(a, b) -> a)
+__device__ __forceinline__ void swap_halves(float v, int rows, float& a, float& b) {
   const unsigned u = __builtin_bit_cast(unsigned, v);
-  const auto a = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  v = fmaxf(__builtin_bit_cast(float, a[0]), __builtin_bit_cast(float, a[1]));
-  const unsigned w = __builtin_bit_cast(unsigned, v);
-  const auto b = __builtin_amdgcn_permlane16_swap(w, w, false, false);
-  return fmaxf(__builtin_bit_cast(float, b[0]), __builtin_bit_cast(float, b[1]));
+  unsigned x, y;
+  if (rows == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    x = r[0];
+    y = r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    x = r[0];
+    y = r[1];
+  }
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+v"(x), "+v"(y));
+#endif
+  a = __builtin_bit_cast(float, x);
+  b = __builtin_bit_cast(float, y);
+}
+__device__ __forceinline__ float rows4_max(float v) {
+  float a, b;
+  swap_halves(v, 32, a, b);
+  swap_halves(fmaxf(a, b), 16, a, b);
+  return fmaxf(a, b);
 }
 __device__ __forceinline__ float rows4_sum(float v) {
-  const unsigned u = __builtin_bit_cast(unsigned, v);
-  const auto a = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  v = __builtin_bit_cast(float, a[0]) + __builtin_bit_cast(float, a[1]);
-  const unsigned w = __builtin_bit_cast(unsigned, v);
-  const auto b = __builtin_amdgcn_permlane16_swap(w, w, false, false);
-  return __builtin_bit_cast(float, b[0]) + __builtin_bit_cast(float, b[1]);
+  float a, b;
+  swap_halves(v, 32, a, b);
+  swap_halves(a + b, 16, a, b);
+  return a + b;
 }
 constexpr float kLog2e = 1.4426950408889634f;
 
@@ -192,7 +208,10 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
     // the hardware exp instead of expf's range-reduced software sequence; masked keys
     // (-inf) give 0
     const float mL = m_new * kLog2e;
-    const float alpha = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(fmaf(m_run, kLog2e, -mL));
+    // (exactly 1 while the max stands: fma(m, log2 e, -m log2 e) is the product's rounding
+    // residual, not 0)
+    const float alpha = m_run == m_new ? 1.f
+                        : (m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(fmaf(m_run, kLog2e, -mL)));
     float ps = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {

@@ -10,7 +10,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -1 $O/tests_flash.log
 timeout -k 10 120 python tools/bench_attn.py --reps 5 > $O/attn.json 2>&1 || { tail $O/attn.json; exit 1; }
 echo "attn $(tail -1 $O/attn.json)"
-LIBS="we0 we1" bash tools/ab_libs.sh r04g_we > $O/we.log 2>&1 || { tail $O/we.log; exit 1; }
+LIBS="we0 pk0 pk1" bash tools/ab_libs.sh r04g_we > $O/we.log 2>&1 || { tail $O/we.log; exit 1; }
 cat $O/we.log
 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_train.py > $O/tests_train.log 2>&1 || { tail -40 $O/tests_train.log; exit 1; }
 tail -1 $O/tests_train.log
