@@ -53,16 +53,6 @@ constexpr int kW4CK = 8;                   // input channels per chunk
 #ifndef RPST_W4_HP
 #define RPST_W4_HP 2
 #endif
-// the last co tile of a block exchanges its output-transform partials through every ring
-// stage in turn, without the barrier that guards the reuse of one stage between passes:
-// RPST_W4_WIDEEPI=0 restores the one-stage exchange everywhere (A/B)
-#ifndef RPST_W4_WIDEEPI
-#define RPST_W4_WIDEEPI 1
-#endif
-// input transform on packed fp32 (RPST_W4_PACKED=0: the scalar form, A/B)
-#ifndef RPST_W4_PACKED
-#define RPST_W4_PACKED 1
-#endif
 #ifndef RPST_W4_ORDER  // spatial block order (w4_tile)
 #define RPST_W4_ORDER 0
 #endif
@@ -270,39 +260,6 @@ __device__ __forceinline__ void bt6(float& d0, float& d1, float& d2, float& d3, 
   d3 = fmaf(2.f, E, C);
   d4 = fmaf(-2.f, E, C);
   d5 = t5;
-}
-
-typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-// bt6 on a row held as column pairs x = ((x0, x1), (x2, x3), (x4, x5)), packed: (o0, o5),
-// (A, C) = (x4 - 4 x2, x4 - x2), (B, E) = (x3 - 4 x1, x3 - x1) from broadcast halves, then
-// (o1, o3) = (A + B, C + 2 E) and (o2, o4) = (A - B, C - 2 E): six v_pk_fma_f32 for the
-// twelve operations of bt6, each rounding as there
-// The non-inline constant pairs (-5, -5), (-4, -1), (1, 2), (-1, -2) come in VGPRs (kc),
-// pinned once per kernel: as SGPR pairs they are rematerialised every step (the scalar
-// file is full)
-struct PkC {
-  f2 m5, m4m1, p12, m1m2;
-};
-__device__ __forceinline__ PkC pk_consts() {
-  PkC c{f2{-5.f, -5.f}, f2{-4.f, -1.f}, f2{1.f, 2.f}, f2{-1.f, -2.f}};
-#if __HIP_DEVICE_COMPILE__
-  asm volatile("" : "+v"(c.m5), "+v"(c.m4m1), "+v"(c.p12), "+v"(c.m1m2));
-#endif
-  return c;
-}
-__device__ __forceinline__ void bt6_pk(const f2 (&x)[3], float (&o)[6], const PkC& kc) {
-  const f2 o05 = pfma(f2{4.f, 4.f}, x[0], pfma(kc.m5, x[1], x[2]));
-  const f2 AC = pfma(kc.m4m1, x[1].xx, x[2].xx);
-  const f2 BE = pfma(kc.m4m1, x[0].yy, x[1].yy);
-  const f2 o13 = pfma(kc.p12, BE, AC);
-  const f2 o24 = pfma(kc.m1m2, BE, AC);
-  o[0] = o05.x;
-  o[5] = o05.y;
-  o[1] = o13.x;
-  o[3] = o13.y;
-  o[2] = o24.x;
-  o[4] = o24.y;
 }
 
 // A^T applied to one 6-vector -> 4 values
@@ -558,7 +515,6 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
   };
 
 
-  [[maybe_unused]] const PkC kc = kAff ? PkC{} : pk_consts();
   // one K step of 4 channels from a stage: 72 VALU of input transform + 36 MFMAs
   // hw / hp: called after MFMA pair kHW / kHP (RPST_W4VAR placement experiments)
   // input rows ph .. ph + 4 of this lane's 6x6 window of one step
@@ -586,69 +542,33 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
       for (int q = 0; q < 3; ++q)
         w4[q] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
                            : *reinterpret_cast<const float4*>(wq + q * 256);
-      // rows 3ph..3ph+2 of B^T d (d[r] = input row ph + r), then B along each row, on
-      // packed fp32 (v_pk_fma_f32 / v_pk_add_f32: two values per VALU issue, which the
-      // MFMA stream of the SIMD otherwise waits for): the column pass on column pairs, the
-      // row pass (bt6) with op_sel-broadcast operands (bt6_pk) -- the same roundings as the
-      // scalar form, so the results are bit-identical
+      // rows 3ph..3ph+2 of B^T d (d[r] = input row ph + r), then B along each row
       float t[3][6];
       if (DBG & 8) {
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
           for (int c = 0; c < 6; ++c) t[i][c] = d[i][c];
-      } else if constexpr (kAff || !RPST_W4_PACKED) {
-        // the in-loader AdaIN variant keeps the scalar form: its VGPR file is full (the
-        // packed form spills there)
-        if (ph == 0) {
+      } else if (ph == 0) {
 #pragma unroll
-          for (int c = 0; c < 6; ++c) {
-            const float A = fmaf(-4.f, d[2][c], d[4][c]), B = fmaf(-4.f, d[1][c], d[3][c]);
-            t[0][c] = fmaf(4.f, d[0][c], fmaf(-5.f, d[2][c], d[4][c]));
-            t[1][c] = A + B;
-            t[2][c] = A - B;
-          }
-        } else {
-#pragma unroll
-          for (int c = 0; c < 6; ++c) {
-            const float C = d[3][c] - d[1][c], E = d[2][c] - d[0][c];
-            t[0][c] = fmaf(2.f, E, C);
-            t[1][c] = fmaf(-2.f, E, C);
-            t[2][c] = fmaf(4.f, d[0][c], fmaf(-5.f, d[2][c], d[4][c]));
-          }
+        for (int c = 0; c < 6; ++c) {
+          const float A = fmaf(-4.f, d[2][c], d[4][c]), B = fmaf(-4.f, d[1][c], d[3][c]);
+          t[0][c] = fmaf(4.f, d[0][c], fmaf(-5.f, d[2][c], d[4][c]));
+          t[1][c] = A + B;
+          t[2][c] = A - B;
         }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) bt6(t[i][0], t[i][1], t[i][2], t[i][3], t[i][4], t[i][5]);
       } else {
-        f2 tp[3][3];
-        auto col_pair = [&](int cp, f2 (&D)[5]) {
 #pragma unroll
-          for (int r = 0; r < 5; ++r) D[r] = f2{d[r][2 * cp], d[r][2 * cp + 1]};
-        };
-        if (ph == 0) {
-#pragma unroll
-          for (int cp = 0; cp < 3; ++cp) {
-            f2 D[5];
-            col_pair(cp, D);
-            const f2 A = pfma(f2{-4.f, -4.f}, D[2], D[4]), B = pfma(f2{-4.f, -4.f}, D[1], D[3]);
-            tp[0][cp] = pfma(f2{4.f, 4.f}, D[0], pfma(kc.m5, D[2], D[4]));
-            tp[1][cp] = A + B;
-            tp[2][cp] = A - B;
-          }
-        } else {
-#pragma unroll
-          for (int cp = 0; cp < 3; ++cp) {
-            f2 D[5];
-            col_pair(cp, D);
-            const f2 C = D[3] - D[1], E = D[2] - D[0];
-            tp[0][cp] = pfma(f2{2.f, 2.f}, E, C);
-            tp[1][cp] = pfma(f2{-2.f, -2.f}, E, C);
-            tp[2][cp] = pfma(f2{4.f, 4.f}, D[0], pfma(kc.m5, D[2], D[4]));
-          }
+        for (int c = 0; c < 6; ++c) {
+          const float C = d[3][c] - d[1][c], E = d[2][c] - d[0][c];
+          t[0][c] = fmaf(2.f, E, C);
+          t[1][c] = fmaf(-2.f, E, C);
+          t[2][c] = fmaf(4.f, d[0][c], fmaf(-5.f, d[2][c], d[4][c]));
         }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) bt6_pk(tp[i], t[i], kc);
       }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (!(DBG & 8)) bt6(t[i][0], t[i][1], t[i][2], t[i][3], t[i][4], t[i][5]);
 #pragma unroll
       for (int q = 0; q < 9; ++q) {
         if (q + 3 < 9)
@@ -884,18 +804,10 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
   };
   // PH = ph: the half this wave finishes is channel half PH; it hands the other half's
   // partial tile to its partner wave
-  // last (the block's last co tile; RPST_W4_WIDEEPI): no live DMA is left, and the dead
-  // pieces past the last step (zeros into the other stages) have landed after one
-  // vmcnt(0), so pass r goes through ring stage r % S and no pass waits for the previous
-  // one's reads before writing (5 barriers per epilogue instead of 8)
-  auto epilogue_ph = [&](auto PHc, int ct, float* xs, bool last) {
+  auto epilogue_ph = [&](auto PHc, int ct, float* xs) {
     constexpr int PH = decltype(PHc)::value;
-    if (last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();  // every wave is done reading the stage (and its dead DMA has landed)
-    auto xbuf = [&](int r) -> float* {
-      float* st = !last ? xs : (r % S == 0 ? smem0 : (r % S == 1 ? smem1 : (r % S == 2 ? smem2 : smem3)));
-      return st + wr * 2048;
-    };
+    lds_barrier();  // every wave is done reading the stage
+    float* xb = xs + wr * 2048;
     const EpiCtx e = epi_ctx();
     const int co0 = ct * kW4BM + 16 * PH + 4 * k;
     // PH = 0 adds the biases of both channel halves (its own and the partner's partial),
@@ -914,7 +826,6 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float* xb = xbuf(r);
       float own[16];
       {
         float give[16];
@@ -936,14 +847,13 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
         own[4 * g4 + 3] += o4.w;
       }
       finish(e, co0 + r, own);
-      if (r < 3 && !last) lds_barrier();  // the next pass overwrites the exchange region
+      if (r < 3) lds_barrier();  // the next pass overwrites the exchange region
     }
   };
-  auto epilogue = [&](int ct, float* xs, bool last) {
-    if (ph) epilogue_ph(std::integral_constant<int, 1>{}, ct, xs, last);
-    else epilogue_ph(std::integral_constant<int, 0>{}, ct, xs, last);
+  auto epilogue = [&](int ct, float* xs) {
+    if (ph) epilogue_ph(std::integral_constant<int, 1>{}, ct, xs);
+    else epilogue_ph(std::integral_constant<int, 0>{}, ct, xs);
   };
-
 
   // ---- pipeline: ring of 4 stages, K step g in stage g % 4, issued 3 steps ahead --------
   // Every step issues one group of `per` pieces per wave, also past the last step (those
@@ -989,9 +899,7 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
     compute(cur, d, hw, hp);
     ks3 = ks3 + 1 == K4 ? 0 : ks3 + 1;
     if (ks == K4 - 1) {
-      if (!(DBG & 32)) {
-        epilogue(ct, cur, RPST_W4_WIDEEPI && ct == ct0 + nct - 1);
-      }
+      if (!(DBG & 32)) epilogue(ct, cur);
 #pragma unroll
       for (int x = 0; x < 18; ++x) acc[x][0] = acc[x][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     }

@@ -621,13 +621,11 @@ class _SAModelStep(torch.autograd.Function):
     @staticmethod
     def _forward(ctx, content, style, model, cfg, *params):
         n = content.shape[0]
-        # frozen VGG of the inputs: constants of the step, on F(4x4) -- except for the
-        # AdaptiveSAModel, whose 'aea' clamp (a slope-50 sigmoid of a peaked softmax)
-        # amplifies their ~1e-5 difference past its loss bar (profiles/r04f: style loss
-        # 2.85e-4 against 2.73e-4)
-        adaptive = _is_adaptive(model.transform.sanet4_1)
-        with ops.precise_convs(on=adaptive):
-            feats = model.encode_with_intermediate(torch.cat([style, content], dim=0))
+        # frozen VGG of the inputs: constants of the step, but they feed the differentiated
+        # transforms, so they stay precise: on F(4x4) the AdaptiveSAModel's style loss moves
+        # 2.85e-4 against its 2.73e-4 bar (profiles/r04f) and SAModel's sanet5_1.h.weight
+        # gradient 1.06e-4 against 1e-4 (profiles/r04g)
+        feats = model.encode_with_intermediate(torch.cat([style, content], dim=0))
         sf = [f[:n].contiguous() for f in feats]
         cf = [f[n:].contiguous() for f in feats]
         dec_steps = plan.compile_layers(model.decoder.children())

@@ -194,7 +194,10 @@ def _conv_name(ksize, cin, cout, hs, ws, n, in_op):
 # 8.0e-5 of its bar), but the CPU-autograd check at hidden 8, 40x56 does not (AdaIN-RP
 # rp_shared_encoder.0.weight 3.3e-3, profiles/r04e), so F(4x4) is kept to the step's
 # constant branches (precise_convs(on=False)): the VGG loss targets, WCT-RP's detached
-# encoder + WCT, the frozen VGG features of SourceNet / SAModel. TRAIN_F4 opts a whole step in.
+# encoder + WCT, the frozen VGG features of SourceNet. SAModel's frozen VGG features stay
+# precise: they feed the differentiated attention transforms, and on F(4x4) a
+# sanet5_1.h.weight gradient moves 1.06e-4 against its 1e-4 bar (profiles/r04g). TRAIN_F4
+# opts a whole step in.
 TRAIN_F4 = {"adain": False, "multiscale": False, "wct": False, "sanet": False, "source": False}
 
 
