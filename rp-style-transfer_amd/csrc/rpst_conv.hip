@@ -378,7 +378,7 @@ static int pad_cout(int Cout) {
 static int ck_of(int ksize) { return ksize == 3 ? ConvK<3>::CK : ConvK<1>::CK; }
 
 // ---- narrow 3x3 layers on the VALU ------------------------------------------------------
-// Cout <= 4 with Cin <= 32, or Cout <= 16 with Cin <= 4 (narrow_shape; the RP stacks'
+// Cout <= 4 with Cin <= 64, or Cout <= 16 with Cin <= 4 (narrow_shape; the RP stacks'
 // 3->16 input and 16->3 output convs, base.py:363-396 encoder / decoder ends, and the
 // MultiScale decoder's last block 32->3, whose loader forms stylized + AdaIN(c) per element:
 // INOP = RPST_IN_ADD_ADAIN, adain_rp.py:301): an MFMA tile
@@ -389,7 +389,7 @@ static int ck_of(int ksize) { return ksize == 3 ? ConvK<3>::CK : ConvK<1>::CK; }
 // whole block. Same epilogue as the direct kernel: bias, activation, residual. Images go
 // on grid.z: batches above 65535 images (or 65535 row tiles) take the MFMA direct path.
 constexpr int kNrTW = 64, kNrPW = kNrTW + 2;
-constexpr int kNrMaxCin = 32, kNrMaxCo = 16, kNrWl = 128 * 9;  // weight floats in LDS
+constexpr int kNrMaxCin = 64, kNrMaxCo = 16, kNrWl = 256 * 9;  // weight floats in LDS
 
 static bool narrow_shape(int Cin, int Cout) {
   return (Cout <= 4 && Cin <= kNrMaxCin) || (Cout <= kNrMaxCo && Cin <= 4);
@@ -403,7 +403,7 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
   constexpr bool kSkip = INOP == RPST_IN_ADD_ADAIN;
   constexpr int CK = ConvK<3>::CK, kNrTH = 4 * RPT, kNrPS = (kNrTH + 2) * kNrPW;
   __shared__ float patch[kNrPS];
-  __shared__ __attribute__((aligned(8))) float wl[kNrWl];  // Cin * 9 * CO <= 1152 (narrow_shape)
+  __shared__ __attribute__((aligned(8))) float wl[kNrWl];  // Cin * 9 * CO <= 2304 (narrow_shape)
   const int x0 = blockIdx.x * kNrTW, y0 = blockIdx.y * kNrTH, n = blockIdx.z;
   const int tid = threadIdx.x, col = tid & 63, rg = tid >> 6;  // output rows RPT rg ..
   // direct-packed weights [ci / CK][tap][ci % CK][Cout_pad] (zero beyond Cout)

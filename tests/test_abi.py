@@ -129,7 +129,8 @@ def test_conv_algorithm_choice_is_host_only(monkeypatch):
     assert lib.rpst_conv2d_algorithm(64, 3, 512, 512, 3, 0) == W4       # 3-channel input
     assert lib.rpst_conv2d_algorithm(64, 8, 512, 512, 3, 0) == D        # 8-channel input
     assert lib.rpst_conv2d_algorithm(3, 32, 512, 512, 3, 5) == NR       # skip-AdaIN 32->3
-    assert lib.rpst_conv2d_algorithm(3, 64, 512, 512, 3, 0) != NR       # Cin > 32
+    assert lib.rpst_conv2d_algorithm(3, 64, 512, 512, 3, 0) == NR       # VGG decoder 64->3
+    assert lib.rpst_conv2d_algorithm(3, 128, 512, 512, 3, 0) != NR      # Cin > 64
     assert lib.rpst_conv2d_algorithm(16, 3, 512, 512, 3, 0) == NR      # RP 3->16
     assert lib.rpst_conv2d_algorithm(3, 16, 512, 512, 3, 0) == NR      # RP 16->3
     assert lib.rpst_conv2d_algorithm(8, 8, 512, 512, 3, 0) == D        # not narrow_shape

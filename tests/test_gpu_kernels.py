@@ -324,7 +324,8 @@ NARROW_CASES = [  # (N, Cin, Hs, Ws, Cout, pad, relu, residual)
     (1, 16, 33, 64, 3, 0, True, True),     # 16->3 with the residual epilogue
     (2, 3, 21, 130, 16, 0, True, True),    # 3->16 with the residual epilogue
     (1, 4, 9, 66, 4, 1, True, False),      # Cout <= 4 instantiation, Cin 4
-    (2, 32, 19, 130, 3, 1, False, False),  # Cin 32 (the largest narrow input), reflect
+    (2, 32, 19, 130, 3, 1, False, False),  # Cin 32, reflect
+    (2, 64, 21, 70, 3, 1, False, False),   # Cin 64 (the largest narrow input: VGG decoder end)
 ]
 
 

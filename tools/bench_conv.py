@@ -34,6 +34,7 @@ VGG = [
     (64, 128, 256, 256, 128, 3, 1, 0), (64, 128, 256, 256, 256, 3, 1, 1),
     (64, 256, 128, 128, 256, 3, 1, 0), (64, 256, 128, 128, 512, 3, 1, 1),
     (64, 512, 64, 64, 512, 3, 1, 0), (32, 512, 64, 64, 512, 1, 0, 0),
+    (32, 64, 512, 512, 3, 3, 1, 0),  # the VGG decoders' last conv (SAModel, SourceNet)
 ]
 VARIANTS = {128: [0, 1, 2, 3, 4], 64: [0, 1, 2], 32: [0, 1, 2]}
 
