@@ -120,6 +120,20 @@ def main():
                 rec[f"encode_pairs_s_{name}"] = round(args.pairs / (time.perf_counter() - t0), 1)
                 rec[f"png_bytes_per_pair_{name}"] = (os.path.getsize(os.path.join(out, "0.png")) +
                                                      os.path.getsize(os.path.join(out, "0c.png")))
+        # the GPU side of the decode: PNG reconstruction of one batch (2 x batch images)
+        from rpst.imageio import png_unfilter
+        nb = min(2 * args.batch, len(paths))
+        rows = torch.from_numpy(np.stack([read_png_filtered(p, args.size) for p in paths[:nb]]))
+        rows = rows.to(dev)
+        png_unfilter(rows)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            png_unfilter(rows)
+        e1.record()
+        torch.cuda.synchronize()
+        rec["unfilter_ms_per_batch"] = round(e0.elapsed_time(e1) / 3, 3)
+        del rows
         # bare test() on resident tensors
         cfg = {"rp_blocks": 5, "hidden_dim": 16, "content_weight": 1.0, "style_weight": 10.0,
                "resume": False}
