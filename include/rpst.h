@@ -281,13 +281,6 @@ int rpst_f32nchw_to_u8_tile(const float* in, uint8_t* canvas, int N, int H, int 
 int rpst_png_filter_up(const uint8_t* in, uint8_t* out, int N, int H, int rowbytes,
                        rpst_stream_t stream);
 
-/* PNG reconstruction (filter types 0-4, 8-bit RGB) of N images: in (N, H, 1 + 3 W) = the
- * inflated IDAT scanlines of each image (4-byte aligned; the host only inflates,
- * rpst.imageio.read_png_filtered), out (N, H, 3 W) = the pixels HWC, the uint8 input of
- * transforms.ToTensor in the test driver's loader (test.py:49-54). Bit-exact with any PNG
- * decoder. Type bytes > 4 reconstruct as None (the host validates them first). */
-int rpst_png_unfilter(const uint8_t* in, uint8_t* out, int N, int H, int W, rpst_stream_t stream);
-
 /* ---- f2: training backward  AdaINRPNet.forward adain_rp.py:110-138 +
  * total_loss.backward() train.py:186-189. Conv dgrad runs on rpst_conv2d with weights from
  * rpst_conv_weight_flip (packed by rpst_conv2d_pack); reflect-padded convs then add

@@ -625,7 +625,8 @@ static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
   // measured (profiles/r01_bench_conv_wino4.log): F(4x4) wins every layer with >= 16 input
   // channels it supports, the 16-wide 32->16 decoder layer included; the narrow shapes
   // (3->16 / 16->3 of the RP stacks, <= 4-channel outputs) run on the VALU kernel (3->16
-  // 0.44 / 16->3 0.16 ms vs 0.57 / 0.64 on MFMA tiles); the wider 3-channel first convs
+  // 0.44 / 16->3 0.16 ms vs 0.57 / 0.64 on MFMA tiles; the VGG decoders' 64->3 reflect at
+  // 512^2, N = 32: 0.63 ms vs 1.05 on F(4x4), profiles/r04/narrow64.log); the wider 3-channel first convs
   // (VGG 3->64, MultiScale 3->32) run on F(4x4): 3->64 reflect at 512^2, N = 64: 1.25 ms vs
   // 1.59 direct and 2.49 on the VALU kernel (tools/bench_conv.py); other inputs below 16
   // channels, and precise mode, stay direct

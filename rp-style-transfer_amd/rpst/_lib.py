@@ -86,7 +86,6 @@ SIGNATURES = {
     "rpst_u8hwc_to_f32nchw": (_I, [_P, _P, _I, _I, _I, _P]),
     "rpst_f32nchw_to_u8_tile": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "rpst_png_filter_up": (_I, [_P, _P, _I, _I, _I, _P]),
-    "rpst_png_unfilter": (_I, [_P, _P, _I, _I, _I, _P]),
     "rpst_cosine_affinity_workspace_size": (_SZ, [_I, _I, _I]),
     "rpst_cosine_affinity": (_I, [_P, _P, _P, _I, _I, _I, _P, _SZ, _P]),
     "rpst_aea_clamp_workspace_size": (_SZ, [_I, _I, _I]),

@@ -6,10 +6,8 @@ test driver does around `network.test()` (test.py:117-150, datasets/base.py:51-1
              without 'in'>, plus labelme_segmentation mask paths)
   decode     PIL open -> convert('RGB') -> resize((size, size), BILINEAR): exactly what
              transforms.Resize((s, s)) does to a PIL image (test.py:49-54), on a host
-             thread pool. An 8-bit RGB PNG already size x size (where both are the
-             identity) is only inflated on the host (read_png_filtered) and its PNG
-             filters are undone on the GPU (`rpst_png_unfilter`), bit-exact.
-  ToTensor   on the GPU (`rpst_u8hwc_to_f32nchw`): uint8 bytes cross PCIe, 3 B/pixel
+             thread pool
+  ToTensor   on the GPU (`rpst_u8hwc_to_f32nchw`): uint8 pixels cross PCIe, 3 B/pixel
   save_image on the GPU (`rpst_f32nchw_to_u8_tile`): make_grid(nrow=3, padding=2,
              pad_value=0) of [content, style, stylized] and the single stylised image,
              x*255+0.5 clamped to uint8 (test.py:139-149), then the PNG scanline filter
@@ -92,46 +90,6 @@ def load_image(path: str, size: int) -> np.ndarray:
         return np.asarray(im, dtype=np.uint8).copy()
 
 
-PNG_SIGNATURE = b"\x89PNG\r\n\x1a\n"
-
-
-def read_png_filtered(path: str, size: int) -> Optional[np.ndarray]:
-    """The inflated IDAT scanlines (size, 1 + 3 size) of an 8-bit RGB, non-interlaced PNG of
-    exactly size x size pixels -- Image.open().convert('RGB') + Resize((size, size)) is the
-    identity there, and the reconstruction (the PNG filters) runs on the GPU
-    (rpst_png_unfilter). None for any other file (another format, size, bit depth, colour
-    type or interlacing): the caller decodes it with load_image. zlib releases the GIL, so
-    reader threads inflate in parallel."""
-    import struct
-    import zlib
-    with open(path, "rb") as f:
-        data = f.read()
-    if data[:8] != PNG_SIGNATURE:
-        return None
-    pos, ihdr, idat = 8, None, []
-    while pos + 8 <= len(data):
-        n, kind = struct.unpack(">I4s", data[pos:pos + 8])
-        if kind == b"IHDR":
-            ihdr = struct.unpack(">IIBBBBB", data[pos + 8:pos + 8 + 13])
-        elif kind == b"IDAT":
-            idat.append(data[pos + 8:pos + 8 + n])
-        elif kind == b"IEND":
-            break
-        pos += 12 + n
-    if ihdr is None or not idat:
-        return None
-    w, h, depth, ctype, comp, filt, interlace = ihdr
-    if (w, h) != (size, size) or (depth, ctype, comp, filt, interlace) != (8, 2, 0, 0, 0):
-        return None
-    raw = zlib.decompress(b"".join(idat))
-    if len(raw) != h * (1 + 3 * w):
-        raise ValueError(f"{path}: {len(raw)} bytes of scanlines for a {w}x{h} RGB image")
-    rows = np.frombuffer(raw, np.uint8).reshape(h, 1 + 3 * w)
-    if int(rows[:, 0].max()) > 4:
-        raise ValueError(f"{path}: invalid PNG filter type {int(rows[:, 0].max())}")
-    return rows
-
-
 def save_png(arr: np.ndarray, path: str, level: int = 6) -> None:
     """torchvision.utils.save_image's file write: PIL PNG (zlib level 6 by default)."""
     from PIL import Image
@@ -167,19 +125,6 @@ def write_png(path: str, filtered: np.ndarray, level: int = 6, strategy: str = "
 
 
 # ---- GPU pixel conversions -------------------------------------------------------------
-def png_unfilter(rows: torch.Tensor) -> torch.Tensor:
-    """(N, H, 1 + 3 W) inflated PNG scanlines on the GPU -> (N, H, W, 3) uint8 pixels
-    (rpst_png_unfilter: filter types 0-4, bit-exact with any PNG decoder)."""
-    assert rows.dim() == 3 and rows.dtype == torch.uint8 and rows.is_cuda
-    rows = rows.contiguous()
-    n, h, rb = rows.shape
-    assert (rb - 1) % 3 == 0 and rows.data_ptr() % 4 == 0
-    w = (rb - 1) // 3
-    out = torch.empty((n, h, w, 3), device=rows.device, dtype=torch.uint8)
-    _lib.call("rpst_png_unfilter", rows.data_ptr(), out.data_ptr(), n, h, w, _stream(rows))
-    return out
-
-
 def png_filter_up(u8: torch.Tensor) -> torch.Tensor:
     """(N, H, W, 3) uint8 on the GPU -> (N, H, 1 + 3 W) PNG scanlines with the Up filter
     (rpst_png_filter_up), ready for write_png's deflate."""
@@ -239,8 +184,8 @@ class Pipeline:
 
     stylize(content, style) -> stylized runs on `device` (e.g. a model's `test`).
 
-    Host work is per image on thread pools (zlib and PIL release the GIL): batch k + 1
-    inflates (or PIL-decodes) straight into a pinned buffer while batch k runs on the GPU,
+    Host work is per image on thread pools (PIL releases the GIL in decode, resize and
+    zlib): batch k + 1 decodes straight into a pinned buffer while batch k runs on the GPU,
     and the PNG encodes of batch k are queued as soon as its pixels are back on the host (a
     HIP event on the copy stream), one task per file. png_level / png_strategy: zlib level
     and strategy of the PNGs (PIL's default level 6 and strategy is what
@@ -263,22 +208,14 @@ class Pipeline:
         self.png_strategy = png_strategy
 
     def _decode_start(self, pool, dataset, idx: List[int]):
-        """Queue the decodes of one batch (one task per image) into a pinned buffer of PNG
-        scanlines (N, size, 1 + 3 size): an RGB8 PNG of the right size is only inflated
-        (read_png_filtered; the filters are undone on the GPU), any other image is decoded and
-        resized by PIL and stored as filter-type-0 scanlines."""
+        """Queue the decodes of one batch (one task per image) into a pinned buffer."""
         items = [dataset.item(i) for i in idx]
-        sz = self.img_size
-        pinned = torch.empty((2, len(idx), sz, 1 + 3 * sz), dtype=torch.uint8, pin_memory=True)
-        rows = pinned.numpy()
+        pinned = torch.empty((2, len(idx), self.img_size, self.img_size, 3), dtype=torch.uint8,
+                             pin_memory=True)
+        pix = pinned.numpy()
 
         def load(k, j, path):
-            f = read_png_filtered(path, sz)
-            if f is not None:
-                rows[k, j] = f
-            else:
-                rows[k, j, :, 0] = 0
-                rows[k, j, :, 1:] = load_image(path, sz).reshape(sz, 3 * sz)
+            pix[k, j] = load_image(path, self.img_size)
         futs = [pool.submit(load, k, j, it[k]) for j, it in enumerate(items) for k in (0, 1)]
         return items, pinned, futs
 
@@ -308,13 +245,10 @@ class Pipeline:
                 t1 = clock()
                 st["wait_decode"] += t1 - t0
                 with torch.cuda.stream(copy_stream):
-                    dev_rows = pinned.to(self.device, non_blocking=True)
+                    dev_u8 = pinned.to(self.device, non_blocking=True)
                 compute = torch.cuda.current_stream(self.device)
                 compute.wait_stream(copy_stream)
-                dev_rows.record_stream(compute)
-                nb = pinned.shape[1]
-                dev_u8 = png_unfilter(dev_rows.view(2 * nb, self.img_size, -1)).view(
-                    2, nb, self.img_size, self.img_size, 3)
+                dev_u8.record_stream(compute)
                 content, style = to_tensor(dev_u8[0]), to_tensor(dev_u8[1])
                 stylized = self.stylize(content, style)
                 outs = [to_uint8(stylized)]

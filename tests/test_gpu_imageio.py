@@ -59,69 +59,6 @@ def test_png_filter_up_and_writer_round_trip(cuda, tmp_path):
         np.testing.assert_array_equal(np.asarray(Image.open(p).convert("RGB")), u8[1])
 
 
-def png_filter_rows(pix, types):
-    """PNG spec 9.2 filtering of (H, W, 3) uint8 pixels, scanline r with filter type
-    types[r] -> (H, 1 + 3 W) scanlines (the encoder side, for the reconstruction tests)."""
-    h, w, _ = pix.shape
-    x = pix.reshape(h, 3 * w).astype(np.int32)
-    out = np.empty((h, 1 + 3 * w), np.uint8)
-    z3 = np.zeros(3, np.int32)
-    for r in range(h):
-        cur = x[r]
-        prev = x[r - 1] if r else np.zeros_like(cur)
-        a = np.concatenate([z3, cur[:-3]])
-        b = prev
-        c = np.concatenate([z3, prev[:-3]])
-        t = int(types[r])
-        if t == 0:
-            pred = 0
-        elif t == 1:
-            pred = a
-        elif t == 2:
-            pred = b
-        elif t == 3:
-            pred = (a + b) >> 1
-        else:
-            p = a + b - c
-            pa, pb, pc = np.abs(p - a), np.abs(p - b), np.abs(p - c)
-            pred = np.where((pa <= pb) & (pa <= pc), a, np.where(pb <= pc, b, c))
-        out[r, 0] = t
-        out[r, 1:] = (cur - pred) & 255
-    return out
-
-
-@pytest.mark.parametrize("n,h,w", [(3, 70, 37), (2, 512, 512), (1, 50, 2048), (2, 1, 5)])
-def test_png_unfilter_every_filter_type(cuda, n, h, w):
-    """rpst_png_unfilter reconstructs PNG scanlines of every filter type (0-4, chosen per
-    row at random) bit for bit: several bands (H > 64), bands the LDS limits to fewer rows
-    (W = 2048: 23 rows), odd widths (image bases not 4-byte aligned) and a single row."""
-    from rpst.imageio import png_unfilter
-    rng = np.random.default_rng(h * w)
-    pix = rng.integers(0, 256, size=(n, h, w, 3), dtype=np.uint8)
-    pix[:, h // 2:] //= 7  # runs of small values, where Paeth picks a, b and c in turn
-    rows = np.stack([png_filter_rows(pix[i], rng.integers(0, 5, size=h)) for i in range(n)])
-    got = png_unfilter(torch.from_numpy(rows).to(cuda)).cpu().numpy()
-    np.testing.assert_array_equal(got, pix)
-
-
-def test_png_unfilter_decodes_pil_files(cuda, tmp_path):
-    """read_png_filtered (host inflate) + rpst_png_unfilter == PIL's decode of PNGs that PIL
-    wrote with its adaptive per-row filters, at zlib levels 1 and 6."""
-    from PIL import Image
-    from rpst.imageio import png_unfilter, read_png_filtered
-    rng = np.random.default_rng(11)
-    y, x = np.mgrid[0:96, 0:96]
-    smooth = np.stack([(x * 2 + y) % 256, (x * y) % 256, (y * 3) % 256], -1).astype(np.uint8)
-    for k, img in enumerate((rng.integers(0, 256, (96, 96, 3), dtype=np.uint8), smooth)):
-        for lvl in (1, 6):
-            p = str(tmp_path / f"i{k}{lvl}.png")
-            Image.fromarray(img).save(p, compress_level=lvl)
-            rows = read_png_filtered(p, 96)
-            assert rows is not None
-            got = png_unfilter(torch.from_numpy(rows.copy())[None].to(cuda)).cpu().numpy()[0]
-            np.testing.assert_array_equal(got, np.asarray(Image.open(p).convert("RGB")))
-
-
 def _write_pairs(root, sizes):
     from PIL import Image
     rng = np.random.default_rng(7)
@@ -145,7 +82,6 @@ def test_stylize_driver_end_to_end(cuda, tmp_path, batch_size):
     import stylize
     from rpst.imageio import PairedDataset, load_image
     root = str(tmp_path / "data")
-    # (32, 32, RGB): inflated on the host, reconstructed on the GPU; the others PIL-decoded
     _write_pairs(root, [(40, 30, "RGB"), (64, 64, "RGBA"), (32, 32, "RGB"), (33, 50, "RGB")])
     cfg = {"network": "adain", "vgg": "unused", "rp_blocks": 5, "hidden_dim": 4,
            "content_weight": 1.0, "style_weight": 10.0, "resume": False, "use_mask": False,

@@ -90,56 +90,3 @@ def test_write_png_round_trip(tmp_path):
         p = str(tmp_path / f"w{lvl}{strat}.png")
         write_png(p, f, lvl, strat)
         np.testing.assert_array_equal(np.asarray(Image.open(p).convert("RGB")), a)
-
-
-def _unfilter_ref(rows):
-    """PNG spec 9.2 reconstruction, one pixel at a time (test reference for the host reader)."""
-    h, rb = rows.shape
-    out = np.zeros((h, rb - 1), np.int32)
-    for r in range(h):
-        t = int(rows[r, 0])
-        for i in range(rb - 1):
-            a = out[r, i - 3] if i >= 3 else 0
-            b = out[r - 1, i] if r else 0
-            c = out[r - 1, i - 3] if r and i >= 3 else 0
-            if t == 0:
-                pred = 0
-            elif t == 1:
-                pred = a
-            elif t == 2:
-                pred = b
-            elif t == 3:
-                pred = (a + b) >> 1
-            else:
-                p = a + b - c
-                pa, pb, pc = abs(p - a), abs(p - b), abs(p - c)
-                pred = a if pa <= pb and pa <= pc else (b if pb <= pc else c)
-            out[r, i] = (int(rows[r, 1 + i]) + pred) & 255
-    return out.astype(np.uint8).reshape(h, (rb - 1) // 3, 3)
-
-
-def test_read_png_filtered(tmp_path):
-    """read_png_filtered returns the inflated scanlines of an RGB8 PNG of the requested size
-    (reconstructing them gives PIL's pixels), None for anything the GPU path does not take
-    (another size, RGBA, grayscale, JPEG), and rejects an invalid filter type."""
-    from PIL import Image
-    from rpst.imageio import read_png_filtered, write_png
-    rng = np.random.default_rng(2)
-    a = rng.integers(0, 256, (12, 12, 3), dtype=np.uint8)
-    p = str(tmp_path / "a.png")
-    Image.fromarray(a).save(p)
-    rows = read_png_filtered(p, 12)
-    assert rows.shape == (12, 37)
-    np.testing.assert_array_equal(_unfilter_ref(rows), a)
-    assert read_png_filtered(p, 16) is None
-    Image.fromarray(rng.integers(0, 256, (12, 12, 4), dtype=np.uint8), "RGBA").save(tmp_path / "b.png")
-    assert read_png_filtered(str(tmp_path / "b.png"), 12) is None
-    Image.fromarray(a[..., 0]).save(tmp_path / "c.png")
-    assert read_png_filtered(str(tmp_path / "c.png"), 12) is None
-    Image.fromarray(a).save(tmp_path / "d.jpg")
-    assert read_png_filtered(str(tmp_path / "d.jpg"), 12) is None
-    bad = rows.copy()
-    bad[3, 0] = 7
-    write_png(str(tmp_path / "e.png"), bad, 6)
-    with pytest.raises(ValueError):
-        read_png_filtered(str(tmp_path / "e.png"), 12)

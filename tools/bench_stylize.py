@@ -4,9 +4,8 @@ counterpart of test.py:117-150) against bare AdaINRPNet.test() on resident tenso
 Writes N synthetic photo-like PNG pairs at 512x512 (smooth gradients, sinusoids and mild
 noise, so zlib sees image-like data) into a scratch directory, then times on one GPU:
   test_img_s      AdaINRPNet.test() at batch B on tensors already in HBM (bench.py's step)
-  pipeline_img_s  Pipeline.run over the N pairs: PNG inflate on host threads, H2D of the
-                  scanlines, PNG reconstruction (rpst_png_unfilter) and ToTensor on the GPU,
-                  test(), save_image's pixel path on the
+  pipeline_img_s  Pipeline.run over the N pairs: PNG decode + resize on host threads, H2D of
+                  uint8 pixels, ToTensor on the GPU, test(), save_image's pixel path on the
                   GPU, D2H, PNG encode of {cn}-{sn}.png and the 3-up -cat.png on host threads
   decode / encode host rates with the same thread counts, alone (the host-side bound)
 for three PNG encodings of the same pixels: zlib level 6 with the default strategy
@@ -65,8 +64,7 @@ def main():
     args = ap.parse_args()
     import network as net
     from rpst import synth
-    from rpst.imageio import (PairedDataset, Pipeline, load_image, read_png_filtered, save_png,
-                              write_png)
+    from rpst.imageio import PairedDataset, Pipeline, load_image, save_png, write_png
     dev = torch.device("cuda:0")
     root = tempfile.mkdtemp(prefix="rpst_stylize_", dir="/tmp")
     try:
@@ -90,14 +88,9 @@ def main():
         # 3-up -cat image per pair (here: filtered on the host from the decoded photos)
         encs = {"l6": (6, "default"), "rle": (6, "rle"), "l0": (0, "default")}
         with ThreadPoolExecutor(args.workers) as pool:
-            # the pipeline's host decode: inflate only (read_png_filtered; the PNG filters are
-            # undone on the GPU) -- and PIL's full decode for comparison
-            t0 = time.perf_counter()
-            list(pool.map(lambda p: read_png_filtered(p, args.size), paths))
-            rec["decode_pairs_s"] = round(args.pairs / (time.perf_counter() - t0), 1)
             t0 = time.perf_counter()
             imgs = list(pool.map(lambda p: load_image(p, args.size), paths))
-            rec["pil_decode_pairs_s"] = round(args.pairs / (time.perf_counter() - t0), 1)
+            rec["decode_pairs_s"] = round(args.pairs / (time.perf_counter() - t0), 1)
         pad = np.zeros((args.size + 4, 3 * (args.size + 2) + 2, 3), np.uint8)
         single = [up_filter(imgs[2 * i]) for i in range(min(args.pairs, 16))]
         cat = []
@@ -120,20 +113,6 @@ def main():
                 rec[f"encode_pairs_s_{name}"] = round(args.pairs / (time.perf_counter() - t0), 1)
                 rec[f"png_bytes_per_pair_{name}"] = (os.path.getsize(os.path.join(out, "0.png")) +
                                                      os.path.getsize(os.path.join(out, "0c.png")))
-        # the GPU side of the decode: PNG reconstruction of one batch (2 x batch images)
-        from rpst.imageio import png_unfilter
-        nb = min(2 * args.batch, len(paths))
-        rows = torch.from_numpy(np.stack([read_png_filtered(p, args.size) for p in paths[:nb]]))
-        rows = rows.to(dev)
-        png_unfilter(rows)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(3):
-            png_unfilter(rows)
-        e1.record()
-        torch.cuda.synchronize()
-        rec["unfilter_ms_per_batch"] = round(e0.elapsed_time(e1) / 3, 3)
-        del rows
         # bare test() on resident tensors
         cfg = {"rp_blocks": 5, "hidden_dim": 16, "content_weight": 1.0, "style_weight": 10.0,
                "resume": False}
