@@ -23,7 +23,9 @@ if [ "${PART:-1}" = 1 ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_adain -o adain -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs > $O/prof_adain.log 2>&1 || exit 1
 else
-  for m in ${RUNS:-"--config 2" "--config 3" "--config 4" "--model forward" "--model multiscale" "--model source" "--model adaptive" "--model train" "--model train_wct" "--model train_sanet" "--model train_multiscale" "--model train_source" "--model train_adaptive"}; do
+  # RUNS: '|'-separated bench.py argument sets (default: all of them)
+  IFS='|' read -r -a LINES <<< "${RUNS:---config 2|--config 3|--config 4|--model forward|--model multiscale|--model source|--model adaptive|--model train|--model train_wct|--model train_sanet|--model train_multiscale|--model train_source|--model train_adaptive}"
+  for m in "${LINES[@]}"; do
     f=$O/bench_$(echo $m | tr -d ' -').json
     timeout -k 10 400 python bench.py $m --no-cpu-baseline > $f 2> $f.err || { tail $f.err; exit 1; }
     python -c "import json;d=json.load(open('$f'));r=d['roofline'];print('$m', d['value'], d['ms_per_step'], r['kernel'], r['frac'])"
