@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--workers", type=int, default=4, help="decode threads")
     ap.add_argument("--encode-workers", type=int, default=12, help="deflate / write threads")
+    ap.add_argument("--rle-splits", default="",
+                    help="extra rle pipeline runs at other decode:encode thread splits, e.g. 5:11,6:10")
     args = ap.parse_args()
     import network as net
     from rpst import synth
@@ -132,12 +134,16 @@ def main():
         torch.cuda.synchronize()
         rec["test_img_s"] = round(reps * args.batch / (time.perf_counter() - t0), 1)
         del c, s
-        # the pipeline, end to end (a warm-up pass over one batch first)
-        for name, (lvl, strat) in encs.items():
-            # the thread split follows the bound: the default match search at level 6 gets
-            # most threads for encoding; rle and stored PNGs are decode-bound: an even split
-            dw, ew = (args.workers, args.encode_workers) if name != "l0" else (
-                (args.workers + args.encode_workers) // 2,) * 2
+        # the pipeline, end to end (a warm-up pass over one batch first). The thread split
+        # follows the bound: the deflating encodings get most threads for encoding; stored
+        # PNGs are decode-bound, an even split
+        half = (args.workers + args.encode_workers) // 2
+        runs = [(name, lvl, strat, (args.workers, args.encode_workers) if name != "l0" else (half, half))
+                for name, (lvl, strat) in encs.items()]
+        for sp in filter(None, args.rle_splits.split(",")):
+            dw, ew = (int(v) for v in sp.split(":"))
+            runs.append((f"rle_{dw}_{ew}", 6, "rle", (dw, ew)))
+        for name, lvl, strat, (dw, ew) in runs:
             rec[f"pipeline_threads_{name}"] = [dw, ew]
             pipe = Pipeline(m.test, dev, args.size, args.batch, dw, png_level=lvl,
                             encode_workers=ew, png_strategy=strat)
@@ -154,8 +160,9 @@ def main():
             rec[f"pipeline_host_s_{name}"] = {k: round(v, 3) for k, v in pipe.stats.items()}
             rec[f"pipeline_wall_s_{name}"] = round(dt, 3)
             shutil.rmtree(os.path.join(root, f"out{name}"), ignore_errors=True)
-        for name in encs:
+        for name, *_ in runs:
             rec[f"pipeline_vs_test_{name}"] = round(rec[f"pipeline_img_s_{name}"] / rec["test_img_s"], 3)
+        for name in encs:
             # host bound: decode and deflate run on their own thread pools (rates measured
             # above with --workers decode / --encode-workers deflate threads)
             rec[f"host_bound_pairs_s_{name}"] = min(rec["decode_pairs_s"],
