@@ -87,7 +87,7 @@ def main(argv=None) -> int:
     ap.add_argument("--png-strategy", default="rle", choices=["default", "filtered", "huffman", "rle"],
                     help="zlib strategy of the written PNGs (rle: ~6x faster than the default "
                          "match search at level 6, ~1.5 %% larger files, identical pixels)")
-    ap.add_argument("--encode-workers", type=int, default=8,
+    ap.add_argument("--encode-workers", type=int, default=11,
                     help="PNG writer threads (decode threads: the config's num_workers)")
     args = ap.parse_args(argv)
     with open(args.config) as f:

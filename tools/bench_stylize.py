@@ -13,7 +13,7 @@ for three PNG encodings of the same pixels: zlib level 6 with the default strate
 The PNG scanline filter runs on the GPU (rpst_png_filter_up), so the host threads only
 decode, deflate and write.
 
-    python tools/bench_stylize.py [--pairs 512] [--batch 32] [--workers 4] [--encode-workers 12]
+    python tools/bench_stylize.py [--pairs 512] [--batch 32] [--workers 5] [--encode-workers 11]
 """
 import argparse
 import json
@@ -59,8 +59,8 @@ def main():
     ap.add_argument("--pairs", type=int, default=512)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--size", type=int, default=512)
-    ap.add_argument("--workers", type=int, default=4, help="decode threads")
-    ap.add_argument("--encode-workers", type=int, default=12, help="deflate / write threads")
+    ap.add_argument("--workers", type=int, default=5, help="decode threads")
+    ap.add_argument("--encode-workers", type=int, default=11, help="deflate / write threads")
     ap.add_argument("--rle-splits", default="",
                     help="extra rle pipeline runs at other decode:encode thread splits, e.g. 5:11,6:10")
     args = ap.parse_args()
