@@ -26,6 +26,8 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional, Tuple
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -607,6 +609,9 @@ def _transform_backward(tr, saved, g, grads):
     _sanet_backward(tr.sanet5_1, sb, _upsample_backward(dz), grads)
 
 
+SAM_F4_SLICES = 0
+
+
 class _SAModelStep(torch.autograd.Function):
     @staticmethod
     def forward(ctx, content, style, model, cfg, *params):
@@ -624,8 +629,15 @@ class _SAModelStep(torch.autograd.Function):
         # frozen VGG of the inputs: constants of the step, but they feed the differentiated
         # transforms, so they stay precise: on F(4x4) the AdaptiveSAModel's style loss moves
         # 2.85e-4 against its 2.73e-4 bar (profiles/r04f) and SAModel's sanet5_1.h.weight
-        # gradient 1.06e-4 against 1e-4 (profiles/r04g)
-        feats = model.encode_with_intermediate(torch.cat([style, content], dim=0))
+        # gradient 1.06e-4 against 1e-4 (profiles/r04g). The first SAM_F4_SLICES VGG slices
+        # (relu1_1 .. ) may run F(4x4) (RPST_SAM_F4_SLICES overrides; accuracy A/B)
+        feats = []
+        x = torch.cat([style, content], dim=0)
+        f4 = int(os.environ.get("RPST_SAM_F4_SLICES", SAM_F4_SLICES))
+        for i in range(5):
+            with ops.precise_convs(on=None if i >= f4 else False):
+                x = getattr(model, f"enc_{i + 1}")(x)
+            feats.append(x)
         sf = [f[:n].contiguous() for f in feats]
         cf = [f[n:].contiguous() for f in feats]
         dec_steps = plan.compile_layers(model.decoder.children())
