@@ -630,7 +630,9 @@ class _SAModelStep(torch.autograd.Function):
         # transforms, so they stay precise: on F(4x4) the AdaptiveSAModel's style loss moves
         # 2.85e-4 against its 2.73e-4 bar (profiles/r04f) and SAModel's sanet5_1.h.weight
         # gradient 1.06e-4 against 1e-4 (profiles/r04g). The first SAM_F4_SLICES VGG slices
-        # (relu1_1 .. ) may run F(4x4) (RPST_SAM_F4_SLICES overrides; accuracy A/B)
+        # (relu1_1 .. ) may run F(4x4) (RPST_SAM_F4_SLICES overrides; accuracy A/B,
+        # profiles/r04/sam_f4.log: one slice passes the tests for +0.5 %, two already move
+        # sanet4_1.h.weight's gradient to 3.5e-4 against 1e-4, so 0)
         feats = []
         x = torch.cat([style, content], dim=0)
         f4 = int(os.environ.get("RPST_SAM_F4_SLICES", SAM_F4_SLICES))
