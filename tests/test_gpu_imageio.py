@@ -142,3 +142,33 @@ def test_baseline_config0_256_pair(cuda, tmp_path):
         assert got.shape == ref.shape, suffix
         diff = np.abs(got.astype(int) - ref.astype(int))
         assert diff.max() <= 1 and (diff == 0).mean() > 0.99, (suffix, diff.max())
+
+
+def test_stylize_png_strategies_same_pixels(cuda, tmp_path):
+    """stylize.py's --png-strategy / --png-compress-level change only the deflate stream: the
+    files of the default (rle) run and of torchvision's level-6 default strategy decode to
+    the same pixels."""
+    from PIL import Image
+
+    import stylize
+    root = str(tmp_path / "data")
+    _write_pairs(root, [(32, 32, "RGB"), (40, 30, "RGB")])
+    outs = {}
+    for strat, lvl in (("rle", 6), ("default", 6), ("default", 0)):
+        cfg = {"network": "adain", "vgg": "unused", "rp_blocks": 5, "hidden_dim": 4,
+               "content_weight": 1.0, "style_weight": 10.0, "resume": False, "use_mask": False,
+               "img_size": 32, "test_dir": root, "test_dataset": "paired", "batch_size": 2,
+               "num_workers": 2, "output": str(tmp_path / f"out_{strat}{lvl}")}
+        cfg_path = str(tmp_path / f"cfg_{strat}{lvl}.yaml")
+        with open(cfg_path, "w") as f:
+            yaml.safe_dump(cfg, f)
+        assert stylize.main(["--config", cfg_path, "--synthetic-weights", "5", "--png-strategy",
+                             strat, "--png-compress-level", str(lvl)]) == 0
+        d = tmp_path / f"out_{strat}{lvl}" / "test" / "test_output"
+        outs[(strat, lvl)] = {p.name: np.asarray(Image.open(p)) for p in sorted(d.glob("*.png"))}
+    ref = outs[("default", 6)]
+    assert len(ref) == 4
+    for key, got in outs.items():
+        assert got.keys() == ref.keys(), key
+        for name in ref:
+            np.testing.assert_array_equal(got[name], ref[name], err_msg=f"{key} {name}")
