@@ -113,16 +113,26 @@ __device__ __forceinline__ int refl(int t, int n) { return t < 0 ? -t : (t >= n 
 // row 0 / H+1) the line is dY's row 0 / H-1 and the taps are the weights' row 0 / 2; for side
 // 2/3 (padded column 0 / W+1) the line is dY's column 0 / W-1 and the taps the weights'
 // column 0 / 2:  ring[ci][u] = sum_co sum_k line[co][u - k] tap[co][ci][k].
-// Block = (64 ring positions) x (64 input channels) of one image and side; co in chunks of
-// 16 staged in LDS (line segment with its 2-element halo, taps transposed ci-contiguous);
-// each thread accumulates 4 ci x 4 positions.
+// Block = (64 ring positions) x (64 input channels) of one image and side and one of ks
+// split-K ranges of co (a latency-bound co loop otherwise: 32 chunks at Cout = 512); co in
+// chunks of 16 staged in LDS (line segment with its 2-element halo, taps transposed
+// ci-contiguous); each thread accumulates 4 ci x 4 positions. Split s writes ring copy s; the
+// fold sums the copies in order (ks is a function of Cout only).
+constexpr int kRingKS = 4;  // ring copies in the workspace
+static int ring_splits(int Cout) {
+  const int ks = Cout / 64;
+  return ks < 1 ? 1 : (ks > kRingKS ? kRingKS : ks);
+}
 __global__ __launch_bounds__(256) void reflect_ring_kernel(
     const float* __restrict__ dy, const float* __restrict__ w, float* __restrict__ ring, int N,
-    int Cin, int Cout, int H, int W) {
+    int Cin, int Cout, int H, int W, int ks) {
   constexpr int CC = 16;
   __shared__ float line[CC][64 + 2];
   __shared__ __attribute__((aligned(16))) float taps[CC][3][64];
-  const int side = blockIdx.z & 3, n = blockIdx.z >> 2;
+  const int split = blockIdx.z % ks, zs = blockIdx.z / ks;
+  const int side = zs & 3, n = zs >> 2;
+  const int cper = ((Cout + ks - 1) / ks + CC - 1) / CC * CC;
+  const int cbeg = split * cper, cend = min(Cout, cbeg + cper);
   const bool row = side < 2;
   const int L = row ? W : H;                  // line length
   const int U = row ? W + 2 : H;              // outputs on this side
@@ -143,7 +153,7 @@ __global__ __launch_bounds__(256) void reflect_ring_kernel(
       const int e = tid + 256 * i;
       const int cc = e / 66, tt = e - cc * 66, t = u0 - 2 + tt, co = c0 + cc;
       float v = 0.f;
-      if (e < CC * 66 && co < Cout && t >= 0 && t < L) {
+      if (e < CC * 66 && co < cend && t >= 0 && t < L) {
         const int64_t off = row ? (int64_t)(side == 0 ? 0 : H - 1) * W + t
                                 : (int64_t)t * W + (side == 2 ? 0 : W - 1);
         v = dyn[co * HW + off];
@@ -156,15 +166,15 @@ __global__ __launch_bounds__(256) void reflect_ring_kernel(
       const int cc = e / 192, r = e - cc * 192, k = r / 64, c = r - k * 64;
       const int co = c0 + cc, ci = ci0 + c;
       float v = 0.f;
-      if (co < Cout && ci < Cin) {
+      if (co < cend && ci < Cin) {
         const int kh = row ? (side == 0 ? 0 : 2) : k, kw = row ? k : (side == 2 ? 0 : 2);
         v = w[((int64_t)co * Cin + ci) * 9 + kh * 3 + kw];
       }
       tv[i] = v;
     }
   };
-  gload(0);
-  for (int c0 = 0; c0 < Cout; c0 += CC) {
+  gload(cbeg);
+  for (int c0 = cbeg; c0 < cend; c0 += CC) {
 #pragma unroll
     for (int i = 0; i < kLn; ++i) {
       const int e = tid + 256 * i;
@@ -176,7 +186,7 @@ __global__ __launch_bounds__(256) void reflect_ring_kernel(
       taps[e / 192][(e % 192) / 64][e % 64] = tv[i];
     }
     __syncthreads();
-    if (c0 + CC < Cout) gload(c0 + CC);
+    if (c0 + CC < cend) gload(c0 + CC);
 #pragma unroll 4
     for (int cc = 0; cc < CC; ++cc) {
 #pragma unroll
@@ -202,7 +212,7 @@ __global__ __launch_bounds__(256) void reflect_ring_kernel(
   for (int a = 0; a < 4; ++a) {
     const int ci = ci0 + cg * 4 + a;
     if (ci >= Cin) continue;
-    float* rg = ring + ((int64_t)n * Cin + ci) * R;
+    float* rg = ring + ((int64_t)split * N * Cin + (int64_t)n * Cin + ci) * R;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int u = u0 + ug * 4 + e;
@@ -213,7 +223,7 @@ __global__ __launch_bounds__(256) void reflect_ring_kernel(
 
 __global__ __launch_bounds__(256) void reflect_fold_kernel(
     const float* __restrict__ ring, float* __restrict__ dx, const float* __restrict__ mask,
-    int N, int Cin, int H, int W, int nrows, int r0, int r1, int ncols, int c0, int c1) {
+    int N, int Cin, int H, int W, int nrows, int r0, int r1, int ncols, int c0, int c1, int ks) {
   const int64_t per = (int64_t)nrows * W + (int64_t)ncols * (H - nrows);
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)N * Cin * per) return;
@@ -236,19 +246,25 @@ __global__ __launch_bounds__(256) void reflect_fold_kernel(
   }
   const int R = 2 * (W + 2) + 2 * H;
   const float* rg = ring + plane * R;
+  const int64_t copy = (int64_t)N * Cin * R;
+  auto rv = [&](int idx) {  // ring entry idx, its ks split-K copies summed in order
+    float v = rg[idx];
+    for (int s = 1; s < ks; ++s) v += rg[s * copy + idx];
+    return v;
+  };
   float add = 0.f;
   // padded rows p in {0, H+1}: every column q of the padded row that reflects to j
   for (int pi = 0; pi < 2; ++pi) {
     const int p = pi ? H + 1 : 0;
     if (refl(p - 1, H) != i) continue;
-    const float* row = rg + pi * (W + 2);
-    if (refl(-1, W) == j) add += row[0];
-    add += row[j + 1];
-    if (refl(W, W) == j) add += row[W + 1];
+    const int row = pi * (W + 2);
+    if (refl(-1, W) == j) add += rv(row);
+    add += rv(row + j + 1);
+    if (refl(W, W) == j) add += rv(row + W + 1);
   }
   // padded columns q in {0, W+1} on the interior padded row p = i + 1
-  if (refl(-1, W) == j) add += rg[2 * (W + 2) + i];
-  if (refl(W, W) == j) add += rg[2 * (W + 2) + H + i];
+  if (refl(-1, W) == j) add += rv(2 * (W + 2) + i);
+  if (refl(W, W) == j) add += rv(2 * (W + 2) + H + i);
   const int64_t o = plane * H * W + (int64_t)i * W + j;
   if (mask && !(mask[o] > 0.f)) return;  // threshold_backward: dx stays 0 there
   dx[o] = dx[o] + add;
@@ -597,7 +613,7 @@ extern "C" int rpst_maxpool2x2_ceil_backward(const float* x, const float* g, flo
 
 extern "C" size_t rpst_reflect_pad_border_grad_workspace_size(int N, int Cin, int H, int W) {
   if (N <= 0 || Cin <= 0 || H <= 0 || W <= 0) return 0;
-  return sizeof(float) * (size_t)N * Cin * (2 * (size_t)(W + 2) + 2 * (size_t)H);
+  return sizeof(float) * kRingKS * (size_t)N * Cin * (2 * (size_t)(W + 2) + 2 * (size_t)H);
 }
 
 extern "C" int rpst_reflect_pad_border_grad(const float* dy, const float* w, float* dx, int N,
@@ -619,16 +635,17 @@ extern "C" int rpst_reflect_pad_border_grad_masked(const float* dy, const float*
   }
   hipStream_t st = as_stream(stream);
   float* ring = static_cast<float*>(workspace);
-  RPST_REQUIRE((int64_t)N * 4 <= 65535, "reflect_border_grad: batch too large");
+  const int ks = ring_splits(Cout);
+  RPST_REQUIRE((int64_t)N * 4 * ks <= 65535, "reflect_border_grad: batch too large");
   const int umax = (W + 2 > H ? W + 2 : H);
-  reflect_ring_kernel<<<dim3((umax + 63) / 64, (Cin + 63) / 64, N * 4), 256, 0, st>>>(
-      dy, w, ring, N, Cin, Cout, H, W);
+  reflect_ring_kernel<<<dim3((umax + 63) / 64, (Cin + 63) / 64, N * 4 * ks), 256, 0, st>>>(
+      dy, w, ring, N, Cin, Cout, H, W, ks);
   if (int e = launch_status("reflect_ring_kernel")) return e;
   const int r0 = 1, r1 = H - 2, c0 = 1, c1 = W - 2;
   const int nrows = (r0 == r1) ? 1 : 2, ncols = (c0 == c1) ? 1 : 2;
   const int64_t per = (int64_t)nrows * W + (int64_t)ncols * (H - nrows);
   reflect_fold_kernel<<<blocks_for((int64_t)N * Cin * per), 256, 0, st>>>(
-      ring, dx, mask, N, Cin, H, W, nrows, r0, r1, ncols, c0, c1);
+      ring, dx, mask, N, Cin, H, W, nrows, r0, r1, ncols, c0, c1, ks);
   return launch_status("reflect_fold_kernel");
 }
 

@@ -27,7 +27,9 @@ def gen(seed, shape, scale=1.0, offset=0.0):
 # ---- kernels ---------------------------------------------------------------------------
 @pytest.mark.parametrize("pad", ["zero", "reflect"])
 @pytest.mark.parametrize("shape", [(2, 16, 12, 20, 32), (1, 3, 9, 7, 8), (2, 64, 33, 70, 40),
-                                   (1, 8, 70, 9, 12), (2, 5, 2, 2, 7), (1, 80, 3, 130, 20)])
+                                   (1, 8, 70, 9, 12), (2, 5, 2, 2, 7), (1, 80, 3, 130, 20),
+                                   # Cout >= 128: the reflect border's split-K ring (3 / 4 copies)
+                                   (1, 48, 10, 37, 200), (2, 24, 5, 66, 300)])
 def test_conv_dgrad(cuda, pad, shape):
     from rpst import autograd as A
     from rpst import ops, plan
