@@ -259,7 +259,9 @@ constexpr int kW4Rows = 16, kW4Cols = 64, kW4Co = 32;
 bool wino4_supports(int in_op);
 bool wino4_fits(int N, int Cin, int Hs, int Ws, int in_op);
 int wino4_persist();
-int wino4_rows(int Cin, int Cout);  // tile rows per F(4x4) block: 4 (16 output rows) or 2
+// tile rows per F(4x4) block: 4 (16 output rows) or 2 (the position-quarter kernel, or the
+// small layers' 2-row block); statistics partials are per tile row either way
+int wino4_rows(int Cin, int Cout, int in_op);
 size_t wino4_packed_floats(int Cout, int Cin);
 int wino4_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);
 int wino4_launch(ConvArgs& a, int in_op, hipStream_t st);
@@ -269,6 +271,23 @@ int wino4_fold(ConvArgs& a, const float* direct_packed, int direct_cout_pad, flo
 size_t wino4_mix_floats(int N, int Cin, int Cout);
 int wino4_mix(ConvArgs& a, const double* T, const double* cvec, const float* direct_packed,
               int direct_cout_pad, float* ws, hipStream_t st);
+
+// ---- F(4x4,3x3), position-quarter form (rpst_wino4q.hip) ------------------------------
+// 8 x 64 outputs x 64 channels per 512-thread block, each wave 9 of the 36 positions. Its
+// weight image follows the F(4x4) one in the packed buffer; wino4_launch / wino4_fold /
+// wino4_mix dispatch to it for the layers wino4q_applies to.
+bool wino4q_applies(int Cin, int Cout, int in_op);
+size_t wino4q_packed_floats(int Cout, int Cin);
+int wino4q_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);
+int wino4q_pack_mix(const double* wm, float* pk, int N, int Cout, int Cin, hipStream_t st);
+int wino4q_fold_w(const float* pk, float* out, const float* aux, int N, int Cout, int Cin,
+                  hipStream_t st);
+int wino4q_launch(ConvArgs& a, int in_op, hipStream_t st);
+// floats of the F(4x4) weight image a layer launches with (per image when folded)
+inline size_t wino4_image_floats(int Cout, int Cin, int in_op) {
+  return wino4q_applies(Cin, Cout, in_op) ? wino4q_packed_floats(Cout, Cin)
+                                          : wino4_packed_floats(Cout, Cin);
+}
 
 
 }  // namespace rpst

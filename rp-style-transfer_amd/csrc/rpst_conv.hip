@@ -691,11 +691,11 @@ static ConvGeom conv_geom(int N, int Cin, int Hs, int Ws, int Cout, int ksize, i
   g.tiles_x = (W + kTW - 1) / kTW;
   g.stat_tw = kTW;
   if (g.algo == RPST_CONV_WINOGRAD4) {
-    const int nr = wino4_rows(Cin, Cout);
+    const int nr = wino4_rows(Cin, Cout, in_op);
     g.tiles_x = (W + kW4Cols - 1) / kW4Cols;
     const int ty = (H + 4 * nr - 1) / (4 * nr);
     g.blocks = (int64_t)g.tiles_x * ty * N * (wino4_persist() ? 1 : (Cout + kW4Co - 1) / kW4Co);
-    g.nth = 128 * nr;
+    g.nth = wino4q_applies(Cin, Cout, in_op) ? 512 : 128 * nr;
     g.stat_P = g.tiles_x * ty * nr;
     g.stat_nt = 4;
     g.stat_wn = nr;
@@ -739,7 +739,9 @@ using namespace rpst;
 extern "C" size_t rpst_conv2d_packed_size(int Cout, int Cin, int ksize) {
   if (Cout <= 0 || Cin <= 0 || (ksize != 1 && ksize != 3)) return 0;
   size_t f = direct_packed_floats(Cout, Cin, ksize);
-  if (ksize == 3) f += wino_packed_floats(Cout, Cin) + wino4_packed_floats(Cout, Cin);
+  if (ksize == 3)
+    f += wino_packed_floats(Cout, Cin) + wino4_packed_floats(Cout, Cin) +
+         wino4q_packed_floats(Cout, Cin);
   return f * sizeof(float);
 }
 
@@ -774,8 +776,9 @@ extern "C" int rpst_conv2d_pack(const float* weight, float* packed, int Cout, in
   if (int e = launch_status("conv_pack_kernel")) return e;
   if (ksize == 3) {
     if (int e = wino_pack(weight, packed + total, Cout, Cin, as_stream(stream))) return e;
-    return wino4_pack(weight, packed + total + wino_packed_floats(Cout, Cin), Cout, Cin,
-                      as_stream(stream));
+    float* w4 = packed + total + wino_packed_floats(Cout, Cin);
+    if (int e = wino4_pack(weight, w4, Cout, Cin, as_stream(stream))) return e;
+    return wino4q_pack(weight, w4 + wino4_packed_floats(Cout, Cin), Cout, Cin, as_stream(stream));
   }
   return RPST_OK;
 }
@@ -890,9 +893,12 @@ static int conv_common(const float* input, const float* aux, const float* aux2,
     a.stat_part = stat_part;
     int op = in_op;
     // AdaIN in the weights (not with the statistics epilogue: that layer keeps the loader)
-    if (in_op == RPST_IN_ADAIN && fold_ws && !stat_part && a.H >= 2 && a.W >= 2) {
+    const bool fold = in_op == RPST_IN_ADAIN && fold_ws && !stat_part && a.H >= 2 && a.W >= 2;
+    if (fold) op = RPST_IN_NONE;
+    // the position-quarter kernel's image follows the F(4x4) one
+    if (wino4q_applies(Cin, Cout, op)) a.wpk += wino4_packed_floats(Cout, Cin);
+    if (fold) {
       if (int e = wino4_fold(a, packed_weight, pad_cout(Cout), fold_ws, st)) return e;
-      op = RPST_IN_NONE;
     }
     if (int e = wino4_launch(a, op, st)) return e;
     if (mask) {  // F(4x4)'s epilogue has no mask: threshold the output in a second pass
@@ -1079,6 +1085,7 @@ extern "C" int rpst_conv2d_mix(const float* input, const double* T, const double
   ConvArgs a{};
   a.in = input;
   a.wpk = packed_weight + direct_packed_floats(Cout, Cin, ksize) + wino_packed_floats(Cout, Cin);
+  if (wino4q_applies(Cin, Cout, RPST_IN_NONE)) a.wpk += wino4_packed_floats(Cout, Cin);
   a.bias = bias;
   a.out = out;
   a.N = N;

@@ -195,11 +195,12 @@ int wino4_persist() { return 1; }  // one block per spatial tile loops over the 
 // of the first dispatch round sleeping 16k / 36k cycles first) changed nothing (16->32
 // 0.970 / 0.976 / 0.969 ms, profiles/r03/wino4_half_ab.log): the small layers are not bound
 // by exposed prologues. Only the two smallest layers switch.
-int wino4_rows(int Cin, int Cout) {
+int wino4_rows(int Cin, int Cout, int in_op) {
   static const int lim = [] {
     const char* e = getenv("RPST_WINO4_HALF");
     return (e && *e) ? atoi(e) : 512;
   }();
+  if (wino4q_applies(Cin, Cout, in_op)) return 2;  // rpst_wino4q.hip: 8 output rows
   return (int64_t)Cin * Cout <= lim ? 2 : 4;
 }
 
@@ -936,8 +937,9 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
 // padding every tap sees s * x + b, so all nine classes are equal). The conv itself then
 // streams the raw feature by plain LDS-DMA: no per-element affine, no extra LDS traffic.
 size_t wino4_fold_floats(int N, int Cin, int Cout) {
-  // per-image packed U and border biases, then the class sums (fp64)
-  return (size_t)N * (wino4_packed_floats(Cout, Cin) + (size_t)Cout * 9) +
+  // per-image packed U (the layout the folded NONE launch runs) and border biases, then the
+  // class sums (fp64)
+  return (size_t)N * (wino4_image_floats(Cout, Cin, RPST_IN_NONE) + (size_t)Cout * 9) +
          2 * (size_t)9 * Cout * Cin + 2;
 }
 
@@ -1042,14 +1044,20 @@ int wino4_fold(ConvArgs& a, const float* direct_packed, int direct_cout_pad, flo
                hipStream_t st) {
   RPST_REQUIRE(a.H >= 2 && a.W >= 2, "conv2d: folded AdaIN needs H, W >= 2");
   const int nch = (a.Cin + kW4CK - 1) / kW4CK;
-  const int64_t per = (int64_t)wino4_packed_floats(a.Cout, a.Cin);
+  // a.wpk is the image of the launched (NONE) form: the quarter layout where it applies
+  const bool q = wino4q_applies(a.Cin, a.Cout, RPST_IN_NONE);
+  const int64_t per = (int64_t)wino4_image_floats(a.Cout, a.Cin, RPST_IN_NONE);
   const int64_t n4 = (int64_t)a.N * (per / 4);
   float* wf = ws;
   float* bt = ws + (int64_t)a.N * per;
-  wino4_fold_w_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(
-      reinterpret_cast<const float4*>(a.wpk), reinterpret_cast<float4*>(wf), a.aux, a.N, a.Cin,
-      nch, per / 4);
-  if (int e = launch_status("wino4_fold_w_kernel")) return e;
+  if (q) {
+    if (int e = wino4q_fold_w(a.wpk, wf, a.aux, a.N, a.Cout, a.Cin, st)) return e;
+  } else {
+    wino4_fold_w_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(
+        reinterpret_cast<const float4*>(a.wpk), reinterpret_cast<float4*>(wf), a.aux, a.N,
+        a.Cin, nch, per / 4);
+    if (int e = launch_status("wino4_fold_w_kernel")) return e;
+  }
   double* S = align8(bt + (int64_t)a.N * a.Cout * 9);
   if (int e = border_biases(direct_packed, direct_cout_pad, a.bias, a.aux, nullptr, bt, S, a.N,
                             a.Cin, a.Cout, a.pad == RPST_PAD_REFLECT, st))
@@ -1089,7 +1097,8 @@ int wino4_mix(ConvArgs& a, const double* T, const double* cvec, const float* dir
               int direct_cout_pad, float* ws, hipStream_t st) {
   RPST_REQUIRE(a.H >= 2 && a.W >= 2, "conv2d_mix: needs H, W >= 2");
   const int nch = (a.Cin + kW4CK - 1) / kW4CK;
-  const int64_t per = (int64_t)wino4_packed_floats(a.Cout, a.Cin);
+  const bool q = wino4q_applies(a.Cin, a.Cout, RPST_IN_NONE);
+  const int64_t per = (int64_t)wino4_image_floats(a.Cout, a.Cin, RPST_IN_NONE);
   float* wf = ws;
   float* bt = ws + (int64_t)a.N * per;
   double* S = align8(bt + (int64_t)a.N * a.Cout * 9);
@@ -1102,9 +1111,13 @@ int wino4_mix(ConvArgs& a, const double* T, const double* cvec, const float* dir
   // W'_n = W T_n on the fp64 MFMA: (9 Cout x Cin) x (Cin x Cin) per image
   if (int e = gemm_f32w_f64(wt, T, wm, a.N, 9 * a.Cout, a.Cin, st)) return e;
   const int64_t tot = (int64_t)a.N * per;
-  wino4_pack_kernel<double><<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(
-      wm, wf, a.Cout, a.Cin, nch, per, tot, a.Cin, 1, (int64_t)a.Cout * a.Cin);
-  if (int e = launch_status("wino4_pack_kernel(mix)")) return e;
+  if (q) {
+    if (int e = wino4q_pack_mix(wm, wf, a.N, a.Cout, a.Cin, st)) return e;
+  } else {
+    wino4_pack_kernel<double><<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(
+        wm, wf, a.Cout, a.Cin, nch, per, tot, a.Cin, 1, (int64_t)a.Cout * a.Cin);
+    if (int e = launch_status("wino4_pack_kernel(mix)")) return e;
+  }
   if (int e = border_biases(direct_packed, direct_cout_pad, a.bias, nullptr, cvec, bt, S, a.N,
                             a.Cin, a.Cout, a.pad == RPST_PAD_REFLECT, st))
     return e;
@@ -1118,10 +1131,11 @@ int wino4_launch(ConvArgs& a, int in_op, hipStream_t st) {
   RPST_REQUIRE(wino4_supports(in_op), "conv2d: winograd4 does not support in_op %d", in_op);
   RPST_REQUIRE(a.res == nullptr, "conv2d: winograd4 has no residual epilogue");
   RPST_REQUIRE(wino4_fits(a.N, a.Cin, a.Hs, a.Ws, in_op), "conv2d: image too large for winograd4");
+  if (wino4q_applies(a.Cin, a.Cout, in_op)) return wino4q_launch(a, in_op, st);
   a.Cout_pad = (a.Cout + kW4BM - 1) / kW4BM * kW4BM;
   a.nchunks = (a.Cin + kW4CK - 1) / kW4CK;
   a.tiles_x = (a.W + kW4TW - 1) / kW4TW;
-  const int nr = wino4_rows(a.Cin, a.Cout);
+  const int nr = wino4_rows(a.Cin, a.Cout, in_op);
   a.tiles_y = (a.H + 4 * nr - 1) / (4 * nr);
   a.co_tiles = a.Cout_pad / kW4BM;
   a.stat_P = a.tiles_x * a.tiles_y * nr;

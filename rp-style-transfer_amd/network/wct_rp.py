@@ -10,6 +10,7 @@ fp32, widened to fp64 in registers, and the fused feature is written back as fp3
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 import torch.nn as nn
@@ -24,13 +25,26 @@ from .base import (BaseNet, build_decrease_depth_rp_blocks, build_increase_depth
 
 # RPST_FUSE_WCT=0 disables the fused path (A/B measurements, debugging)
 FUSED_WCT = os.environ.get("RPST_FUSE_WCT", "1") != "0"
-# RPST_WCT_CHECK=1: read the per-image WCT status after each launch (one host sync) and raise
-# on an invalid image (non-convergence, or a timed-out persistent launch) instead of letting
-# its NaN output through; off by default (the inference path never synchronises)
+# Every WCT launch returns a per-image status word (non-convergence, or a timed-out persistent
+# launch: that image's output is NaN). By default test() / fuse() / whiten_and_color() check it
+# one call late (ops.WCTStatusWatch: no host sync of their own, the error is raised at the
+# latest during the next call, or by WCTRPNet.check()); RPST_WCT_CHECK=1 checks right after
+# each launch instead (one host sync per call).
 CHECK_WCT = os.environ.get("RPST_WCT_CHECK", "0") == "1"
+_WATCH = weakref.WeakKeyDictionary()  # model -> ops.WCTStatusWatch (kept out of deepcopy)
 
 
-def wct_rp_fused(encoder, decoder, content, style):
+def _status(model, st, what):
+    if CHECK_WCT:
+        ops.check_wct_status(st, what)
+        return
+    w = _WATCH.get(model)
+    if w is None:
+        w = _WATCH[model] = ops.WCTStatusWatch()
+    w.push(st, what)
+
+
+def wct_rp_fused(encoder, decoder, content, style, model=None):
     """enc -> WCT -> dec (wct_rp.py:139-147) with the colour transform fused away: the
     encoder runs once over [content; style] and its last conv reduces the row means in its
     epilogue; the closed-form matrices T and c = mu_s - T mu_c come from rpst_wct_params
@@ -43,10 +57,12 @@ def wct_rp_fused(encoder, decoder, content, style):
     T, c, res, st = ops.wct_params(feats[:n], feats[n:], means=mean.reshape(2 * n, -1),
                                    status=True)
     out = plan.run(plan.compile_layers(decoder.children()), feats[:n], first_mix=(T, c))
-    # st: per-image status on the device; no host sync unless RPST_WCT_CHECK=1: an image whose
-    # iteration did not converge (non-finite features), or whose persistent launch timed out,
-    # has NaN T and c, so its output is NaN
-    if CHECK_WCT:
+    # st: per-image status on the device: an image whose iteration did not converge
+    # (non-finite features), or whose persistent launch timed out, has NaN T and c, so its
+    # output is NaN; checked after this call's launches are queued (_status)
+    if model is not None:
+        _status(model, st, "WCTRPNet.test")
+    elif CHECK_WCT:
         ops.check_wct_status(st, "WCTRPNet.test")
     return out
 
@@ -93,11 +109,16 @@ class WCTRPNet(BaseNet):
     def whiten_and_color(self, cF, sF, method='closed-form'):
         """cF, sF: (C, HW) fp64 device tensors -> (C, HW) fp64; method 'closed-form' (Lu et
         al., wct_rp.py:102-111) or 'original' (Li et al., :96-101)."""
-        if CHECK_WCT:
-            out, st = ops.whiten_and_color(cF, sF, method=method, status=True)
-            ops.check_wct_status(st, "WCTRPNet.whiten_and_color")
-            return out
-        return ops.whiten_and_color(cF, sF, method=method)
+        out, st = ops.whiten_and_color(cF, sF, method=method, status=True)
+        _status(self, st, "WCTRPNet.whiten_and_color")
+        return out
+
+    def check(self):
+        """Wait for the last WCT launch of this model and raise RuntimeError if any of its
+        images is invalid (the calls themselves raise one call late, see _status)."""
+        w = _WATCH.get(self)
+        if w is not None:
+            w.check()
 
     def encode_with_intermediate(self, input):
         results = [input]
@@ -122,7 +143,8 @@ class WCTRPNet(BaseNet):
         self.eval()
         with torch.no_grad():
             if type(self).fuse is WCTRPNet.fuse and FUSED_WCT:
-                stylized = wct_rp_fused(self.rp_shared_encoder, self.rp_decoder, content, style)
+                stylized = wct_rp_fused(self.rp_shared_encoder, self.rp_decoder, content, style,
+                                        model=self)
             else:
                 content_feat, style_feat = encode_both(self.rp_shared_encoder, content, style)
                 fusion_feat = self.fuse(content_feat, style_feat)
@@ -136,11 +158,9 @@ class WCTRPNet(BaseNet):
 
     def fuse(self, content_feats, style_feats):
         """Per-image closed-form WCT, all images of the batch in one set of launches."""
-        if CHECK_WCT:
-            out, st = ops.wct_fuse(content_feats, style_feats, status=True)
-            ops.check_wct_status(st, "WCTRPNet.fuse")
-            return out
-        return ops.wct_fuse(content_feats, style_feats)
+        out, st = ops.wct_fuse(content_feats, style_feats, status=True)
+        _status(self, st, "WCTRPNet.fuse")
+        return out
 
     def forward(self, content, style, alpha=1.0):
         """Loss dict of wct_rp.py:168-194. With autograd enabled and a trainable decoder

@@ -588,8 +588,9 @@ def whiten_and_color(cF: torch.Tensor, sF: torch.Tensor, method: str = 'closed-f
     """WCTRPNet.whiten_and_color (wct_rp.py:82-114): (C,HW) fp64 -> fp64. method
     'closed-form' (Lu et al., :102-111) or 'original' (Li et al., :96-101: matrix_sqrt(Cs)
     matrix_inv_sqrt(Cc) in the reference's SVD form). status=True also returns the (1,)
-    int32 device status word (rpst_whiten_and_color_status; always 0 for 'original', whose
-    Jacobi fallback recomputes any matrix Newton-Schulz could not take)."""
+    int32 device status word: rpst_whiten_and_color_status for 'closed-form'; for 'original'
+    (whose Jacobi fallback recomputes any matrix Newton-Schulz could not take) RPST_WCT_NOCONV
+    when the output is not finite (a device-side test, no host sync)."""
     assert cF.dim() == 2 and cF.shape == sF.shape
     assert method in ('closed-form', 'original'), method
     _check(cF, sF, dtype=torch.float64)
@@ -609,7 +610,7 @@ def whiten_and_color(cF: torch.Tensor, sF: torch.Tensor, method: str = 'closed-f
         return out
     st = torch.empty(1, device=cF.device, dtype=torch.int32)
     if method == 'original':
-        st.zero_()
+        st.copy_((~torch.isfinite(out)).any().reshape(1).to(torch.int32) * WCT_NOCONV)
     else:
         _lib.call("rpst_whiten_and_color_status", ws.data_ptr(), C, hw, st.data_ptr(),
                   _stream(cF))
@@ -631,6 +632,39 @@ def check_wct_status(status: torch.Tensor, what: str = "wct") -> None:
         why = {i: "+".join(w for f, w in ((WCT_TIMEOUT, "timeout"), (WCT_NOCONV, "no-convergence"))
                            if int(st[i]) & f) for i in bad}
         raise RuntimeError(f"{what}: invalid WCT matrices for images {why} (outputs are NaN)")
+
+
+class WCTStatusWatch:
+    """Deferred check of the WCT status words without a host sync per call (the
+    C side returns status codes and Python raises, no silent fallback). push() copies a call's
+    device status to pinned host memory behind an event on the launch stream, then checks the
+    PREVIOUS call's: that call's kernels were enqueued a whole call earlier, so the wait is
+    normally already over, and the GPU has this call's work queued meanwhile -- a failed image
+    raises RuntimeError at the latest during the following call. check() waits for and checks
+    the last pushed call (end of a run, tests)."""
+
+    def __init__(self):
+        self._pending = None
+
+    def push(self, status: torch.Tensor, what: str) -> None:
+        host = torch.empty(status.shape, dtype=status.dtype, pin_memory=True)
+        host.copy_(status, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(status.device))
+        prev, self._pending = self._pending, (host, ev, what)
+        if prev is not None:
+            self._check(prev)
+
+    def check(self) -> None:
+        prev, self._pending = self._pending, None
+        if prev is not None:
+            self._check(prev)
+
+    @staticmethod
+    def _check(p) -> None:
+        host, ev, what = p
+        ev.synchronize()
+        check_wct_status(host, what)
 
 
 def _wct_status(ws: torch.Tensor, n: int, C: int, hw: int, dev) -> torch.Tensor:

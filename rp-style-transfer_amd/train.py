@@ -188,16 +188,26 @@ def main(argv=None) -> int:
         content_images, style_images = next(loader)
         loss_dict, total_loss = network(content_images, style_images)
         total_loss.backward()
+        st = getattr(network, "_wct_status", None)
+        if st is not None:
+            # WCTRPNet: an image whose fp64 matrices failed (non-convergence, or a timed-out
+            # persistent launch) has a NaN feature and NaN gradients. Checked on EVERY rank
+            # BEFORE the gradient all-reduce and the Adam step: the per-rank flag is
+            # all-reduced (MAX), so either no rank applies the step and all raise together, or
+            # all go on -- a NaN never reaches another replica's parameters or the optimizer state
+            bad = (st != 0).any().to(torch.int32).reshape(1)
+            if world > 1:
+                dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+            if int(bad) != 0:
+                ops.check_wct_status(st, f"iteration {i} (rank {rank})")
+                raise RuntimeError(f"iteration {i}: invalid WCT matrices on another rank "
+                                   f"(step not applied)")
         if reduce_grads is not None:
             reduce_grads()
         optimizer.step()
         if rank != 0:
             continue
         scalars = {k: float(v.detach()) for k, v in loss_dict.items()}
-        if getattr(network, "_wct_status", None) is not None:
-            # WCTRPNet: an image whose fp64 matrices failed (non-convergence, or a timed-out
-            # persistent launch) would train on a NaN feature; surface it (the step is synced)
-            ops.check_wct_status(network._wct_status, f"iteration {i}")
         elapsed = round(time.time() - start, 2)
         log.write(json.dumps({"iteration": _begin(network) + i, "elapsed": elapsed,
                               **scalars}) + "\n")

@@ -45,8 +45,10 @@ def test_size_queries_are_host_only():
     assert lib.rpst_adain_workspace_size(2, 3) == 4 * 4 * 6
     # 3x3, Cin=3 -> one chunk of 8 channels, Cout=16 padded to 32 (direct image), then
     # the F(2x2) Winograd image: Cout padded to 32, 16 transformed taps per (co, ci), then
-    # the F(4x4) image: one (32-channel co tile, 8-channel chunk) slice of 36 taps
-    assert lib.rpst_conv2d_packed_size(16, 3, 3) == (1 * 9 * 8 * 32 + 32 * 8 * 16 + 36 * 32 * 8) * 4
+    # the F(4x4) image: one (32-channel co tile, 8-channel chunk) slice of 36 taps, then the
+    # position-quarter F(4x4) image: one (64-channel co tile, 4-channel K step) slice
+    assert lib.rpst_conv2d_packed_size(16, 3, 3) == (1 * 9 * 8 * 32 + 32 * 8 * 16 + 36 * 32 * 8 +
+                                                     36 * 64 * 4) * 4
     assert lib.rpst_conv2d_packed_size(16, 3, 1) == 1 * 16 * 32 * 4
     assert lib.rpst_conv2d_packed_size(16, 3, 2) == 0
 

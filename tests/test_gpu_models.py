@@ -374,6 +374,53 @@ def test_wct_barrier_timeout_is_nan_not_wrong(cuda, monkeypatch):
     assert st3.cpu().tolist() == [0] * n and torch.equal(T2, T0)
 
 
+def test_wct_rp_status_raises_without_check_env(cuda, monkeypatch):
+    """RPST_WCT_CHECK unset (the default): a WCTRPNet.test() whose persistent matrix launch
+    times out (RPST_MATFUN_DEBUG_SKIP) returns without a host sync of its own, and the
+    failure is raised at the latest by the next call (VERDICT r04 item 4, SURVEY §8(b));
+    WCTRPNet.check() raises it at once. Clean calls raise nothing."""
+    import network as net
+    from network import wct_rp
+    from rpst import synth
+    monkeypatch.setattr(wct_rp, "CHECK_WCT", False)
+    m = net.WCTRPNet(rp_config(8), copy.deepcopy(net.vgg))  # C = 128: four-workgroup groups
+    synth_(m, 7)
+    m = m.to(cuda)
+    c = torch.from_numpy(synth.image(7, (2, 3, 32, 48))).to(cuda)
+    s = torch.from_numpy(synth.image(8, (2, 3, 32, 48))).to(cuda)
+    clean = m.test(c, s)
+    m.test(c, s)
+    m.check()
+    monkeypatch.setenv("RPST_MATFUN_DEBUG_SKIP", "1")
+    bad = m.test(c, s)  # returns: the failure surfaces one call later
+    monkeypatch.delenv("RPST_MATFUN_DEBUG_SKIP")
+    with pytest.raises(RuntimeError, match="timeout"):
+        m.test(c, s)
+    m.check()  # that clean call's status: valid
+    assert torch.isnan(bad[0]).all() and torch.equal(m.test(c, s), clean)
+    monkeypatch.setenv("RPST_MATFUN_DEBUG_SKIP", "1")
+    m.test(c, s)
+    monkeypatch.delenv("RPST_MATFUN_DEBUG_SKIP")
+    with pytest.raises(RuntimeError, match="timeout"):
+        m.check()
+    m.check()  # nothing pending
+
+
+def test_whiten_and_color_original_status_nan_input(cuda):
+    """whiten_and_color(method='original', status=True) reports RPST_WCT_NOCONV when its
+    output is not finite (a NaN feature), and 0 on a clean input."""
+    from rpst import ops
+    cf = gen(65, (64, 300), 1.0, 0.3, relu=True).double().to(cuda)
+    sf = gen(66, (64, 300), 1.2, 0.2, relu=True).double().to(cuda)
+    out, st = ops.whiten_and_color(cf, sf, method='original', status=True)
+    assert st.cpu().tolist() == [0] and torch.isfinite(out).all()
+    cf[3, 7] = float("nan")
+    out, st = ops.whiten_and_color(cf, sf, method='original', status=True)
+    assert st.cpu().tolist() == [ops.WCT_NOCONV]
+    with pytest.raises(RuntimeError, match="no-convergence"):
+        ops.check_wct_status(st)
+
+
 def test_wct_large_mean_features(cuda):
     """Features with a large mean and a small spread (mean 1e3, std ~0.6): the fused path
     centres on the fp32 means the encoder epilogue hands over and recovers the fp64 means
