@@ -200,8 +200,9 @@ int rpst_conv2d_algorithm(int Cout, int Cin, int Hs, int Ws, int ksize, int in_o
 /* Precise mode for the CALLING THREAD (host-only): while on, the default choice never picks
  * F(4x4,3x3) (its fp32 rounding, ~1e-6 per conv, compounds through the ~30 convolutions of
  * a training step's backward chain); F(2x2) runs instead. Returns the previous setting.
- * The training autograd path (rpst/autograd.py) turns it on; an explicit
- * RPST_CONV_ALGO still wins. */
+ * on = 2: F(4x4) allowed, on its 32-channel form only (not the position-quarter kernel):
+ * a training step's constant branches. The training autograd path (rpst/autograd.py)
+ * sets it; an explicit RPST_CONV_ALGO still wins. */
 int rpst_conv2d_set_precise(int on);
 
 /* ---- stand-alone pool / upsample (same semantics as the conv input operators) ----- */

@@ -277,6 +277,8 @@ int wino4_mix(ConvArgs& a, const double* T, const double* cvec, const float* dir
 // weight image follows the F(4x4) one in the packed buffer; wino4_launch / wino4_fold /
 // wino4_mix dispatch to it for the layers wino4q_applies to.
 bool wino4q_applies(int Cin, int Cout, int in_op);
+// false while the calling thread is at precise level 2 (rpst_conv.hip)
+bool conv_quarter_allowed();
 size_t wino4q_packed_floats(int Cout, int Cin);
 int wino4q_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);
 int wino4q_pack_mix(const double* wm, float* pk, int N, int Cout, int Cin, hipStream_t st);

@@ -608,8 +608,11 @@ static int conv_variant(int BM, int ksize, int in_op) {
 // operators it implements, F(2x2,3x3) (rpst_wino.hip) for the others, the direct implicit
 // GEMM for the 16-wide layers and every 1x1. RPST_CONV_ALGO=direct|winograd|winograd4
 // overrides (tests, A/B benches; winograd4 falls back to winograd where unsupported).
-// rpst_conv2d_set_precise: this thread's launches keep to F(2x2) where F(4x4) would run
+// rpst_conv2d_set_precise: at 1 this thread's launches keep to F(2x2) where F(4x4) would
+// run; at 2 F(4x4) runs, on its 32-channel form only (wino4q_applies)
 static thread_local int t_conv_precise = 0;
+
+bool conv_quarter_allowed() { return t_conv_precise != 2; }
 
 static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
   if (ksize != 3) return RPST_CONV_DIRECT;
@@ -631,9 +634,9 @@ static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
   // 1.59 direct and 2.49 on the VALU kernel (tools/bench_conv.py); other inputs below 16
   // channels, and precise mode, stay direct
   if (nr) return RPST_CONV_NARROW;
-  if (Cin <= 4 && w4 && !t_conv_precise) return RPST_CONV_WINOGRAD4;
+  if (Cin <= 4 && w4 && t_conv_precise != 1) return RPST_CONV_WINOGRAD4;
   if (Cin < 16) return RPST_CONV_DIRECT;
-  if (w4 && !t_conv_precise) return RPST_CONV_WINOGRAD4;
+  if (w4 && t_conv_precise != 1) return RPST_CONV_WINOGRAD4;
   if (w4) return RPST_CONV_WINOGRAD;  // precise mode, same shapes as F(4x4)
   return Cout >= 32 ? RPST_CONV_WINOGRAD : RPST_CONV_DIRECT;
 }
@@ -755,7 +758,7 @@ extern "C" int64_t rpst_conv2d_grid_threads(int N, int Cin, int Hs, int Ws, int 
 
 extern "C" int rpst_conv2d_set_precise(int on) {
   const int old = t_conv_precise;
-  t_conv_precise = on != 0;
+  t_conv_precise = on == 2 ? 2 : on != 0;
   return old;
 }
 

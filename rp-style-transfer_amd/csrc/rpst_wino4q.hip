@@ -20,8 +20,8 @@
 // positions x 4 ci = 36 KiB) and the patch (4 channels x 10 rows x 68) stream into a 3-stage
 // LDS ring by LDS-DMA: W(x + 2) and P(x + 3) are issued inside step x. The four quarters of
 // a tile row meet in the epilogue: each wave sends its 9 positions of the other three
-// quarters' 16-channel blocks through the consumed weight stage (6 passes of 2 accumulator
-// elements x 3 positions) and finishes its own block with the full output transform.
+// quarters' 16-channel blocks through a weight stage (6 passes of 2 accumulator elements x 3
+// positions) and finishes its own block with the full output transform.
 #include "rpst_conv.h"
 
 #include <type_traits>
@@ -93,6 +93,25 @@ __device__ __forceinline__ void q_mfma(floatx4& acc, float a, float b) {
   else
     asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
 }
+// LDS-DMA issue (buffer_load ... lds) as inline asm, M0 written in the same statement
+// (cdna_hip_programming.md 5.7): the compiler then tracks none of the ring's DMA, so it inserts
+// no vmcnt of its own before the ring's LDS reads (its alias analysis cannot separate the
+// padding pieces' dummy target from the stages and drained the ring to vmcnt(1) after every
+// barrier); the ring's waits are the counted ones of wait_ring. "memory": no LDS access of
+// the compiler's moves across an issue.
+__device__ __forceinline__ unsigned q_lds_addr(const float* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
+}
+__device__ __forceinline__ void q_dma16(__amdgpu_buffer_rsrc_t r, const float* lds, unsigned voff,
+                                        int soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :: "s"(q_lds_addr(lds)), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
+__device__ __forceinline__ void q_dma4(__amdgpu_buffer_rsrc_t r, const float* lds, unsigned voff,
+                                       int soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %3 offen lds"
+               :: "s"(q_lds_addr(lds)), "v"(voff), "s"(r), "s"(soff) : "memory");
+}
 __device__ __forceinline__ void q_lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -128,7 +147,13 @@ constexpr int kQNTH = 512;
 constexpr int kQWPI = 5;                     // 1-KiB weight pieces per wave and step (36 / 8)
 constexpr int kQWide = 2, kQSlow = 6;        // patch pieces per wave and step: 16-B / 4-B
 constexpr int kQDMA4 = 3, kQDMA = 11;        // patch pieces per channel: 16-B / 4-B
-constexpr int kQXS = 4 * 3 * 3 * 64 * 2;     // epilogue exchange floats per tile row (2 halves)
+constexpr int kQXS = 4 * 3 * 3 * 64 * 2;     // epilogue exchange floats per tile row and pass
+// timing-only experiments (results wrong; tools/build_variants.sh -DRPST_W4Q_DBG=n): 1 no patch
+// DMA, 2 no weight DMA, 4 no epilogue exchange, 8 no input transform, 16 no step barriers,
+// 32 no epilogue at all, 128 no DMA waits
+#ifndef RPST_W4Q_DBG
+#define RPST_W4Q_DBG 0
+#endif
 #ifndef RPST_W4Q_AHEAD
 #define RPST_W4Q_AHEAD 2                     // MFMA groups whose A operands are read ahead
 #endif
@@ -233,17 +258,22 @@ int wino4q_fold_w(const float* pk, float* out, const float* aux, int N, int Cout
 }
 
 // the layers this kernel takes: DMA loaders (NONE, UPSAMPLE2), >= 64 output channels (a
-// 64-channel co tile; narrower layers stay on rpst_wino4.hip's 32-channel tile) and >= 16
-// input channels in multiples of 16 (a co tile = a whole number of 4-step ring turns; the
-// 3-channel first convs keep the old kernel). RPST_W4Q=1 turns it on (default off until
-// measured on the GPU).
+// 64-channel co tile; narrower layers stay on rpst_wino4.hip's 32-channel tile) and >= 128
+// input channels in multiples of 16 (a co tile = a whole number of 4-step ring turns).
+// Below 128 input channels a block's 8-16 K steps per co tile leave the prologue and the
+// 4-way epilogue exposed: 32->64 @512^2 N64 3.12 vs 2.54 ms, 64->128 8.16 vs 8.09 on the
+// 32-channel kernel (gpurun_out/w4q_d, profiles/r05). RPST_W4Q=0 turns it off, =2 forces it
+// on for every shape it supports (Cin >= 16; tests, A/B). A training step's constant
+// branches (rpst_conv2d_set_precise(2)) keep the 32-channel form: same per-conv error
+// (tools/conv_err.py), but the gradient goldens were pinned on its rounding pattern.
 bool wino4q_applies(int Cin, int Cout, int in_op) {
   static const int en = [] {
     const char* e = getenv("RPST_W4Q");
-    return (e && *e) ? atoi(e) : 0;
+    return (e && *e) ? atoi(e) : 1;
   }();
-  return en && (in_op == RPST_IN_NONE || in_op == RPST_IN_UPSAMPLE2) && Cout >= 64 && Cin >= 16 &&
-         Cin % 16 == 0;
+  const int min_cin = en == 2 ? 16 : 128;
+  return en && conv_quarter_allowed() && (in_op == RPST_IN_NONE || in_op == RPST_IN_UPSAMPLE2) && Cout >= 64 &&
+         Cin >= min_cin && Cin % 16 == 0;
 }
 
 // ---- the epilogue of one finished 4x4 tile and channel ---------------------------------
@@ -526,24 +556,25 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
   // weight slice of step g (the block's co tiles' slices are consecutive) into stage stg:
   // pieces w + 8 i of its 36 1-KiB pieces; pieces 32-35 come from waves 0-3, waves 4-7 issue
   // a padding piece into the dummy. Dead steps (g >= G) read zero records.
+  constexpr int DBG = RPST_W4Q_DBG;
   auto issue_w = [&](int g, float* stg, int i) {
+    if (DBG & 2) return;
     const int wv = q_launder(wave);
     const int pc = wv + 8 * i;
     const bool live = g < G;
     const int so = q_mask((g * kQWS + pc * 256) * 4, live);
     if (i < 4) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(q_rsrc(w_img, wbytes, live),
-                                               (q_lds_t)(stg + pc * 256), 16, lane * 16, so, 0, 0);
+      q_dma16(q_rsrc(w_img, wbytes, live), stg + pc * 256, lane * 16, so);
     } else {
       const bool real = pc < 36;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(q_rsrc(w_img, wbytes, live && real),
-                                               (q_lds_t)(real ? stg + pc * 256 : dummy), 16,
-                                               lane * 16, q_mask(so, real), 0, 0);
+      q_dma16(q_rsrc(w_img, wbytes, live && real), real ? stg + pc * 256 : dummy, lane * 16,
+              q_mask(so, real));
     }
   };
   // every patch piece of this wave for step g (K step ks) into stage stg
   auto issue_p = [&](auto WIDEc, int g, int ks, float* stg) {
     constexpr bool WIDE = decltype(WIDEc)::value;
+    if (DBG & 1) return;
     const int wv = q_launder(wave);
     const int c = 4 * ks + (wv >> 1);
     const bool ok = g < G && c < a.Cin;
@@ -552,22 +583,19 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     float* xs = stg + (wv >> 1) * kQCS;
     const bool h1 = (wv & 1) != 0;
     if constexpr (WIDE) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (q_lds_t)(xs + (h1 ? 512 : 0)), 16,
-                                               (int)poffs[0][tid], so, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (q_lds_t)(h1 ? dummy : xs + 256), 16,
-                                               (int)poffs[1][tid], so, 0, 0);
+      q_dma16(r, xs + (h1 ? 512 : 0), poffs[0][tid], so);
+      q_dma16(r, h1 ? dummy : xs + 256, poffs[1][tid], so);
     } else {
 #pragma unroll
       for (int i = 0; i < kQSlow - 1; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (q_lds_t)(xs + 64 * (h1 ? kQSlow + i : i)), 4,
-                                                 (int)poffs[i][tid], so, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (q_lds_t)(h1 ? dummy : xs + 64 * (kQSlow - 1)),
-                                               4, (int)poffs[kQSlow - 1][tid], so, 0, 0);
+        q_dma4(r, xs + 64 * (h1 ? kQSlow + i : i), poffs[i][tid], so);
+      q_dma4(r, h1 ? dummy : xs + 64 * (kQSlow - 1), poffs[kQSlow - 1][tid], so);
     }
   };
   // before step x's barrier: W(x) (issued in step x - 1 ahead of its patch group) and
   // everything older have landed; that youngest patch group (2 / 6 pieces) stays in flight
   auto wait_ring = [&]() {
+    if (DBG & 128) return;
     if (wide) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   };
@@ -606,12 +634,20 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     };
     // column pass of one row (this quarter's 3 transformed columns)
     auto col_pass = [&](const float (&d)[8], float (&u)[3]) {
+      if (DBG & 8) {
+        u[0] = d[0]; u[1] = d[1]; u[2] = d[2];
+        return;
+      }
       q_bt3<QC>(d[0], d[1], d[2], d[3], d[4], d[5], u[0], u[1], u[2]);
     };
     // row pass of column j: u[rr] holds input row QR + rr, so QR = 1's half (inputs 1..5)
     // takes u[0..4] as its inputs 1..5. V[p], p = 3 i + j: transformed row 3 QR + i,
     // column 3 QC + j
     auto row_pass = [&](const float (&u)[5][3], int j, float (&v)[9]) {
+      if (DBG & 8) {
+        v[j] = u[0][j]; v[3 + j] = u[2][j]; v[6 + j] = u[4][j];
+        return;
+      }
       if constexpr (QR == 0)
         q_bt3<0>(u[0][j], u[1][j], u[2][j], u[3][j], u[4][j], 0.f, v[j], v[3 + j], v[6 + j]);
       else
@@ -637,7 +673,8 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     // column j overwrites V[j], V[3 + j], V[6 + j] after their last use.
     auto step = [&](float* wsx, float* psn, float* wsn, float* psx, int ks) {
       wait_ring();
-      q_lds_barrier();  // W(x), P(x + 1) complete; every wave is done with step x - 1
+      if (DBG & 16) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else q_lds_barrier();  // W(x), P(x + 1) complete; every wave is done with step x - 1
       constexpr int ord[9] = {0, 3, 6, 1, 4, 7, 2, 5, 8};
       constexpr int kA = RPST_W4Q_AHEAD;  // A-operand groups read ahead
       float4 w4[9];
@@ -657,10 +694,11 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
         q_mfma<0>(acc[p][2], w4[p].z, V[p]);
         q_mfma<0>(acc[p][3], w4[p].w, V[p]);
         if (q < kQWPI) issue_w(x + 1, wsn, q);
-        // (K step of P(x + 4) = ks of this step: K4 is a multiple of 4)
+        // P(x + 4): K step ks + 4 of this co tile, or of the next one
         if (q == 5) {
-          if (wide) issue_p(std::true_type{}, x + 4, ks, psx);
-          else issue_p(std::false_type{}, x + 4, ks, psx);
+          const int k4 = ks + 4 < K4 ? ks + 4 : ks + 4 - K4;
+          if (wide) issue_p(std::true_type{}, x + 4, k4, psx);
+          else issue_p(std::false_type{}, x + 4, k4, psx);
         }
         // pipelined transform of P(x + 1): rows at groups 0-4, column j's row pass at
         // groups 5, 6 and (after its MFMAs) 8
@@ -692,6 +730,19 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
         return;
       }
 #endif
+      if (DBG & 32) {  // keep the accumulators live, skip the epilogue
+        float t = 0.f;
+#pragma unroll
+        for (int p = 0; p < 9; ++p)
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) t += acc[p][cb][0];
+        if (t == 1.2345f) q_args()->out[threadIdx.x] = t;
+#pragma unroll
+        for (int p = 0; p < 9; ++p)
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) acc[p][cb] = floatx4{0.f, 0.f, 0.f, 0.f};
+        return;
+      }
       q_lds_barrier();  // every wave is done reading ws1
       // 12 wait states between the last MFMAs and the first reader of their results (8-pass
       // XDL), with every accumulator passed through the statements so no read moves above them
@@ -706,63 +757,78 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
                    "+v"(acc[7][2]), "+v"(acc[7][3]), "+v"(acc[8][0]), "+v"(acc[8][1]),
                    "+v"(acc[8][2]), "+v"(acc[8][3]));
       const int co0 = ctile * kQCo + 16 * Q + 4 * k;
-      // 12 passes (accumulator element r, position row pt): each wave writes its 3 positions
-      // of row pt of the other quarters' blocks (element r) into one half of ws1 (the halves
-      // alternate, so one barrier per pass suffices) and reads the other quarters' positions
-      // of its own block. After pass pt it holds transformed rows pt and 3 + pt of M for its
-      // channel co0 + r: their column transform (A^T along the row) runs at once, so only
-      // P = M A (6 x 4) stays live, never M.
+      // 6 passes (accumulator element pair rp, position row pt): each wave writes its 3
+      // positions of row pt of the other quarters' blocks (elements 2 rp, 2 rp + 1) into ws1
+      // and, after a barrier, reads the other quarters' positions of its own block. After pass pt it holds transformed rows
+      // pt and 3 + pt of M for channels co0 + 2 rp + {0, 1}: their column transform (A^T along
+      // the row) runs at once, so only P = M A (6 x 4 per channel) stays live, never M.
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float P[6][4];
+      for (int rp = 0; rp < 2; ++rp) {
+        float P[2][6][4];
 #pragma unroll
         for (int pt = 0; pt < 3; ++pt) {
-          float* xb = ws1 + ((r * 3 + pt) & 1) * (kQWS / 2) + wr * (kQXS / 2);
+          float* xb = ws1 + wr * kQXS;
 #pragma unroll
           for (int dq = 0; dq < 4; ++dq) {
-            if (dq == Q) continue;
+            if (dq == Q || (DBG & 4)) continue;
             const int slot = (Q - dq - 1) & 3;
 #pragma unroll
             for (int j = 0; j < 3; ++j)
-              xb[((dq * 3 + slot) * 3 + j) * 64 + lane] = acc[3 * pt + j][dq][r];
+              *reinterpret_cast<float2*>(xb + (((dq * 3 + slot) * 3 + j) * 64 + lane) * 2) =
+                  make_float2(acc[3 * pt + j][dq][2 * rp], acc[3 * pt + j][dq][2 * rp + 1]);
           }
-          q_lds_barrier();
-          float m[2][6];  // transformed rows pt (m[0]) and 3 + pt (m[1]), all six columns
+          if (!(DBG & 4)) q_lds_barrier();
+          float m[2][2][6];  // [element][row pt / 3 + pt][six columns]
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
-              const float v = s == Q ? acc[3 * pt + j][Q][r]
-                                     : xb[((Q * 3 + ((s - Q - 1) & 3)) * 3 + j) * 64 + lane];
-              m[s >> 1][3 * (s & 1) + j] = v;
+              float2 v;
+              if (s == Q || (DBG & 4)) {
+                const int src = (DBG & 4) ? s : Q;
+                v = make_float2(acc[3 * pt + j][src][2 * rp], acc[3 * pt + j][src][2 * rp + 1]);
+              } else {
+                v = *reinterpret_cast<const float2*>(
+                    xb + (((Q * 3 + ((s - Q - 1) & 3)) * 3 + j) * 64 + lane) * 2);
+              }
+              m[0][s >> 1][3 * (s & 1) + j] = v.x;
+              m[1][s >> 1][3 * (s & 1) + j] = v.y;
             }
           }
-          q_at6(m[0], P[pt]);
-          q_at6(m[1], P[3 + pt]);
-        }
-        // the epilogue context is re-derived per channel from the kernel arguments: kept
-        // across the exchange passes it overflows the scalar registers
-        const QEpi e = q_epi_ctx(wr, tn);
-        float bias = 0.f;
-        {
-          const int co = co0 + r;
-          const float* bp = BTAB ? nullptr : q_args()->bias;
-          if (co < e.Cout)
-            bias = BTAB ? e.btab[((int64_t)e.n * e.Cout + co) * 9 + 4] : (bp ? bp[co] : 0.f);
+#pragma unroll
+          for (int e2 = 0; e2 < 2; ++e2) {
+            q_at6(m[e2][0], P[e2][pt]);
+            q_at6(m[e2][1], P[e2][3 + pt]);
+          }
+          if (!(DBG & 4) && (rp == 0 || pt < 2)) q_lds_barrier();  // the next pass rewrites ws1
         }
 #pragma unroll
-        for (int x = 0; x < 4; ++x) P[1][x] += bias;
-        float Y[16];
+        for (int e2 = 0; e2 < 2; ++e2) {
+          const int r = 2 * rp + e2;
+          // the epilogue context is re-derived per channel from the kernel arguments: kept
+          // across the exchange passes it overflows the scalar registers
+          const QEpi e = q_epi_ctx(wr, tn);
+          float bias = 0.f;
+          {
+            const int co = co0 + r;
+            const float* bp = BTAB ? nullptr : q_args()->bias;
+            if (co < e.Cout)
+              bias = BTAB ? e.btab[((int64_t)e.n * e.Cout + co) * 9 + 4] : (bp ? bp[co] : 0.f);
+          }
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          float c6[6], y[4];
+          for (int x = 0; x < 4; ++x) P[e2][1][x] += bias;
+          float Y[16];
 #pragma unroll
-          for (int I = 0; I < 6; ++I) c6[I] = P[I][x];
-          q_at6(c6, y);
+          for (int x = 0; x < 4; ++x) {
+            float c6[6], y[4];
 #pragma unroll
-          for (int yy = 0; yy < 4; ++yy) Y[yy * 4 + x] = y[yy];
+            for (int I = 0; I < 6; ++I) c6[I] = P[e2][I][x];
+            q_at6(c6, y);
+#pragma unroll
+            for (int yy = 0; yy < 4; ++yy) Y[yy * 4 + x] = y[yy];
+          }
+          q_finish<STATS, BTAB, RELU>(e, co0 + r, Y, tn);
         }
-        q_finish<STATS, BTAB, RELU>(e, co0 + r, Y, tn);
       }
 #pragma unroll
       for (int p = 0; p < 9; ++p)
@@ -814,9 +880,10 @@ int wino4q_launch(ConvArgs& a, int in_op, hipStream_t st) {
                "conv2d: winograd4 weight image exceeds 2 GiB");
   {
     // blocks per spatial tile: the co tiles split over RPST_W4Q_COSPLIT same-XCD blocks
-    // (default: 2 once there are >= 4 co tiles and >= 32 K steps)
+    // (default 1: 128->256 @512^2 N64 27.08 / 27.70 / 29.04 ms at 1 / 2 / 4 blocks, the longer
+    // blocks amortise the ring's prologue; gpurun_out/w4q_cs)
     const char* e = getenv("RPST_W4Q_COSPLIT");
-    int c = (e && *e) ? atoi(e) : (a.nchunks >= 32 && a.co_tiles >= 4 ? 2 : 1);
+    int c = (e && *e) ? atoi(e) : 1;
     c = c < 1 ? 1 : (c > a.co_tiles ? a.co_tiles : c);
     while (a.co_tiles % c) --c;
     a.cosplit = c;

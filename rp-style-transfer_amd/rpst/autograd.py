@@ -637,7 +637,7 @@ class _SAModelStep(torch.autograd.Function):
         x = torch.cat([style, content], dim=0)
         f4 = int(os.environ.get("RPST_SAM_F4_SLICES", SAM_F4_SLICES))
         for i in range(5):
-            with ops.precise_convs(on=None if i >= f4 else False):
+            with ops.precise_convs("sanet", on=None if i >= f4 else False):
                 x = getattr(model, f"enc_{i + 1}")(x)
             feats.append(x)
         sf = [f[:n].contiguous() for f in feats]

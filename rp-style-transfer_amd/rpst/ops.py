@@ -197,7 +197,10 @@ def _conv_name(ksize, cin, cout, hs, ws, n, in_op):
 # encoder + WCT, the frozen VGG features of SourceNet. SAModel's frozen VGG features stay
 # precise: they feed the differentiated attention transforms, and on F(4x4) a
 # sanet5_1.h.weight gradient moves 1.06e-4 against its 1e-4 bar (profiles/r04g). TRAIN_F4
-# opts a whole step in.
+# opts a whole step in. Where a training step runs F(4x4) it runs the 32-channel form
+# (rpst_conv2d_set_precise(2)), not the round-5 position-quarter kernel: the per-conv error
+# is the same (tools/conv_err.py), but SourceNet's frozen-VGG gradient probe, pinned on the
+# 32-channel rounding, reads 2.9e-4 against 1e-4 on the quarter kernel (6.1e-5 on its own).
 TRAIN_F4 = {"adain": False, "multiscale": False, "wct": False, "sanet": False, "source": False}
 
 
@@ -206,7 +209,8 @@ class precise_convs:
     include/rpst.h) — used by the training steps, whose gradients pass ~30 convolutions.
     `model`: the step's network family (TRAIN_F4); on=False: a constant (not differentiated)
     branch of the step, where F(4x4) is allowed. RPST_TRAIN_PRECISE=1 / 0 forces precise /
-    F(4x4) everywhere (accuracy A/B)."""
+    F(4x4) everywhere (accuracy A/B). F(4x4) inside a training step is level 2 of the C
+    switch: the 32-channel kernel only."""
 
     def __init__(self, model: Optional[str] = None, on: Optional[bool] = None):
         self.model, self.on = model, on
@@ -219,7 +223,7 @@ class precise_convs:
             on = self.on
         else:
             on = not TRAIN_F4.get(self.model, False)
-        self._old = _lib.load().rpst_conv2d_set_precise(int(on))
+        self._old = _lib.load().rpst_conv2d_set_precise(1 if on else 2)
         return self
 
     def __exit__(self, *exc):

@@ -151,6 +151,12 @@ def test_conv_algorithm_choice_is_host_only(monkeypatch):
         assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == W2
     finally:
         lib.rpst_conv2d_set_precise(old)
+    old = lib.rpst_conv2d_set_precise(2)   # training constant branch: F(4x4), 32-channel form
+    try:
+        assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == W4
+        assert lib.rpst_conv2d_set_precise(2) == 2
+    finally:
+        lib.rpst_conv2d_set_precise(old)
     assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == W4
     monkeypatch.setenv("RPST_CONV_ALGO", "direct")
     assert lib.rpst_conv2d_algorithm(256, 128, 512, 512, 3, 0) == D

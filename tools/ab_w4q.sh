@@ -7,7 +7,7 @@ O=$R/gpurun_out/${1:-w4q}
 L=${2:-adain}
 mkdir -p $O
 cd $R
-RPST_W4Q=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q -k "conv" --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+RPST_W4Q=2 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q -k "conv" --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for rep in 1 2; do
   for q in 1 0; do

@@ -7,7 +7,7 @@ SRC=$1; shift
 C=rp-style-transfer_amd/csrc
 OBJ=build/${SRC%.hip}.o
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function"
-case $SRC in rpst_wino4.hip) FLAGS="$FLAGS -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form=1";; rpst_flash.hip) FLAGS="$FLAGS -mllvm -amdgpu-mfma-vgpr-form=1";; esac
+case $SRC in rpst_wino4.hip|rpst_wino4q.hip) FLAGS="$FLAGS -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form=1";; rpst_flash.hip) FLAGS="$FLAGS -mllvm -amdgpu-mfma-vgpr-form=1";; esac
 for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}
   mkdir -p var/$name

@@ -21,7 +21,7 @@ import glob
 import json
 import sys
 
-CONV_MAIN = ("wino4_mfma_kernel", "wino_mfma_kernel", "conv_mfma_kernel", "conv3x3_narrow_kernel")
+CONV_MAIN = ("wino4_mfma_kernel", "wino4q_mfma_kernel", "wino_mfma_kernel", "conv_mfma_kernel", "conv3x3_narrow_kernel")
 
 
 def load(d):
