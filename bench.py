@@ -522,9 +522,22 @@ def run_workload(kind, size, batch, gbatch, gather, micro, steps, warmup, world,
                         out.record_stream(copy_stream)
             return out
 
+    # the WCT launch's covariance / matrix-function split, from HIP events armed for the
+    # warm-up steps only (rpst_wct_phase_timing): the timed region records nothing extra
+    phases = None
+    arm = cuda and kind == "wct" and warmup > 0
+    if arm:
+        from rpst import _lib
+        _lib.load().rpst_wct_phase_timing(1)
     for _ in range(warmup):
         out = step()
     sync()
+    if arm:
+        import ctypes
+        cov_ms, mat_ms = ctypes.c_float(), ctypes.c_float()
+        _lib.load().rpst_wct_phase_timing(0)
+        _lib.call("rpst_wct_phase_ms", ctypes.byref(cov_ms), ctypes.byref(mat_ms))
+        phases = (cov_ms.value, mat_ms.value)
 
     ops.TRACE = ops.Trace() if cuda else None
     if world > 1:
@@ -577,7 +590,7 @@ def run_workload(kind, size, batch, gbatch, gather, micro, steps, warmup, world,
         torch.cuda.empty_cache()
     return {"value": total * steps / dt, "dt": dt, "per_rank": per_rank, "summary": summary,
             "order": order, "B": B, "total": total, "scaling": scaling, "mb": mb,
-            "host": host_rec, "steps": steps, "warmup": warmup}
+            "host": host_rec, "steps": steps, "warmup": warmup, "wct_phases": phases}
 
 
 def stack_roofline(summary, steps, dt):
@@ -603,22 +616,34 @@ def stack_roofline(summary, steps, dt):
             "conv_share_of_step": round(conv_ms / steps / (1e3 * step_s), 4)}
 
 
-def wct_roofline(summary):
-    """fp64 rate of rpst_wct_params (covariances + matrix functions, wct_rp.py:82-109) on the
-    covariance FLOPs alone against the fp64 MFMA peak; the launch is bound by the fp64 MFMA
-    (SURVEY §8(d) config #3). The covariances are symmetric, so their algorithmic count is the
-    SYRK one, 2 x C (C + 1) HW per image (one triangle each of cF cF^T and sF sF^T; the
-    reference's full products are 2 x 2 C^2 HW); the Newton-Schulz products are not counted."""
+def wct_roofline(summary, phases=None):
+    """fp64 rate of rpst_wct_params (covariances + matrix functions, wct_rp.py:82-109)
+    against the fp64 MFMA peak (78.6 TF/s; tools/mfma_peak.bin sustains 77.9 on a tied
+    in-place 16x16x4 loop, profiles/r05/mfma_peak.log). The covariances are symmetric, so
+    their algorithmic count is the SYRK one, 2 x C (C + 1) HW per image (one triangle each of
+    cF cF^T and sF sF^T; the reference's full products are 2 x 2 C^2 HW); the Newton-Schulz
+    products are not counted. Two numbers: "covariance" = those FLOPs
+    over the covariance phase alone (HIP events of the warm-up calls, `phases`), and the
+    matrix-function launch's milliseconds beside it; achieved / frac stay the whole-launch
+    rate on the covariance count."""
     for name, a in summary.items():
         if name.startswith("wct_params"):
             avg_ms = a["ms"] / a["launches"]
             tf = a["flops"] / (avg_ms * 1e-3) / 1e12
-            return {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP64_TFLOPS,
-                    "unit": "TFLOP/s (fp64)", "frac": round(tf / PEAK_FP64_TFLOPS, 4),
-                    "kernel": f"cov_syrk16_kernel + matfun_kernel [{name}]",
-                    "launch_ms": round(avg_ms, 4), "flop_per_launch": a["flops"],
-                    "traffic": pmc_lookup("wct", name, PMC_CONFIG.get(2)),
-                    "flop_basis": "covariances (SYRK) 2 x C (C + 1) HW per image"}
+            rec = {"bound": "mfma", "achieved": round(tf, 2), "peak": PEAK_FP64_TFLOPS,
+                   "unit": "TFLOP/s (fp64)", "frac": round(tf / PEAK_FP64_TFLOPS, 4),
+                   "kernel": f"cov_syrk16_kernel + matfun_kernel [{name}]",
+                   "launch_ms": round(avg_ms, 4), "flop_per_launch": a["flops"],
+                   "traffic": pmc_lookup("wct", name, PMC_CONFIG.get(2)),
+                   "flop_basis": "covariances (SYRK) 2 x C (C + 1) HW per image"}
+            if phases:
+                cov_ms, mat_ms = phases
+                ctf = a["flops"] / (cov_ms * 1e-3) / 1e12
+                rec["covariance"] = {"ms": round(cov_ms, 4), "achieved": round(ctf, 2),
+                                     "frac": round(ctf / PEAK_FP64_TFLOPS, 4),
+                                     "source": "HIP events around the phase, warm-up calls"}
+                rec["matfun_ms"] = round(mat_ms, 4)
+            return rec
     return None
 
 
@@ -634,7 +659,7 @@ def sub_record(cfg_index, meas, kind, size, world, steps, with_cpu):
            "kernel_ms_per_step": {k: round(v["ms"] / steps, 3) for k, v in sorted(
                meas["summary"].items(), key=lambda kv: -kv[1]["ms"])[:8]}}
     if kind == "wct":
-        rec["roofline_wct"] = wct_roofline(meas["summary"])
+        rec["roofline_wct"] = wct_roofline(meas["summary"], meas.get("wct_phases"))
     if meas["host"] is not None:
         rec["host_gather"] = meas["host"]
     if kind == "sanet":
@@ -773,7 +798,7 @@ def main():
             rec["roofline"] = roofline_from_trace(summary, PMC_CONFIG.get(cfg_i))
             rec["roofline_stack"] = stack_roofline(summary, args.steps, dt)
             if model_kind == "wct":
-                rec["roofline_wct"] = wct_roofline(summary)
+                rec["roofline_wct"] = wct_roofline(summary, meas.get("wct_phases"))
             adain_summary = measure_adain_standalone(dev, min(meas["B"], 32), 256,
                                                      min(size, 512) ** 2)
             rec["roofline_adain"] = adain_roofline(

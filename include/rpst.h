@@ -252,9 +252,12 @@ int rpst_aea_clamp(const float* x, const float* fx, const float* w1, const float
 
 /* AdaptiveSANet attention core (sanet.py:106-124): with S = F^T G and P = softmax_rows(S),
  * O[b] = H[b] Q^T with Q = AEA(cal_affinity_matrix(content, style), P) as rpst_aea_clamp
- * (mode/scale/from/interval). P and Q are formed while S is staged into the second GEMM and
- * are never stored unless claim_before / claim_after (B, HW, HW) are non-null;
- * claim_value (B, HW) receives the clamp values when non-null.
+ * (mode/scale/from/interval). For C in {64, 128, 256, 512} and HW % 4 == 0 S is never
+ * stored: a flash pass forms each query's softmax statistics, a second recomputes S per key
+ * block and applies P and Q in registers (no B x HW x HW workspace); other shapes form S in
+ * the workspace and apply P and Q while staging it into the second GEMM. claim_before /
+ * claim_after (B, HW, HW) are written only when non-null; claim_value (B, HW) receives the
+ * clamp values when non-null.
  * Workspace: rpst_adaptive_attention_workspace_size(B, C, HW, hidden). */
 size_t rpst_adaptive_attention_workspace_size(int B, int C, int HW, int hidden);
 int rpst_adaptive_attention(const float* F, const float* G, const float* H,
@@ -471,6 +474,13 @@ int rpst_wct_status(const void* workspace, int n, int C, int64_t HW, int* status
                     rpst_stream_t stream);
 int rpst_whiten_and_color_status(const void* workspace, int C, int64_t HW, int* status,
                                  rpst_stream_t stream);
+
+/* Measurement (bench.py): while armed (rpst_wct_phase_timing(1); returns the previous
+ * setting), rpst_wct_params / rpst_wct_fuse record HIP events around their covariance phase
+ * (means + SYRK + reduce) and their matrix-function launch; rpst_wct_phase_ms waits for the
+ * last armed call and returns the two durations in milliseconds. */
+int rpst_wct_phase_timing(int on);
+int rpst_wct_phase_ms(float* cov_ms, float* matfun_ms);
 
 /* out = act(conv(pad(T_n x + c_n)) + bias) per image n: the WCT colour transform fused into
  * the consumer conv. F(4x4) layers fold T_n into per-image weights W T_n (fp64, rounded

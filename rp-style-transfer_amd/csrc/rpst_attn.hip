@@ -27,6 +27,11 @@ namespace rpst {
 bool sanet_flash_ok(int C, int HW);
 int sanet_flash(const float* F, const float* G, const float* H, float* O, int B, int C, int HW,
                 hipStream_t st);
+int adaptive_flash_stats(const float* F, const float* G, int B, int C, int HW, float* rm,
+                         float* rinv, hipStream_t st);
+int adaptive_flash_apply(const float* F, const float* G, const float* H, float* O, int B, int C,
+                         int HW, const float* rm, const float* rinv, const float* clamp, int mode,
+                         float scale, hipStream_t st);
 
 enum { LAY_RK = 0, LAY_KR = 1 };
 
@@ -614,9 +619,11 @@ __global__ __launch_bounds__(256) void rowstats_relu_kernel(
 
 // Materialise P = softmax(S) (claim_before) and/or the clamped attention (claim_after)
 // for callers that keep them (AdaptiveSANet.claim_before / claim_after).
+// (S may be one of the outputs: the flash path forms S in the caller's claim buffer, and each
+// element is read before it is overwritten)
 __global__ __launch_bounds__(256) void claim_maps_kernel(
-    const float* __restrict__ S, RowVec rv, const float* __restrict__ inv2, int mode,
-    float* __restrict__ before, float* __restrict__ after, int64_t rows, int L) {
+    const float* S, RowVec rv, const float* __restrict__ inv2, int mode, float* before,
+    float* after, int64_t rows, int L) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= rows * L) return;
   const int64_t r = idx / L;
@@ -829,15 +836,17 @@ extern "C" int rpst_aea_clamp(const float* x, const float* fx, const float* w1,
   return launch_status("aea_apply_kernel");
 }
 
-// the logits' region first holds T = sn W1^T (C x hidden per image): whichever is larger
+// the logits' region first holds T = sn W1^T (C x hidden per image): whichever is larger.
+// On the flash path (sanet_flash_ok) S is never formed: T only.
 static size_t sq_or_t(int B, int C, int HW, int hidden) {
+  if (sanet_flash_ok(C, HW)) return (size_t)B * C * hidden;
   return (size_t)B * std::max((size_t)HW * HW, (size_t)C * hidden);
 }
 
 extern "C" size_t rpst_adaptive_attention_workspace_size(int B, int C, int HW, int hidden) {
   if (B <= 0 || C <= 0 || HW <= 0 || hidden <= 0) return 0;
   return sizeof(float) * (sq_or_t(B, C, HW, hidden) + (size_t)B * HW * hidden +
-                          2 * (size_t)B * C * HW + 5 * (size_t)B * HW);
+                          2 * (size_t)B * C * HW + 7 * (size_t)B * HW);
 }
 
 extern "C" int rpst_adaptive_attention(const float* F, const float* G, const float* H,
@@ -875,13 +884,52 @@ extern "C" int rpst_adaptive_attention(const float* F, const float* G, const flo
   if (int e = clamp_values_factored(cn, sn, w1, b1, w2, b2, hidden, mode, from, interval, S, Z,
                                     clamp, B, C, HW, st))
     return e;
-  // 2. logits S = F^T G and softmax row statistics (sanet.py:114-117)
   const int64_t fhw = (int64_t)C * HW;
+  const int64_t rows = (int64_t)B * HW;
+  if (sanet_flash_ok(C, HW)) {
+    // 2. pass 1: softmax row statistics of S = F^T G, S never written (rpst_flash.hip)
+    if (int e = adaptive_flash_stats(F, G, B, C, HW, rmax, rinv, st)) return e;
+    if (claim_before || claim_after) {
+      // the maps the caller keeps: S formed in its own (B, HW, HW) buffer and transformed in
+      // place, with pass 1's statistics
+      // (row statistics of this S itself: pass 1's, from the flash kernel's summation order,
+      // would put the maps ~1e-5 off the logits they transform, amplified by the slope-50
+      // sigmoid)
+      float* Sx = claim_before ? claim_before : claim_after;
+      float* cmax = inv2 + (size_t)B * HW;
+      float* cinv = cmax + (size_t)B * HW;
+      GemmArgs g1{F, G, Sx, {}, nullptr, nullptr, 0, HW, HW, C, HW, HW, HW,
+                  fhw, fhw, (int64_t)HW * HW, 0};
+      launch_gemm<LAY_KR, LAY_KR, BX_NONE>(g1, B, st);
+      if (int e = launch_status("gemm_f32_kernel(S=F^T G, claims)")) return e;
+      rowstats_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Sx, cmax, cinv, rows, HW);
+      if (int e = launch_status("rowstats_kernel")) return e;
+      if (mode == 1) {
+        rowstats_relu_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Sx, cmax, cinv, clamp,
+                                                                         m2, inv2, rows, HW);
+        if (int e = launch_status("rowstats_relu_kernel")) return e;
+      }
+      const RowVec rv{cmax, cinv, clamp, m2, scale};
+      const int64_t n = rows * HW;
+      claim_maps_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(Sx, rv, inv2, mode,
+                                                                     claim_before, claim_after,
+                                                                     rows, HW);
+      if (int e = launch_status("claim_maps_kernel")) return e;
+    }
+    if (claim_value &&
+        hipMemcpyAsync(claim_value, clamp, sizeof(float) * rows, hipMemcpyDeviceToDevice, st) !=
+            hipSuccess) {
+      set_error("adaptive_attention: claim_value copy failed");
+      return RPST_EHIP;
+    }
+    // 3. pass 2: S recomputed per key block, Q formed in registers, O = H Q^T
+    return adaptive_flash_apply(F, G, H, O, B, C, HW, rmax, rinv, clamp, mode, scale, st);
+  }
+  // 2. logits S = F^T G and softmax row statistics (sanet.py:114-117)
   GemmArgs g1{F, G, S, {}, nullptr, nullptr, 0, HW, HW, C, HW, HW, HW,
               fhw, fhw, (int64_t)HW * HW, 0};
   launch_gemm<LAY_KR, LAY_KR, BX_NONE>(g1, B, st);
   if (int e = launch_status("gemm_f32_kernel(S=F^T G)")) return e;
-  const int64_t rows = (int64_t)B * HW;
   rowstats_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rmax, rinv, rows, HW);
   if (int e = launch_status("rowstats_kernel")) return e;
   RowVec rv{rmax, rinv, clamp, m2, scale};

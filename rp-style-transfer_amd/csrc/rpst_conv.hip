@@ -341,6 +341,60 @@ __global__ __launch_bounds__(256) void stat_merge_kernel(const float2* __restric
   }
 }
 
+// The same merge for partials in [n][partial][co] order (ConvGeom::stat_t): a block takes 64
+// consecutive channels of one image (coalesced 512-B reads per partial); its 4 waves fold
+// the partials in 4 consecutive segments, each lane in order, then the 4 segment states are
+// combined in segment order -- a fixed order, as above (the float2 partials are rounded the
+// same; the fp64 merge tree differs from stat_merge_kernel's).
+__global__ __launch_bounds__(256) void stat_merge_t_kernel(const float2* __restrict__ part,
+                                                           float* __restrict__ mean,
+                                                           float* __restrict__ stdv, int Cout,
+                                                           int P, int tiles_x, int WN, int NT,
+                                                           int TW, int H, int W, float eps) {
+  const int cgroups = (Cout + 63) / 64;
+  const int n = blockIdx.x / cgroups;
+  const int co = (blockIdx.x - n * cgroups) * 64 + (threadIdx.x & 63);
+  const int seg = threadIdx.x >> 6;
+  const int per = (P + 3) / 4, p0 = seg * per, p1 = min(P, p0 + per);
+  double cn = 0.0, cm = 0.0, c2 = 0.0;
+  if (co < Cout) {
+    const float2* pp = part + (int64_t)n * P * Cout + co;
+    for (int p = p0; p < p1; ++p) {
+      const int tile = p / WN, wn = p - tile * WN;
+      const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+      const int rows = max(0, min(NT, H - (ty * NT * WN + wn * NT)));
+      const int cols = max(0, min(TW, W - tx * TW));
+      const double nb = (double)(rows * cols);
+      if (nb == 0.0) continue;
+      const float2 v = pp[(int64_t)p * Cout];
+      const double n2 = cn + nb, d = (double)v.x - cm;
+      cm += d * nb / n2;
+      c2 += (double)v.y + d * d * cn * nb / n2;
+      cn = n2;
+    }
+  }
+  __shared__ double sh[3][256];
+  sh[0][threadIdx.x] = cn;
+  sh[1][threadIdx.x] = cm;
+  sh[2][threadIdx.x] = c2;
+  __syncthreads();
+  if (seg != 0 || co >= Cout) return;
+  for (int s = 1; s < 4; ++s) {
+    const int t = s * 64 + threadIdx.x;
+    const double on = sh[0][t], om = sh[1][t], o2 = sh[2][t];
+    const double n2 = cn + on;
+    if (n2 > 0.0) {
+      const double d = om - cm;
+      cm += d * on / n2;
+      c2 += o2 + d * d * cn * on / n2;
+    }
+    cn = n2;
+  }
+  const float varf = (float)(cn > 1.0 ? c2 / (cn - 1.0) : __builtin_nan(""));
+  mean[(int64_t)n * Cout + co] = (float)cm;
+  stdv[(int64_t)n * Cout + co] = __fsqrt_rn(__fadd_rn(varf, eps));
+}
+
 // ---- weight packing: (Cout,Cin,KS,KS) -> [chunk][tap][ci_local][Cout_pad] ------------
 __global__ void conv_pack_kernel(const float* __restrict__ w, float* __restrict__ pk,
                                  int Cout, int Cin, int KS, int CK, int Cout_pad,
@@ -659,6 +713,7 @@ struct ConvGeom {
   int algo;
   int64_t blocks;
   int nth, stat_P, stat_nt, stat_wn, stat_tw, tiles_x;
+  bool stat_t;  // partials in [n][partial][co] order (the position-quarter F(4x4) kernel)
 };
 
 // rows per thread of the narrow kernel: 4 for Cout <= 4 (16->3: 0.307 vs 0.348 ms;
@@ -698,7 +753,8 @@ static ConvGeom conv_geom(int N, int Cin, int Hs, int Ws, int Cout, int ksize, i
     g.tiles_x = (W + kW4Cols - 1) / kW4Cols;
     const int ty = (H + 4 * nr - 1) / (4 * nr);
     g.blocks = (int64_t)g.tiles_x * ty * N * (wino4_persist() ? 1 : (Cout + kW4Co - 1) / kW4Co);
-    g.nth = wino4q_applies(Cin, Cout, in_op) ? 512 : 128 * nr;
+    g.stat_t = wino4q_applies(Cin, Cout, in_op);
+    g.nth = g.stat_t ? 512 : 128 * nr;
     g.stat_P = g.tiles_x * ty * nr;
     g.stat_nt = 4;
     g.stat_wn = nr;
@@ -1153,6 +1209,12 @@ static int conv2d_stats_impl(const float* input, const float* aux, const float* 
                           Cout, ksize, pad_mode, in_op, relu, static_cast<float2*>(workspace), &P,
                           &a, st, fold_ws, store_n < N ? store_n : 0))
     return e;
+  if (g.stat_t) {
+    stat_merge_t_kernel<<<N * ((Cout + 63) / 64), 256, 0, st>>>(
+        static_cast<const float2*>(workspace), mean, std_out, Cout, P, a.tiles_x, g.stat_wn,
+        g.stat_nt, g.stat_tw, a.H, a.W, eps);
+    return launch_status("stat_merge_t_kernel");
+  }
   stat_merge_kernel<<<(planes + 3) / 4, 256, 0, st>>>(static_cast<const float2*>(workspace), mean,
                                                       std_out, planes, P, a.tiles_x, g.stat_wn,
                                                       g.stat_nt, g.stat_tw, a.H, a.W, eps);

@@ -79,12 +79,32 @@ __device__ __forceinline__ float rows4_sum(float v) {
 }
 constexpr float kLog2e = 1.4426950408889634f;
 
-template <int C, bool PIPE>
+// What the kernel forms from a block of scores S (AdaptiveSANet, sanet.py:100-124, runs two
+// passes, since its clamp sigmoid(scale (P - c)) / relu-softmax needs each query's final
+// softmax statistics before any key's weight is known):
+//   AM_SOFTMAX  SANet: online softmax, O = H softmax(S)^T
+//   AM_STATS    pass 1: m = max_j S_ij, inv = 1 / sum_j exp(S_ij - m) only (no H, no O)
+//   AM_AEA      pass 2, AEAModule (sanet.py:42-47): O = H Q^T, Q = sigmoid(scale (P - c))
+//   AM_AEAR     pass 2, AEALReluModule (sanet.py:63-69): Q = softmax_j(relu(P - c)), whose
+//               max is known from pass 1 (max_j P_ij = inv_i: m2 = relu(inv - c)), so pass 2
+//               accumulates O and sum_j exp(relu(P - c) - m2) with no rescaling
+// with P_ij = exp(S_ij - m_i) inv_i. Neither pass writes S: no B x HW x HW workspace.
+enum { AM_SOFTMAX = 0, AM_STATS = 1, AM_AEA = 2, AM_AEAR = 3 };
+struct AttnRows {
+  const float* m;    // AM_AEA / AM_AEAR: pass 1's row max ...
+  const float* inv;  // ... and inverse row sum
+  const float* c;    // clamp value per query row
+  float scale;       // AM_AEA: sigmoid slope (scale_value)
+  float* out_m;      // AM_STATS outputs
+  float* out_inv;
+};
+
+template <int C, bool PIPE, int AM = AM_SOFTMAX>
 __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __restrict__ F,
                                                              const float* __restrict__ G,
                                                              const float* __restrict__ H,
                                                              float* __restrict__ O, int HW,
-                                                             int qblocks) {
+                                                             int qblocks, AttnRows rows) {
   constexpr int NQ = C / 4;            // Q registers per lane
   constexpr int NMB = C / 16;          // O accumulators (16 channel rows each)
   constexpr int TILE = C * kFBN;       // floats per G / H tile
@@ -106,8 +126,11 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
   const unsigned bytes = (unsigned)(plane * 4);
   const auto rG = __builtin_amdgcn_make_buffer_rsrc((void*)(G + b * plane), (short)0, (int)bytes, 0x00020000);
   const auto rH = __builtin_amdgcn_make_buffer_rsrc((void*)(H + b * plane), (short)0, (int)bytes, 0x00020000);
-  // DMA piece j of a tile: lane -> (channel row 16 j + lane / 4, 16-B segment lane % 4); the
-  // row offset of piece j is the uniform soffset, so one voffset per lane and tile
+  // DMA piece j of a tile: lane -> (channel row 16 j + lane / 4, 16-B segment lane % 4). The
+  // whole offset goes in voffset (not the piece's uniform row offset in soffset): the buffer
+  // range check covers voffset only, and with HW % 16 != 0 the last key block of the last
+  // channel row runs past the image plane -- those keys must read as 0, not as whatever
+  // follows the tensor (a non-finite H there would turn 0 * H into NaN in O)
   const int prow = lane >> 2, pseg = lane & 3;
   const unsigned voffG = (unsigned)(prow * HW + 4 * pseg) * 4u;
   const unsigned voffH = (unsigned)(prow * HW + 4 * (pseg ^ ((lane >> 4) & 3))) * 4u;
@@ -120,11 +143,11 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
     const int j = wave * PPW + (isg ? jj : jj - PPW);
     if (isg) {
       if (k0g >= 0)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (attn_lds_ptr_t)(gs + 256 * j), 16, (int)voffG,
-                                                 (16 * j * HW + k0g) * 4, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (attn_lds_ptr_t)(gs + 256 * j), 16, (int)(voffG + (unsigned)(16 * j * HW + k0g) * 4u), 0,
+                                                 0, 0);
     } else if (k0h >= 0) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rH, (attn_lds_ptr_t)(hs + 256 * j), 16, (int)voffH,
-                                               (16 * j * HW + k0h) * 4, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rH, (attn_lds_ptr_t)(hs + 256 * j), 16, (int)(voffH + (unsigned)(16 * j * HW + k0h) * 4u), 0,
+                                               0, 0);
     }
   };
   static_assert(NQ / 8 == 2 * PPW, "one DMA piece per MFMA group of scores()");
@@ -132,16 +155,16 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
 #pragma unroll
     for (int jj = 0; jj < PPW; ++jj) {
       const int j = wave * PPW + jj;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (attn_lds_ptr_t)(gs + 256 * j), 16, (int)voffG,
-                                               (16 * j * HW + k0) * 4, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (attn_lds_ptr_t)(gs + 256 * j), 16, (int)(voffG + (unsigned)(16 * j * HW + k0) * 4u), 0,
+                                               0, 0);
     }
   };
   auto issue_h = [&](int k0, float* hs) {
 #pragma unroll
     for (int jj = 0; jj < PPW; ++jj) {
       const int j = wave * PPW + jj;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rH, (attn_lds_ptr_t)(hs + 256 * j), 16, (int)voffH,
-                                               (16 * j * HW + k0) * 4, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rH, (attn_lds_ptr_t)(hs + 256 * j), 16, (int)(voffH + (unsigned)(16 * j * HW + k0) * 4u), 0,
+                                               0, 0);
     }
   };
   const int nk = (HW + kFBN - 1) / kFBN;
@@ -158,6 +181,17 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
 #pragma unroll
   for (int mb = 0; mb < NMB; ++mb) acc[mb] = floatx4{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
+  // pass 2: this lane's query's row statistics and clamp, exp2 arguments pre-scaled
+  float a_mL = 0.f, a_inv = 0.f, a_c = 0.f, a_m2L = 0.f;
+  if constexpr (AM >= AM_AEA) {
+    if (q < HW) {
+      const int64_t r = (int64_t)b * HW + q;
+      a_mL = rows.m[r] * kLog2e;
+      a_inv = rows.inv[r];
+      a_c = rows.c[r];
+    }
+    a_m2L = fmaxf(a_inv - a_c, 0.f) * kLog2e;
+  }
   const int hsw = 4 * (g ^ ((lq >> 2) & 3));  // swizzled segment of keys 4 g .. 4 g + 3
 
   float p[4] = {0.f, 0.f, 0.f, 0.f};  // P of the key block whose O update is pending
@@ -197,6 +231,23 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
       return;
     }
     const int kbase = kb * kFBN + 4 * g;
+    if constexpr (AM >= AM_AEA) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float P = __builtin_amdgcn_exp2f(fmaf(sc[r], kLog2e, -a_mL)) * a_inv;
+        float v;
+        if constexpr (AM == AM_AEA) {
+          // sigmoid(scale (P - c)); exp2 overflows to +inf far below the clamp: weight 0
+          const float e = __builtin_amdgcn_exp2f(-rows.scale * kLog2e * (P - a_c));
+          v = __builtin_amdgcn_rcpf(1.f + e);
+        } else {
+          v = __builtin_amdgcn_exp2f(fmaf(fmaxf(P - a_c, 0.f), kLog2e, -a_m2L));
+        }
+        p[r] = kbase + r < HW ? v : 0.f;  // keys past HW weigh nothing
+        if constexpr (AM == AM_AEAR) l_run += p[r];
+      }
+      return;
+    }
     float sv[4], mx = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -220,7 +271,7 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
     }
     l_run = fmaf(l_run, alpha, ps);
     m_run = m_new;
-    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+    if (AM == AM_SOFTMAX && __builtin_amdgcn_ballot_w64(alpha != 1.f)) {
 #pragma unroll
       for (int mb = 0; mb < NMB; ++mb) acc[mb] *= alpha;
     }
@@ -229,7 +280,7 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
   // groups of UG, the H reads of group u + 1 issued before group u's MFMAs
   constexpr int UG = NMB >= 4 ? 4 : NMB;
   auto update = [&](const float* hs) {
-    if (RPST_FLDBG & 8) return;
+    if ((RPST_FLDBG & 8) || AM == AM_STATS) return;
     float4 hb[2][UG];
     auto ld = [&](float4 (&h)[UG], int u) {
 #pragma unroll
@@ -252,14 +303,15 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
         }
     }
   };
+  constexpr bool useH = AM != AM_STATS;
   if constexpr (!PIPE) {
-    issue_h(0, Hs0);
+    if (useH) issue_h(0, Hs0);
     auto step = [&](int kb, const float* gs, const float* hs, float* gn, float* hn) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's key tile kb has landed
       __builtin_amdgcn_s_barrier();                     // ... for every wave; the other
       // (the other buffers are free: step kb - 1 is done everywhere)
       const int k1 = kb + 1 < nk ? (kb + 1) * kFBN : -1;
-      softmax(kb, scores(kb, gs, [&](int t) { piece(t, k1, gn, k1, hn); }));
+      softmax(kb, scores(kb, gs, [&](int t) { piece(t, k1, gn, useH ? k1 : -1, hn); }));
       update(hs);
     };
     for (int kb = 0; kb < nk; kb += 2) {
@@ -276,7 +328,8 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // G(kb), H(kb - 1) have landed
         __builtin_amdgcn_s_barrier();
       }
-      const int kg = kb + 1 < nk ? (kb + 1) * kFBN : -1, kh = kb < nk ? kb * kFBN : -1;
+      const int kg = kb + 1 < nk ? (kb + 1) * kFBN : -1,
+                kh = useH && kb < nk ? kb * kFBN : -1;
       floatx4 sc = {0.f, 0.f, 0.f, 0.f};
       if (kb < nk) sc = scores(kb, gs, [&](int t) { piece(t, kg, gn, kh, hcur); });
       // (the last iteration has no scores and no DMA left: kg, kh < 0)
@@ -289,9 +342,16 @@ __global__ __launch_bounds__(256, 1) void sanet_flash_kernel(const float* __rest
     }
   }
   // the row sum over the four lane groups holding a query's keys; O / l
-  l_run = rows4_sum(l_run);
+  if constexpr (AM != AM_AEA) l_run = rows4_sum(l_run);
+  if constexpr (AM == AM_STATS) {
+    if (q < HW && g == 0) {
+      rows.out_m[(int64_t)b * HW + q] = m_run;
+      rows.out_inv[(int64_t)b * HW + q] = 1.f / l_run;
+    }
+    return;
+  }
   if (q < HW) {
-    const float inv = 1.f / l_run;
+    const float inv = AM == AM_AEA ? 1.f : 1.f / l_run;
     float* Ob = O + b * plane + q;
 #pragma unroll
     for (int mb = 0; mb < NMB; ++mb)
@@ -345,9 +405,9 @@ __global__ __launch_bounds__(512, 1) void sanet_flash8_kernel(const float* __res
 #pragma unroll
     for (int jj = 0; jj < PPW; ++jj) {
       const int j = wave * PPW + jj;
-      const int so = (16 * j * HW + k0) * 4;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (attn_lds_ptr_t)(gs + 256 * j), 16, (int)voffG, so, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rH, (attn_lds_ptr_t)(hs + 256 * j), 16, (int)voffH, so, 0, 0);
+      const unsigned so = (unsigned)(16 * j * HW + k0) * 4u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rG, (attn_lds_ptr_t)(gs + 256 * j), 16, (int)(voffG + so), 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rH, (attn_lds_ptr_t)(hs + 256 * j), 16, (int)(voffH + so), 0, 0, 0);
     }
   };
   const int nk = (HW + kFBN - 1) / kFBN;
@@ -459,15 +519,56 @@ int sanet_flash(const float* F, const float* G, const float* H, float* O, int B,
   }
 #define RPST_FLASH_GO(P)                                                                      \
   switch (C) {                                                                                \
-    case 64: sanet_flash_kernel<64, P><<<(unsigned)nb, 256, 0, st>>>(F, G, H, O, HW, qblocks); break;   \
-    case 128: sanet_flash_kernel<128, P><<<(unsigned)nb, 256, 0, st>>>(F, G, H, O, HW, qblocks); break; \
-    case 256: sanet_flash_kernel<256, P><<<(unsigned)nb, 256, 0, st>>>(F, G, H, O, HW, qblocks); break; \
-    default: sanet_flash_kernel<512, P><<<(unsigned)nb, 256, 0, st>>>(F, G, H, O, HW, qblocks); break;  \
+    case 64: sanet_flash_kernel<64, P><<<(unsigned)nb, 256, 0, st>>>(F, G, H, O, HW, qblocks, {}); break;   \
+    case 128: sanet_flash_kernel<128, P><<<(unsigned)nb, 256, 0, st>>>(F, G, H, O, HW, qblocks, {}); break; \
+    case 256: sanet_flash_kernel<256, P><<<(unsigned)nb, 256, 0, st>>>(F, G, H, O, HW, qblocks, {}); break; \
+    default: sanet_flash_kernel<512, P><<<(unsigned)nb, 256, 0, st>>>(F, G, H, O, HW, qblocks, {}); break;  \
   }
   if (sanet_flash_mode() == 3) RPST_FLASH_GO(false)
   else RPST_FLASH_GO(true)
 #undef RPST_FLASH_GO
   return launch_status("sanet_flash_kernel");
+}
+
+// AdaptiveSANet attention without S (sanet.py:100-124): pass 1 writes each query's softmax
+// statistics (rm, rinv: B x HW each), pass 2 recomputes S per key block and accumulates
+// O = H Q^T with the clamp applied in registers. mode 0 = AEAModule, 1 = AEALReluModule.
+template <int AM>
+static void adaptive_flash_launch(int C, unsigned nb, hipStream_t st, const float* F,
+                                  const float* G, const float* H, float* O, int HW, int qblocks,
+                                  const AttnRows& rows) {
+  switch (C) {
+    case 64: sanet_flash_kernel<64, true, AM><<<nb, 256, 0, st>>>(F, G, H, O, HW, qblocks, rows); break;
+    case 128: sanet_flash_kernel<128, true, AM><<<nb, 256, 0, st>>>(F, G, H, O, HW, qblocks, rows); break;
+    case 256: sanet_flash_kernel<256, true, AM><<<nb, 256, 0, st>>>(F, G, H, O, HW, qblocks, rows); break;
+    default: sanet_flash_kernel<512, true, AM><<<nb, 256, 0, st>>>(F, G, H, O, HW, qblocks, rows); break;
+  }
+}
+
+int adaptive_flash_stats(const float* F, const float* G, int B, int C, int HW, float* rm,
+                         float* rinv, hipStream_t st) {
+  const int qblocks = (HW + kFBM - 1) / kFBM;
+  const int64_t nb = (int64_t)B * qblocks;
+  RPST_REQUIRE(nb <= 0x7fffffffLL, "adaptive_attention: grid too large");
+  AttnRows rows{};
+  rows.out_m = rm;
+  rows.out_inv = rinv;
+  adaptive_flash_launch<AM_STATS>(C, (unsigned)nb, st, F, G, nullptr, nullptr, HW, qblocks, rows);
+  return launch_status("sanet_flash_kernel(stats)");
+}
+
+int adaptive_flash_apply(const float* F, const float* G, const float* H, float* O, int B, int C,
+                         int HW, const float* rm, const float* rinv, const float* clamp, int mode,
+                         float scale, hipStream_t st) {
+  const int qblocks = (HW + kFBM - 1) / kFBM;
+  const int64_t nb = (int64_t)B * qblocks;
+  RPST_REQUIRE(nb <= 0x7fffffffLL, "adaptive_attention: grid too large");
+  const AttnRows rows{rm, rinv, clamp, scale, nullptr, nullptr};
+  if (mode == 0)
+    adaptive_flash_launch<AM_AEA>(C, (unsigned)nb, st, F, G, H, O, HW, qblocks, rows);
+  else
+    adaptive_flash_launch<AM_AEAR>(C, (unsigned)nb, st, F, G, H, O, HW, qblocks, rows);
+  return launch_status("sanet_flash_kernel(adaptive)");
 }
 
 }  // namespace rpst

@@ -593,8 +593,23 @@ __global__ void narrow_means_kernel(const double* __restrict__ m, float* __restr
 // Li et al., wct_rp.py:96-101; offset unused). SRC is SRC_F32C (fp32 features) or SRC_F64C (fp64). means: optional fp32 (2n x C)
 // row means (content rows then style rows), used to centre; residual (2n, optional): final
 // Newton-Schulz residuals of (Cc + 1e-4 I) and of Mid's argument. T / offset: n x C x C / n x C.
+// phase timing (rpst_wct_phase_timing / rpst_wct_phase_ms): events before the means, before
+// the matrix-function launch and after it, on the closed-form path
+static bool g_phase_on = false, g_phase_done = false;
+static hipEvent_t g_phase_ev[3];
+static void phase_mark(int i, hipStream_t st) {
+  if (!g_phase_on) return;
+  static const bool made = [] {
+    for (auto& e : g_phase_ev) (void)hipEventCreate(&e);
+    return true;
+  }();
+  (void)made;
+  (void)hipEventRecord(g_phase_ev[i], st);
+  if (i == 2) g_phase_done = true;
+}
+
 template <int SRC>
-static int wct_matrices(const void* cF, const void* sF, const float* means, int n, int C,
+static int wct_matrices_impl(const void* cF, const void* sF, const float* means, int n, int C,
                         int64_t HW, const WctLayout& L, double* ws, double* T, double* offset,
                         double* residual, hipStream_t st, bool original = false) {
   double *mu_c = ws + L.mu_c, *part = ws + L.part;
@@ -687,7 +702,19 @@ static int wct_matrices(const void* cF, const void* sF, const float* means, int 
   }
   // 3. Sc, Ic = (Cc + 1e-4 I)^(+-1/2); Mid = (Sc Cs Sc + 1e-4 I)^(1/2); T = Ic Mid Ic;
   //    offset = mu_s - T mu_c: one persistent launch
+  phase_mark(1, st);
   return matfun_wct(Cc, Cs, mu_c, T, offset, residual, n, C, ws + L.mf, st);
+}
+
+template <int SRC>
+static int wct_matrices(const void* cF, const void* sF, const float* means, int n, int C,
+                        int64_t HW, const WctLayout& L, double* ws, double* T, double* offset,
+                        double* residual, hipStream_t st, bool original = false) {
+  if (!original) phase_mark(0, st);
+  const int e = wct_matrices_impl<SRC>(cF, sF, means, n, C, HW, L, ws, T, offset, residual, st,
+                                       original);
+  if (!original && !e) phase_mark(2, st);
+  return e;
 }
 
 // Shared WCT body: the matrices, then out = T (cF - mu_c) + mu_s.
@@ -842,6 +869,25 @@ extern "C" int rpst_wct_status(const void* workspace, int n, int C, int64_t HW, 
   const WctLayout L = wct_layout(n, C, HW, true);
   double* ws = static_cast<double*>(const_cast<void*>(workspace));
   return matfun_wct_status(ws + L.mf, n, C, status, as_stream(stream));
+}
+
+extern "C" int rpst_wct_phase_timing(int on) {
+  const int old = g_phase_on;
+  g_phase_on = on != 0;
+  if (on) g_phase_done = false;
+  return old;
+}
+
+extern "C" int rpst_wct_phase_ms(float* cov_ms, float* matfun_ms) {
+  RPST_REQUIRE(cov_ms && matfun_ms, "wct_phase_ms: null pointer");
+  RPST_REQUIRE(g_phase_done, "wct_phase_ms: no call recorded while armed");
+  if (hipEventSynchronize(g_phase_ev[2]) != hipSuccess ||
+      hipEventElapsedTime(cov_ms, g_phase_ev[0], g_phase_ev[1]) != hipSuccess ||
+      hipEventElapsedTime(matfun_ms, g_phase_ev[1], g_phase_ev[2]) != hipSuccess) {
+    set_error("wct_phase_ms: event query failed");
+    return RPST_EHIP;
+  }
+  return RPST_OK;
 }
 
 extern "C" int rpst_whiten_and_color_status(const void* workspace, int C, int64_t HW, int* status,

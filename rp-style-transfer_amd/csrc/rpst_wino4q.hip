@@ -56,6 +56,21 @@ __device__ __forceinline__ float q_row16_sum(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
   return v;
 }
+// this lane's id, computed afresh where it is called (asm volatile: not hoisted or CSE'd).
+// The main loop re-derives every lane-dependent address from it once per iteration, so none
+// is live across the epilogue: there the allocator spilled them, and each spill reload's
+// compiler-inserted vmcnt(0) drained the in-flight DMA ring (cdna_hip_programming.md, glds
+// pitfalls). s_nop 1: the asm's VGPR write is invisible to the hazard recognizer.
+__device__ __forceinline__ int q_lane() {
+  int l;
+#if __HIP_DEVICE_COMPILE__
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\ts_nop 1"
+               : "=v"(l));
+#else
+  l = 0;
+#endif
+  return l;
+}
 // a wave-uniform value made opaque here (not hoisted out of the enclosing loop)
 __device__ __forceinline__ int q_launder(int v) {
 #if __HIP_DEVICE_COMPILE__
@@ -144,6 +159,7 @@ constexpr int kQCS = 768;                    // patch channel stride (floats)
 constexpr int kQWS = 9216;                   // weight floats per (co tile, K step)
 constexpr int kQPAT = 4 * kQCS;              // patch stage: 4 channels (12 KiB)
 constexpr int kQNTH = 512;
+constexpr int kQMaxCo = 512;                 // output channels the LDS bias table holds
 constexpr int kQWPI = 5;                     // 1-KiB weight pieces per wave and step (36 / 8)
 constexpr int kQWide = 2, kQSlow = 6;        // patch pieces per wave and step: 16-B / 4-B
 constexpr int kQDMA4 = 3, kQDMA = 11;        // patch pieces per channel: 16-B / 4-B
@@ -161,7 +177,8 @@ static_assert(10 * 17 <= kQDMA4 * 64 && kQDMA4 * 256 <= kQCS, "16-B pieces in a 
 static_assert(10 * kQPS <= kQDMA * 64 && kQDMA * 64 <= kQCS, "4-B pieces in a channel");
 static_assert(2 * kQWide >= kQDMA4 && 2 * kQSlow >= kQDMA && 8 * kQWPI >= 36, "coverage");
 static_assert(2 * kQXS <= kQWS, "the exchange fits a weight stage");
-static_assert((2 * kQWS + 4 * kQPAT) * 4 + 1024 + kQSlow * kQNTH * 4 <= 163840, "LDS");
+static_assert((2 * kQWS + 4 * kQPAT) * 4 + 1024 + kQSlow * kQNTH * 4 + 9 * kQMaxCo * 4 <= 163840,
+              "LDS");
 
 // ---- weight transform + packing -------------------------------------------------------
 // packed[((((ct * K4 + ks) * 4 + q) * 9 + p) * 64 + l) * 4 + cb] = U_xi[co][ci] with
@@ -272,7 +289,8 @@ bool wino4q_applies(int Cin, int Cout, int in_op) {
     return (e && *e) ? atoi(e) : 1;
   }();
   const int min_cin = en == 2 ? 16 : 128;
-  return en && conv_quarter_allowed() && (in_op == RPST_IN_NONE || in_op == RPST_IN_UPSAMPLE2) && Cout >= 64 &&
+  return en && conv_quarter_allowed() && (in_op == RPST_IN_NONE || in_op == RPST_IN_UPSAMPLE2) &&
+         Cout >= 64 && Cout <= kQMaxCo &&
          Cin >= min_cin && Cin % 16 == 0;
 }
 
@@ -308,7 +326,9 @@ __device__ __forceinline__ QEpi q_epi_ctx(int wr, int tn) {
   e.vec = (e.W & 3) == 0 && e.gx0 + 3 < e.W;
   e.rows = max(0, min(4, e.H - e.gy0));
   const int cols = max(0, min(kQTW, e.W - bx0));
-  e.inv = e.rows * cols > 0 ? 1.f / (float)(e.rows * cols) : 0.f;
+  // (v_rcp: exact for the 256-pixel full tiles; the IEEE division's ~10-instruction sequence
+  // ran per channel)
+  e.inv = e.rows * cols > 0 ? __builtin_amdgcn_rcpf((float)(e.rows * cols)) : 0.f;
   e.full = e.rows == 4 && bx0 + kQTW <= e.W;
   e.edge = e.gy0 == 0 || e.gy0 + 4 >= e.H || bx0 == 0 || bx0 + kQTW >= e.W;
   e.out = L->out;
@@ -338,7 +358,7 @@ __device__ __forceinline__ void q_finish(const QEpi& e, int co, float (&Y)[16], 
   const bool cok = co < e.Cout;
   if constexpr (BTAB) {
     if (e.edge) {
-      const float* bt = e.btab + ((int64_t)n * e.Cout + (cok ? co : 0)) * 9;
+      const float* bt = e.btab + (cok ? co : 0) * 9;  // this image's table, in LDS
       float b9[9];
 #pragma unroll
       for (int i = 0; i < 9; ++i) b9[i] = cok ? bt[i] : 0.f;
@@ -428,11 +448,15 @@ __device__ __forceinline__ void q_finish(const QEpi& e, int co, float (&Y)[16], 
       }
     }
   }
+#ifndef RPST_W4Q_SDBG
+#define RPST_W4Q_SDBG 0
+#endif
   if constexpr (STATS) {
-    sum = q_row16_sum(sum);
+    if (!(RPST_W4Q_SDBG & 4)) sum = q_row16_sum(sum);
     const float mean = sum * e.inv;
     float m2 = 0.f;
-    if (e.full) {
+    if (RPST_W4Q_SDBG & 2) {
+    } else if (e.full) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) m2 = fmaf(Y[i] - mean, Y[i] - mean, m2);
     } else {
@@ -444,8 +468,13 @@ __device__ __forceinline__ void q_finish(const QEpi& e, int co, float (&Y)[16], 
           m2 += (yy < rows && gx0 + xx < e.W) ? dv * dv : 0.f;
         }
     }
-    m2 = q_row16_sum(m2);
-    if (tn == 0 && cok) e.statp[((int64_t)n * e.Cout + co) * e.statP + e.sidx] = make_float2(mean, m2);
+    if (RPST_W4Q_SDBG & 2) m2 = mean;
+    if (!(RPST_W4Q_SDBG & 4)) m2 = q_row16_sum(m2);
+    // partials in [n][partial][co] order (stat_merge_t_kernel): a wave's 16 channels of one
+    // partial fill whole cache lines; in [n][co][partial] order they were 8-B pieces
+    // scattered over 16 planes, 1.1 ms of 28.3 on 128->256 N64 (RPST_W4Q_SDBG=1 skips the store)
+    if (!(RPST_W4Q_SDBG & 1) && tn == 0 && cok)
+      e.statp[((int64_t)n * e.statP + e.sidx) * e.Cout + co] = make_float2(mean, m2);
   }
 }
 
@@ -491,10 +520,15 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
   // per-lane patch source offsets (in registers they are spilled, and every reload's vmcnt
   // wait drains the DMA ring): each lane reads only its own column
   __shared__ unsigned poffs[kQSlow][kQNTH];
+  // the layer's biases (BTAB: this image's 9 border-class biases per channel), copied once
+  // per block before the ring starts: a global load in the epilogue would take a
+  // compiler-inserted vmcnt(0) that drains the in-flight DMA ring (wino4q_applies: Cout <= 512)
+  __shared__ float btl[BTAB ? 9 * kQMaxCo : kQMaxCo];
 
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int k = lane >> 4, tn = lane & 15, wr = wave >> 2;
+  const int wr = wave >> 2;
+  int ln = lane;  // the lane id the loop's addresses derive from (re-read per iteration)
 
   // block -> (co-split group, column tile, row tile, image); XCD-swizzled
   int bid = xcd_swizzle(blockIdx.x, (int)gridDim.x);
@@ -508,6 +542,11 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
   const int K4 = a.nchunks, G = nct * K4;
   const int y0 = ty * kQTH, x0 = tx * kQTW;
 
+  {
+    const int nb = BTAB ? 9 * a.Cout : a.Cout;
+    const float* src = BTAB ? a.btab + (int64_t)n * nb : a.bias;
+    for (int i = threadIdx.x; i < nb; i += kQNTH) btl[i] = src ? src[i] : 0.f;
+  }
   constexpr bool up = INOP == RPST_IN_UPSAMPLE2;
   const unsigned in_plane = up ? (unsigned)(a.Hs * a.Ws) : (unsigned)(a.H * a.W);
   const unsigned oob = a.Cin * in_plane * 4u;  // a padding position's (out-of-range) offset
@@ -564,10 +603,10 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     const bool live = g < G;
     const int so = q_mask((g * kQWS + pc * 256) * 4, live);
     if (i < 4) {
-      q_dma16(q_rsrc(w_img, wbytes, live), stg + pc * 256, lane * 16, so);
+      q_dma16(q_rsrc(w_img, wbytes, live), stg + pc * 256, ln * 16, so);
     } else {
       const bool real = pc < 36;
-      q_dma16(q_rsrc(w_img, wbytes, live && real), real ? stg + pc * 256 : dummy, lane * 16,
+      q_dma16(q_rsrc(w_img, wbytes, live && real), real ? stg + pc * 256 : dummy, ln * 16,
               q_mask(so, real));
     }
   };
@@ -582,6 +621,7 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     const int so = q_mask((int)((unsigned)c * in_plane * 4u), ok);
     float* xs = stg + (wv >> 1) * kQCS;
     const bool h1 = (wv & 1) != 0;
+    const int tid = wv * 64 + ln;
     if constexpr (WIDE) {
       q_dma16(r, xs + (h1 ? 512 : 0), poffs[0][tid], so);
       q_dma16(r, h1 ? dummy : xs + 256, poffs[1][tid], so);
@@ -594,10 +634,25 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
   };
   // before step x's barrier: W(x) (issued in step x - 1 ahead of its patch group) and
   // everything older have landed; that youngest patch group (2 / 6 pieces) stays in flight
+  // The first wait after an epilogue leaves its output stores in flight too: on the buffer-
+  // store path (q_epi_ctx's bst, kernel-uniform) every wave issues exactly 16 (4 channels x 4
+  // rows; the statistics partial stores come after them, so counting only these 16 is
+  // conservative). Waiting them out (vmcnt(2)) stalled every co tile's first step on the
+  // stores' write acknowledgements.
+  const bool bst_all = !a.pool_out && (a.W & 3) == 0 &&
+                       (int64_t)a.Cout * a.H * a.W * 4 < (1LL << 31);
+  bool post_epi = false;
   auto wait_ring = [&]() {
     if (DBG & 128) return;
-    if (wide) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (post_epi && bst_all) {
+      if (wide) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+    } else if (wide) {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    }
+    post_epi = false;
   };
 
   // ---- prologue: P(0), P(1), W(0), P(2), P(3) -------------------------------------------
@@ -624,8 +679,8 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     // lane (k, tn) reads rows 4 wr + QR .. + 4 of channel k of a patch, columns 4 tn .. + 7
     // (two conflict-free ds_read_b128; the empty asm keeps them whole, the compiler would
     // otherwise narrow them to the 5 floats a quarter uses, as bank-conflicted b32 reads)
-    const int roff = k * kQCS + (4 * wr + QR) * kQPS + 4 * tn;
     auto read_row = [&](const float* stg, int rr, float (&d)[8]) {
+      const int roff = (ln >> 4) * kQCS + (4 * wr + QR) * kQPS + 4 * (ln & 15);
       floatx4 u = *reinterpret_cast<const floatx4*>(stg + roff + rr * kQPS);
       floatx4 v = *reinterpret_cast<const floatx4*>(stg + roff + rr * kQPS + 4);
       asm("" : "+v"(u), "+v"(v));
@@ -666,8 +721,7 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
       for (int j = 0; j < 3; ++j) row_pass(u, j, V);
     }
 
-    const int woff = Q * 9 * 256 + lane * 4;  // this wave's A operands in a weight stage
-    int x = 0;                                // global K step
+    int x = 0;  // global K step
     // one K step: W(x) from wsx, P(x + 1) from psn (-> V(x + 1)), DMA W(x + 1) into wsn and
     // P(x + 4) into psx. MFMA groups in column-major position order, so the row pass of
     // column j overwrites V[j], V[3 + j], V[6 + j] after their last use.
@@ -676,6 +730,7 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
       if (DBG & 16) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else q_lds_barrier();  // W(x), P(x + 1) complete; every wave is done with step x - 1
       constexpr int ord[9] = {0, 3, 6, 1, 4, 7, 2, 5, 8};
+      const int woff = Q * 9 * 256 + ln * 4;  // this wave's A operands in a weight stage
       constexpr int kA = RPST_W4Q_AHEAD;  // A-operand groups read ahead
       float4 w4[9];
 #pragma unroll
@@ -756,6 +811,7 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
                    "+v"(acc[6][2]), "+v"(acc[6][3]), "+v"(acc[7][0]), "+v"(acc[7][1]),
                    "+v"(acc[7][2]), "+v"(acc[7][3]), "+v"(acc[8][0]), "+v"(acc[8][1]),
                    "+v"(acc[8][2]), "+v"(acc[8][3]));
+      const int lane = ln, k = ln >> 4, tn = ln & 15;
       const int co0 = ctile * kQCo + 16 * Q + 4 * k;
       // 6 passes (accumulator element pair rp, position row pt): each wave writes its 3
       // positions of row pt of the other quarters' blocks (elements 2 rp, 2 rp + 1) into ws1
@@ -807,13 +863,12 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
           const int r = 2 * rp + e2;
           // the epilogue context is re-derived per channel from the kernel arguments: kept
           // across the exchange passes it overflows the scalar registers
-          const QEpi e = q_epi_ctx(wr, tn);
+          QEpi e = q_epi_ctx(wr, tn);
+          e.btab = btl;
           float bias = 0.f;
           {
             const int co = co0 + r;
-            const float* bp = BTAB ? nullptr : q_args()->bias;
-            if (co < e.Cout)
-              bias = BTAB ? e.btab[((int64_t)e.n * e.Cout + co) * 9 + 4] : (bp ? bp[co] : 0.f);
+            if (co < e.Cout) bias = BTAB ? btl[co * 9 + 4] : btl[co];
           }
 #pragma unroll
           for (int x = 0; x < 4; ++x) P[e2][1][x] += bias;
@@ -842,6 +897,7 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     // values, and the compiler then renames every such MFMA's destination)
     int ks = 0, ct = ct0;
     for (int g = 0; g < G; g += 4) {
+      ln = q_lane();
       step(ws0, ps1, ws1, ps0, ks);
       step(ws1, ps2, ws0, ps1, ks + 1);
       step(ws0, ps3, ws1, ps2, ks + 2);
@@ -849,6 +905,7 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
       ks += 4;
       if (ks == K4) {
         epilogue(ct);
+        post_epi = true;
         ks = 0;
         ++ct;
       }

@@ -101,6 +101,8 @@ SIGNATURES = {
     "rpst_wct_fuse": (_I, [_P, _P, _P, _I, _I, _I64, _P, _P, _SZ, _P]),
     "rpst_wct_params": (_I, [_P, _P, _P, _P, _P, _I, _I, _I64, _P, _P, _SZ, _P]),
     "rpst_wct_status": (_I, [_P, _I, _I, _I64, _P, _P]),
+    "rpst_wct_phase_timing": (_I, [_I]),
+    "rpst_wct_phase_ms": (_I, [_P, _P]),
     "rpst_whiten_and_color_original_f64": (_I, [_P, _P, _P, _I, _I64, _P, _SZ, _P]),
     "rpst_whiten_and_color_status": (_I, [_P, _I, _I64, _P, _P]),
     "rpst_conv2d_mix_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I]),

@@ -78,12 +78,16 @@ def test_adaptive_sanet_golden(cuda, golden, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_adaptive_attention_peaked(cuda, mode):
+@pytest.mark.parametrize("hw2", [(12, 16), (9, 20)])
+def test_adaptive_attention_peaked(cuda, mode, hw2):
     """Logits in the hundreds: the softmax is peaked, so P crosses the clamp and both AEA
-    branches (sigmoid slope 50, relu + second softmax) carry weight. float64 reference."""
+    branches (sigmoid slope 50, relu + second softmax) carry weight. float64 reference.
+    C = 64 runs the two-pass flash kernels (no S); HW = 180 leaves a ragged last key block
+    (keys past HW weigh nothing). Without keep_claims the output is the same bits."""
     import network as net
     from rpst import ops
-    B, C, h, w = 2, 64, 12, 16
+    B, C = 2, 64
+    h, w = hw2
     hw = h * w
     mod = net.AEAModule(hw) if mode == "aea" else net.AEALReluModule(hw)
     synth_(mod, 7)
@@ -109,6 +113,54 @@ def test_adaptive_attention_peaked(cuda, mode):
     assert rel_l2(before, P) < 1e-5
     assert rel_l2(after, Q) < 1e-5
     assert rel_l2(out, ref) < 1e-5
+    with torch.no_grad():
+        out2, cl2, b2, a2 = ops.adaptive_attention(
+            F.to(cuda), G.to(cuda), H.to(cuda), c.to(cuda), s.to(cuda), mod.f_psi, mod.mode,
+            50.0, 0.4, 0.5, keep_claims=False)
+    assert b2 is None and a2 is None
+    assert torch.equal(out2, out) and torch.equal(cl2, cl)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_adaptive_attention_relu4_1_at_1024(cuda, mode):
+    """AdaptiveSANet at relu4_1 of a 1024x1024 image (C = 512, HW =
+    128 x 128 = 16384) on the two-pass flash path: the workspace holds no B x HW x HW term (S
+    alone would be 1 GiB per image) and the output matches a float64 reference formed in
+    query chunks on the GPU (torch, S of 2048 queries at a time)."""
+    import network as net
+    from rpst import _lib, ops
+    B, C, h, w = 1, 512, 128, 128
+    hw = h * w
+    mod = net.AEAModule(hw) if mode == "aea" else net.AEALReluModule(hw)
+    synth_(mod, 31)
+    hid = mod.f_psi[0].out_features
+    nbytes = _lib.load().rpst_adaptive_attention_workspace_size(B, C, hw, hid)
+    # T = sn W1^T, Z = cn^T T (f_psi's hidden layer: HW x HW/16 by the reference's design),
+    # the normalised features and 7 per-query vectors -- no B x HW x HW term (S: 1 GiB)
+    assert nbytes == 4 * (B * C * hid + B * hw * hid + 2 * B * C * hw + 7 * B * hw), nbytes
+    g = torch.Generator(device=cuda).manual_seed(5)
+    F, G, H = ((torch.rand((B, C, h, w), device=cuda, generator=g) * 2 - 1) * sc
+               for sc in (0.3, 0.3, 1.0))
+    c, s = (torch.rand((B, C, h, w), device=cuda, generator=g) for _ in range(2))
+    mod = mod.to(cuda)
+    with torch.no_grad():
+        out, cl, _, _ = ops.adaptive_attention(F, G, H, c, s, mod.f_psi, mod.mode, 50.0, 0.4,
+                                               0.5)
+    sd = {k: v.double().to(cuda) for k, v in state_dict_of(mod).items()}
+    F64, G64, H64 = (x.double().view(B, C, hw) for x in (F, G, H))
+    cn = torch.nn.functional.normalize(c.double().view(B, C, hw), dim=1)
+    sn = torch.nn.functional.normalize(s.double().view(B, C, hw), dim=1)
+    ref = torch.empty((B, C, hw), dtype=torch.float64, device=cuda)
+    ref_cl = torch.empty((B, hw, 1), dtype=torch.float64, device=cuda)
+    for q0 in range(0, hw, 2048):
+        qs = slice(q0, q0 + 2048)
+        P = torch.softmax(torch.bmm(F64[:, :, qs].transpose(1, 2), G64), -1)
+        A = torch.bmm(cn[:, :, qs].transpose(1, 2), sn)
+        Q, clamp = R.aea(A, P, sd, "", mode)
+        ref[:, :, qs] = torch.bmm(H64, Q.transpose(1, 2))
+        ref_cl[:, qs] = clamp.view(B, -1, 1)
+    assert rel_l2(cl, ref_cl) < 1e-6
+    assert rel_l2(out, ref.view(B, C, h, w)) < 1e-5
 
 
 @pytest.mark.parametrize("mode", MODES)

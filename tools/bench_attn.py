@@ -3,6 +3,7 @@ softmax(S)^T) at the SAModel.test() shape (B images, C = 512, HW = 4096) against
 (torch.bmm) for the two GEMMs, HIP events on the launch stream.
 
     python tools/bench_attn.py [--batch 32] [--reps 5]
+(+ adaptive_attention, both AEA modules, at the same shape)
     rocprofv3 --kernel-trace --stats -d gpurun_out/attn -- python3 tools/bench_attn.py
 """
 import argparse
@@ -50,11 +51,27 @@ def main():
     t_o = timed(lambda: torch.bmm(Hv, P.transpose(1, 2), out=O), args.reps)
     ref = torch.bmm(Hv, P.transpose(1, 2)).reshape(B, C, 64, 64)
     err = float((ops.sanet_attention(F, G, H) - ref).norm() / ref.norm())
+    del S, P, O, ref
+    torch.cuda.empty_cache()
+    # AdaptiveSANet (sanet.py:100-124) at the same shape, both clamp modules: two flash passes
+    # (statistics, then S recomputed with the clamp applied in registers) + the factored clamp
+    import network as net
+    ada = {}
+    c = torch.rand(B, C, 64, 64, device=dev, generator=g)
+    s = torch.rand(B, C, 64, 64, device=dev, generator=g)
+    torch.set_grad_enabled(False)  # bare kernel ops (the f_psi weights require grad)
+    for mode in ("aea", "relu"):
+        mod = (net.AEAModule(hw) if mode == "aea" else net.AEALReluModule(hw)).to(dev)
+        t = timed(lambda: ops.adaptive_attention(F, G, H, c, s, mod.f_psi, mod.mode, 50.0, 0.4,
+                                                 0.5), args.reps)
+        # executed FLOP: pass 1 2 HW^2 C, pass 2 4 HW^2 C, clamp 4 C hid HW
+        ada[mode] = {"ms": round(t, 3),
+                     "tflops": round(B * (6.0 * hw * hw * C + 4.0 * C * (hw // 16) * hw) / t / 1e9, 1)}
     print(json.dumps({"batch": B, "ours_ms": round(t_ours, 3),
                       "ours_tflops": round(flop / t_ours / 1e9, 1),
                       "rocblas_S_ms": round(t_s, 3), "rocblas_O_ms": round(t_o, 3),
                       "rocblas_gemms_tflops": round(flop / (t_s + t_o) / 1e9, 1),
-                      "rel_l2_vs_torch": err}))
+                      "rel_l2_vs_torch": err, "adaptive": ada}))
 
 
 if __name__ == "__main__":

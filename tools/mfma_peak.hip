@@ -1,7 +1,7 @@
 // MFMA throughput microbenchmark (gfx950): back-to-back independent MFMAs in registers.
 //   hipcc --offload-arch=gfx950 -O3 tools/mfma_peak.hip -o /tmp/mfma_peak && /tmp/mfma_peak
-// fp64 leg (the round-4 form, 4 chains per wave at one wave per SIMD per
-// block, read 49.5 TF/s while cov_syrk16_kernel already ran 62.8 on its SYRK count): sweeps
+// fp64 leg (the round-4 form read 49.2 TF/s while cov_syrk16_kernel
+// already ran 62.8 on its SYRK count -- the loop was measuring accumulator copies): sweeps
 // the independent accumulator chains per wave (ACC) and the waves per SIMD (blocks per CU),
 // on per-lane operands that are not constants (the clock holds higher on trivial data,
 // MI355X_MICROARCH.md DVFS item 1), and reports the best sustained rate of each form.
@@ -30,10 +30,15 @@ __global__ __launch_bounds__(256) void f64_loop(double* out, int iters, double a
   // two operand pairs per lane, alternated between chains (not one broadcast constant)
   const double a0 = a + 1e-3 * (threadIdx.x & 7), a1 = a - 1e-3 * (threadIdx.x & 3);
   const double b0 = b - 1e-3 * (threadIdx.x >> 5), b1 = b + 2e-3 * (threadIdx.x >> 4);
+  // tied in-place asm MFMA: the builtin's untied form made this loop copy every accumulator
+  // VGPR -> AGPR -> VGPR around the MFMAs each iteration (64 VALU moves per 4 MFMAs: the
+  // round-4 "ceiling" of 49.2 TF/s measured those moves); 12 + s_nop before the reads
   for (int it = 0; it < iters; ++it)
 #pragma unroll
     for (int i = 0; i < ACC; ++i)
-      acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64((i & 1) ? a1 : a0, (i & 2) ? b1 : b0, acc[i], 0, 0, 0);
+      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0"
+                   : "+v"(acc[i]) : "v"((i & 1) ? a1 : a0), "v"((i & 2) ? b1 : b0));
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   double s = 0;
   for (int i = 0; i < ACC; ++i) for (int r = 0; r < 4; ++r) s += acc[i][r];
   out[blockIdx.x * 256 + threadIdx.x] = s;
