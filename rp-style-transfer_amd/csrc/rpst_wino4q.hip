@@ -56,21 +56,6 @@ __device__ __forceinline__ float q_row16_sum(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
   return v;
 }
-// this lane's id, computed afresh where it is called (asm volatile: not hoisted or CSE'd).
-// The main loop re-derives every lane-dependent address from it once per iteration, so none
-// is live across the epilogue: there the allocator spilled them, and each spill reload's
-// compiler-inserted vmcnt(0) drained the in-flight DMA ring (cdna_hip_programming.md, glds
-// pitfalls). s_nop 1: the asm's VGPR write is invisible to the hazard recognizer.
-__device__ __forceinline__ int q_lane() {
-  int l;
-#if __HIP_DEVICE_COMPILE__
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\ts_nop 1"
-               : "=v"(l));
-#else
-  l = 0;
-#endif
-  return l;
-}
 // a wave-uniform value made opaque here (not hoisted out of the enclosing loop)
 __device__ __forceinline__ int q_launder(int v) {
 #if __HIP_DEVICE_COMPILE__
@@ -527,8 +512,7 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
 
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int wr = wave >> 2;
-  int ln = lane;  // the lane id the loop's addresses derive from (re-read per iteration)
+  const int k = lane >> 4, tn = lane & 15, wr = wave >> 2;
 
   // block -> (co-split group, column tile, row tile, image); XCD-swizzled
   int bid = xcd_swizzle(blockIdx.x, (int)gridDim.x);
@@ -603,10 +587,10 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     const bool live = g < G;
     const int so = q_mask((g * kQWS + pc * 256) * 4, live);
     if (i < 4) {
-      q_dma16(q_rsrc(w_img, wbytes, live), stg + pc * 256, ln * 16, so);
+      q_dma16(q_rsrc(w_img, wbytes, live), stg + pc * 256, lane * 16, so);
     } else {
       const bool real = pc < 36;
-      q_dma16(q_rsrc(w_img, wbytes, live && real), real ? stg + pc * 256 : dummy, ln * 16,
+      q_dma16(q_rsrc(w_img, wbytes, live && real), real ? stg + pc * 256 : dummy, lane * 16,
               q_mask(so, real));
     }
   };
@@ -621,7 +605,6 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     const int so = q_mask((int)((unsigned)c * in_plane * 4u), ok);
     float* xs = stg + (wv >> 1) * kQCS;
     const bool h1 = (wv & 1) != 0;
-    const int tid = wv * 64 + ln;
     if constexpr (WIDE) {
       q_dma16(r, xs + (h1 ? 512 : 0), poffs[0][tid], so);
       q_dma16(r, h1 ? dummy : xs + 256, poffs[1][tid], so);
@@ -642,9 +625,9 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
   const bool bst_all = !a.pool_out && (a.W & 3) == 0 &&
                        (int64_t)a.Cout * a.H * a.W * 4 < (1LL << 31);
   bool post_epi = false;
-  auto wait_ring = [&]() {
+  auto wait_ring = [&](bool first) {
     if (DBG & 128) return;
-    if (post_epi && bst_all) {
+    if (first && post_epi && bst_all) {
       if (wide) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
     } else if (wide) {
@@ -652,7 +635,7 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     } else {
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     }
-    post_epi = false;
+    if (first) post_epi = false;
   };
 
   // ---- prologue: P(0), P(1), W(0), P(2), P(3) -------------------------------------------
@@ -666,7 +649,7 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
   };
   if (wide) prologue(std::true_type{});
   else prologue(std::false_type{});
-  wait_ring();  // P(3) may stay in flight; conservative for P(2)
+  wait_ring(false);  // P(3) may stay in flight; conservative for P(2)
   q_lds_barrier();
 
   auto body = [&](auto Qc) {
@@ -679,8 +662,8 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     // lane (k, tn) reads rows 4 wr + QR .. + 4 of channel k of a patch, columns 4 tn .. + 7
     // (two conflict-free ds_read_b128; the empty asm keeps them whole, the compiler would
     // otherwise narrow them to the 5 floats a quarter uses, as bank-conflicted b32 reads)
+    const int roff = k * kQCS + (4 * wr + QR) * kQPS + 4 * tn;
     auto read_row = [&](const float* stg, int rr, float (&d)[8]) {
-      const int roff = (ln >> 4) * kQCS + (4 * wr + QR) * kQPS + 4 * (ln & 15);
       floatx4 u = *reinterpret_cast<const floatx4*>(stg + roff + rr * kQPS);
       floatx4 v = *reinterpret_cast<const floatx4*>(stg + roff + rr * kQPS + 4);
       asm("" : "+v"(u), "+v"(v));
@@ -721,16 +704,17 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
       for (int j = 0; j < 3; ++j) row_pass(u, j, V);
     }
 
-    int x = 0;  // global K step
+    const int woff = Q * 9 * 256 + lane * 4;  // this wave's A operands in a weight stage
+    int x = 0;                                // global K step
     // one K step: W(x) from wsx, P(x + 1) from psn (-> V(x + 1)), DMA W(x + 1) into wsn and
     // P(x + 4) into psx. MFMA groups in column-major position order, so the row pass of
     // column j overwrites V[j], V[3 + j], V[6 + j] after their last use.
-    auto step = [&](float* wsx, float* psn, float* wsn, float* psx, int ks) {
-      wait_ring();
+    // (first: the step that may follow an epilogue, the first of an iteration)
+    auto step = [&](float* wsx, float* psn, float* wsn, float* psx, int ks, bool first) {
+      wait_ring(first);
       if (DBG & 16) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else q_lds_barrier();  // W(x), P(x + 1) complete; every wave is done with step x - 1
       constexpr int ord[9] = {0, 3, 6, 1, 4, 7, 2, 5, 8};
-      const int woff = Q * 9 * 256 + ln * 4;  // this wave's A operands in a weight stage
       constexpr int kA = RPST_W4Q_AHEAD;  // A-operand groups read ahead
       float4 w4[9];
 #pragma unroll
@@ -811,7 +795,6 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
                    "+v"(acc[6][2]), "+v"(acc[6][3]), "+v"(acc[7][0]), "+v"(acc[7][1]),
                    "+v"(acc[7][2]), "+v"(acc[7][3]), "+v"(acc[8][0]), "+v"(acc[8][1]),
                    "+v"(acc[8][2]), "+v"(acc[8][3]));
-      const int lane = ln, k = ln >> 4, tn = ln & 15;
       const int co0 = ctile * kQCo + 16 * Q + 4 * k;
       // 6 passes (accumulator element pair rp, position row pt): each wave writes its 3
       // positions of row pt of the other quarters' blocks (elements 2 rp, 2 rp + 1) into ws1
@@ -897,11 +880,10 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     // values, and the compiler then renames every such MFMA's destination)
     int ks = 0, ct = ct0;
     for (int g = 0; g < G; g += 4) {
-      ln = q_lane();
-      step(ws0, ps1, ws1, ps0, ks);
-      step(ws1, ps2, ws0, ps1, ks + 1);
-      step(ws0, ps3, ws1, ps2, ks + 2);
-      step(ws1, ps0, ws0, ps3, ks + 3);
+      step(ws0, ps1, ws1, ps0, ks, true);
+      step(ws1, ps2, ws0, ps1, ks + 1, false);
+      step(ws0, ps3, ws1, ps2, ks + 2, false);
+      step(ws1, ps0, ws0, ps3, ks + 3, false);
       ks += 4;
       if (ks == K4) {
         epilogue(ct);
