@@ -377,6 +377,16 @@ int rpst_sanet_attention_backward(const float* F, const float* G, const float* H
                                   const float* dO, float* dF, float* dG, float* dH, int B, int C,
                                   int HWc, int HWs, void* workspace, size_t workspace_bytes,
                                   rpst_stream_t stream);
+/* The same gradients without the B x HWc x HWs terms (the training path): S and dP exist for
+ * 1024 keys at a time, in two passes over the key chunks (row max, sum exp and rowsum(dP P)
+ * first, then the gradients from the same, recomputed S and dP; dF summed in chunk order).
+ * Rows of at most 1024 keys run rpst_sanet_attention_backward (whose workspace size is then
+ * returned). Workspace: rpst_sanet_attention_backward_chunked_workspace_size(B, C, HWc, HWs). */
+size_t rpst_sanet_attention_backward_chunked_workspace_size(int B, int C, int HWc, int HWs);
+int rpst_sanet_attention_backward_chunked(const float* F, const float* G, const float* H,
+                                          const float* dO, float* dF, float* dG, float* dH,
+                                          int B, int C, int HWc, int HWs, void* workspace,
+                                          size_t workspace_bytes, rpst_stream_t stream);
 /* AdaptiveSANet attention backward (sanet.py:100-138 under autograd; AdaptiveSAModel trains
  * through it, train.py:118-119): with A the cosine affinity of content / style, c the f_psi
  * clamp, S = F^T G, P = softmax_rows(S) and Q = AEA(P) (mode 0 aea: sigmoid(scale (P - c)),

@@ -75,6 +75,7 @@ struct GemmArgs {
   // In-kernel split-K (BX_NONE only): grid z = batch * ks, z -> (batch z / ks, K chunk z % ks
   // of kc elements); C advances by sC per z, so each chunk writes its own partial.
   int ks = 1, kc = 0;
+  int accum = 0;  // epilogue adds to C (a sum over launches, in launch order)
 };
 
 template <int BX>
@@ -281,7 +282,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
         float v = acc[mt][nt][r] * cs;
         if (g.colbias) v += cb;
         if (g.act == 1) v = v > 0.f ? v : 0.2f * v;
-        if (m < g.M) C[(int64_t)m * g.ldc + n] = v;
+        if (m < g.M) {
+          float* cp = C + (int64_t)m * g.ldc + n;
+          *cp = g.accum ? *cp + v : v;
+        }
       }
   }
 }
@@ -370,6 +374,17 @@ __global__ __launch_bounds__(256) void softmax_bwd_logits_kernel(const float* __
   }
   dot = wave_sum(dot) / wave_sum(psum);
   for (int i = lane; i < L; i += 64) d[i] = expf(s[i] - m) * inv * (d[i] - dot);
+}
+
+// dS = P (dP - D) over one key chunk, in place over dP: P = exp(S - m) inv as in
+// softmax_bwd_logits_kernel, D the row's rowsum(dP P) from the first pass
+__global__ __launch_bounds__(256) void softmax_bwd_chunk_kernel(
+    const float* __restrict__ S, const float* __restrict__ rmax, const float* __restrict__ rinv,
+    const float* __restrict__ D, float* __restrict__ dP, int64_t n, int L) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = i / L;
+  dP[i] = expf(S[i] - rmax[r]) * rinv[r] * (dP[i] - D[r]);
 }
 
 // out[i] = sum_b in[b][i] (fixed order over b)
@@ -1014,6 +1029,150 @@ extern "C" int rpst_sanet_attention_backward(const float* F, const float* G, con
   GemmArgs gg{F, dP, dG, {}, nullptr, nullptr, 0, C, HWs, HWc, HWc, HWs, HWs, fc, ss, fs, 0};
   launch_gemm<LAY_RK, LAY_KR, BX_NONE>(gg, B, st);
   return launch_status("gemm_f32_kernel(dG=F dS)");
+}
+
+// ---- SANet attention backward over key chunks (no B x HW x HW workspace) ---------------
+// The same gradients with S and dP formed for attn_kc() = 1024 keys at a time, in two passes over the
+// key chunks. Pass 1: S_c = F^T G_c and dP_c = dO^T H_c, folded into each row's running
+// (max m, l = sum exp(S - m), dot = sum exp(S - m) dP) (attn_rows_merge_kernel, chunk
+// order). Pass 2: S_c and dP_c again (the same GEMMs on the same inputs: bit-identical),
+// dH_c = dO P_c with P = exp(S - m) / l formed while S_c is staged, dS_c = P (dP - dot / l)
+// in place, dF += G_c dS_c^T (accumulated in chunk order), dG_c = F dS_c. dot / l is
+// rowsum(dP P) over the row's own P, so every row of dS sums to zero to fp32 rounding (the
+// softmax's shift invariance: SANet's g.bias gradient, exactly 0, stays at rounding level --
+// a rowsum taken from the flash forward's O instead left 1.9e-4 of max|f.bias grad|,
+// against the 5e-5 bar). Cost: 14 HW^2 C FLOP per image against the single pass's 10; rows
+// of at most attn_kc() keys take the single pass (its S is then no larger than one chunk).
+// Workspace: S_c and dP_c (2 B HWc attn_kc()) + 3 B HWc row vectors.
+// (RPST_ATTN_KC overrides the chunk: A/B against the single pass, tests)
+static int attn_kc() {
+  static const int kc = [] {
+    const char* e = std::getenv("RPST_ATTN_KC");
+    const int v = (e && *e) ? std::atoi(e) : 1024;
+    return v >= 16 ? v / 4 * 4 : 1024;
+  }();
+  return kc;
+}
+
+// Fold one chunk's logits row into the running (m, l, dot) of that row; first: initialise.
+// One wave per row, fixed-order sums.
+__global__ __launch_bounds__(256) void attn_rows_merge_kernel(
+    const float* __restrict__ S, const float* __restrict__ dP, float* __restrict__ m,
+    float* __restrict__ l, float* __restrict__ dot, int64_t rows, int L, int first) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* s = S + row * L;
+  const float* d = dP + row * L;
+  float mx = -INFINITY;
+  for (int i = lane; i < L; i += 64) mx = fmaxf(mx, s[i]);
+  mx = wave_max(mx);
+  float ls = 0.f, ds = 0.f;
+  for (int i = lane; i < L; i += 64) {
+    const float e = expf(s[i] - mx);
+    ls += e;
+    ds = fmaf(e, d[i], ds);
+  }
+  ls = wave_sum(ls);
+  ds = wave_sum(ds);
+  if (lane == 0) {
+    if (first) {
+      m[row] = mx;
+      l[row] = ls;
+      dot[row] = ds;
+    } else {
+      const float m0 = m[row], mn = fmaxf(m0, mx);
+      const float a = expf(m0 - mn), b = expf(mx - mn);
+      m[row] = mn;
+      l[row] = l[row] * a + ls * b;
+      dot[row] = dot[row] * a + ds * b;
+    }
+  }
+}
+
+// l -> 1 / l, dot -> dot / l (the row's rowsum(dP P))
+__global__ void attn_rows_finish_kernel(float* __restrict__ l, float* __restrict__ dot,
+                                        int64_t rows) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows) return;
+  const float inv = 1.f / l[i];
+  l[i] = inv;
+  dot[i] *= inv;
+}
+
+extern "C" size_t rpst_sanet_attention_backward_chunked_workspace_size(int B, int C, int HWc,
+                                                                       int HWs) {
+  if (B <= 0 || C <= 0 || HWc <= 0 || HWs <= 0) return 0;
+  if (HWs <= attn_kc()) return rpst_sanet_attention_backward_workspace_size(B, HWc, HWs);
+  return sizeof(float) * (2 * (size_t)B * HWc * attn_kc() + 3 * (size_t)B * HWc);
+}
+
+extern "C" int rpst_sanet_attention_backward_chunked(const float* F, const float* G,
+                                                     const float* H, const float* dO, float* dF,
+                                                     float* dG, float* dH, int B, int C, int HWc,
+                                                     int HWs, void* workspace,
+                                                     size_t workspace_bytes,
+                                                     rpst_stream_t stream) {
+  RPST_REQUIRE(F && G && H && dO && dF && dG && dH,
+               "sanet_attention_backward_chunked: null pointer");
+  RPST_REQUIRE(B > 0 && C > 0 && HWc > 0 && HWs > 0 && B <= 65535,
+               "sanet_attention_backward_chunked: bad shape B=%d C=%d HW=%d/%d", B, C, HWc, HWs);
+  if (HWs <= attn_kc())  // one chunk: the single pass
+    return rpst_sanet_attention_backward(F, G, H, dO, dF, dG, dH, B, C, HWc, HWs, workspace,
+                                         workspace_bytes, stream);
+  if (!workspace ||
+      workspace_bytes < rpst_sanet_attention_backward_chunked_workspace_size(B, C, HWc, HWs)) {
+    set_error("sanet_attention_backward_chunked: workspace too small");
+    return RPST_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  const int kc = attn_kc();
+  const int64_t fc = (int64_t)C * HWc, fs = (int64_t)C * HWs, sc = (int64_t)HWc * kc;
+  const int64_t rows = (int64_t)B * HWc;
+  float* Sc = static_cast<float*>(workspace);
+  float* dPc = Sc + (size_t)B * sc;
+  float* rmax = dPc + (size_t)B * sc;
+  float* rinv = rmax + rows;  // l, then 1 / l
+  float* D = rinv + rows;     // dot, then dot / l
+  auto logits = [&](int j0, int n) -> int {
+    const int64_t sn = (int64_t)HWc * n;
+    GemmArgs g1{F, G + j0, Sc, {}, nullptr, nullptr, 0, HWc, n, C, HWc, HWs, n, fc, fs, sn, 0};
+    launch_gemm<LAY_KR, LAY_KR, BX_NONE>(g1, B, st);
+    if (int e = launch_status("gemm_f32_kernel(S_c=F^T G_c)")) return e;
+    GemmArgs gp{dO, H + j0, dPc, {}, nullptr, nullptr, 0, HWc, n, C, HWc, HWs, n, fc, fs, sn, 0};
+    launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gp, B, st);
+    return launch_status("gemm_f32_kernel(dP_c=dO^T H_c)");
+  };
+  for (int j0 = 0; j0 < HWs; j0 += kc) {  // pass 1: row statistics and rowsum(dP P)
+    const int n = std::min(kc, HWs - j0);
+    if (int e = logits(j0, n)) return e;
+    attn_rows_merge_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Sc, dPc, rmax, rinv, D,
+                                                                       rows, n, j0 == 0);
+    if (int e = launch_status("attn_rows_merge_kernel")) return e;
+  }
+  attn_rows_finish_kernel<<<(unsigned)((rows + 255) / 256), 256, 0, st>>>(rinv, D, rows);
+  if (int e = launch_status("attn_rows_finish_kernel")) return e;
+  for (int j0 = 0; j0 < HWs; j0 += kc) {  // pass 2: the gradients
+    const int n = std::min(kc, HWs - j0);
+    const int64_t sn = (int64_t)HWc * n;
+    if (int e = logits(j0, n)) return e;
+    GemmArgs gh{dO, Sc, dH + j0, {rmax, rinv, nullptr, nullptr, 0.f}, nullptr, nullptr, 0,
+                C, n, HWc, HWc, n, HWs, fc, sn, fs, HWc};
+    launch_gemm<LAY_RK, LAY_KR, BX_PROB>(gh, B, st);
+    if (int e = launch_status("gemm_f32_kernel(dH_c=dO P_c)")) return e;
+    const int64_t tot = (int64_t)B * sn;
+    softmax_bwd_chunk_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(Sc, rmax, rinv, D,
+                                                                            dPc, tot, n);
+    if (int e = launch_status("softmax_bwd_chunk_kernel")) return e;
+    GemmArgs gf{G + j0, dPc, dF, {}, nullptr, nullptr, 0, C, HWc, n, HWs, n, HWc, fs, sn, fc, 0};
+    gf.accum = j0 > 0;
+    launch_gemm<LAY_RK, LAY_RK, BX_NONE>(gf, B, st);
+    if (int e = launch_status("gemm_f32_kernel(dF+=G_c dS_c^T)")) return e;
+    GemmArgs gg{F, dPc, dG + j0, {}, nullptr, nullptr, 0, C, n, HWc, HWc, n, HWs, fc, sn, fs, 0};
+    launch_gemm<LAY_RK, LAY_KR, BX_NONE>(gg, B, st);
+    if (int e = launch_status("gemm_f32_kernel(dG_c=F dS_c)")) return e;
+  }
+  return RPST_OK;
 }
 
 // K (pixel) chunks per image of the 1x1 weight gradient: the per-image GEMM has only

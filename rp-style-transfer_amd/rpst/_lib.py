@@ -77,6 +77,9 @@ SIGNATURES = {
     "rpst_sanet_attention_backward_workspace_size": (_SZ, [_I, _I, _I]),
     "rpst_sanet_attention_backward": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _SZ,
                                            _P]),
+    "rpst_sanet_attention_backward_chunked_workspace_size": (_SZ, [_I, _I, _I, _I]),
+    "rpst_sanet_attention_backward_chunked": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
+                                                   _P, _SZ, _P]),
     "rpst_adaptive_attention_backward_workspace_size": (_SZ, [_I, _I, _I, _I]),
     "rpst_adaptive_attention_backward": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _F,
                                               _F, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I,

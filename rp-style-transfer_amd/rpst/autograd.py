@@ -574,12 +574,14 @@ def _sanet_backward(m, saved, d_out, grads):
     _acc(grads, m.out_conv.weight, dw)
     _acc(grads, m.out_conv.bias, db)
     dO = ops.conv2d(d_out, flip_packed_weight(m.out_conv), None, c, 1).contiguous()
-    # attention gradients on gemm_f32_kernel (rpst_sanet_attention_backward): S = F^T G, the
-    # softmax probabilities formed while S is staged, dS = P (dP - rowsum(dP P))
+    # attention gradients (rpst_sanet_attention_backward_chunked): S = F^T G and dP for 1024
+    # keys at a time on gemm_f32_kernel (row statistics and rowsum(dP P) in a first pass),
+    # the softmax probabilities formed while S is staged, dS = P (dP - rowsum(dP P)) -- no
+    # B x HW x HW workspace
     dF, dG, dH = torch.empty_like(F), torch.empty_like(G), torch.empty_like(H)
-    nbytes = _lib.load().rpst_sanet_attention_backward_workspace_size(b, hwc, hws)
+    nbytes = _lib.load().rpst_sanet_attention_backward_chunked_workspace_size(b, c, hwc, hws)
     ws = _ws(nbytes, F)
-    _lib.call("rpst_sanet_attention_backward", F.data_ptr(), G.data_ptr(), H.data_ptr(),
+    _lib.call("rpst_sanet_attention_backward_chunked", F.data_ptr(), G.data_ptr(), H.data_ptr(),
               dO.data_ptr(), dF.data_ptr(), dG.data_ptr(), dH.data_ptr(), b, c, hwc, hws,
               ws.data_ptr(), nbytes, _stream(F))
     for conv, dY, X in ((m.f, dF, Fn), (m.g, dG, Gn), (m.h, dH, s)):
