@@ -376,17 +376,6 @@ __global__ __launch_bounds__(256) void softmax_bwd_logits_kernel(const float* __
   for (int i = lane; i < L; i += 64) d[i] = expf(s[i] - m) * inv * (d[i] - dot);
 }
 
-// dS = P (dP - D) over one key chunk, in place over dP: P = exp(S - m) inv as in
-// softmax_bwd_logits_kernel, D the row's rowsum(dP P) from the first pass
-__global__ __launch_bounds__(256) void softmax_bwd_chunk_kernel(
-    const float* __restrict__ S, const float* __restrict__ rmax, const float* __restrict__ rinv,
-    const float* __restrict__ D, float* __restrict__ dP, int64_t n, int L) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const int64_t r = i / L;
-  dP[i] = expf(S[i] - rmax[r]) * rinv[r] * (dP[i] - D[r]);
-}
-
 // out[i] = sum_b in[b][i] (fixed order over b)
 __global__ void batch_sum_kernel(const float* __restrict__ in, float* __restrict__ out,
                                  int64_t per, int nb) {
@@ -424,6 +413,22 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const float* __restric
   if ((tid & 63) == 0) part[tid >> 6] = s;
   __syncthreads();
   if (tid == 0) db[c] = ((part[0] + part[1]) + part[2]) + part[3];
+}
+
+// chunk-local row vectors of a query chunk: dst[b][i] = src[b][q0 + i] and back
+__global__ void rows_gather_kernel(const float* __restrict__ src, float* __restrict__ dst, int B,
+                                   int HW, int q0, int n) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)B * n) return;
+  const int64_t b = t / n;
+  dst[t] = src[b * HW + q0 + (t - b * n)];
+}
+__global__ void rows_scatter_kernel(const float* __restrict__ src, float* __restrict__ dst, int B,
+                                    int HW, int q0, int n) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)B * n) return;
+  const int64_t b = t / n;
+  dst[b * HW + q0 + (t - b * n)] = src[t];
 }
 
 // ---- AdaptiveSANet backward (sanet.py:100-138 under autograd; train.py:118-119 trains it) --
@@ -1031,80 +1036,29 @@ extern "C" int rpst_sanet_attention_backward(const float* F, const float* G, con
   return launch_status("gemm_f32_kernel(dG=F dS)");
 }
 
-// ---- SANet attention backward over key chunks (no B x HW x HW workspace) ---------------
-// The same gradients with S and dP formed for attn_kc() = 1024 keys at a time, in two passes over the
-// key chunks. Pass 1: S_c = F^T G_c and dP_c = dO^T H_c, folded into each row's running
-// (max m, l = sum exp(S - m), dot = sum exp(S - m) dP) (attn_rows_merge_kernel, chunk
-// order). Pass 2: S_c and dP_c again (the same GEMMs on the same inputs: bit-identical),
-// dH_c = dO P_c with P = exp(S - m) / l formed while S_c is staged, dS_c = P (dP - dot / l)
-// in place, dF += G_c dS_c^T (accumulated in chunk order), dG_c = F dS_c. dot / l is
-// rowsum(dP P) over the row's own P, so every row of dS sums to zero to fp32 rounding (the
-// softmax's shift invariance: SANet's g.bias gradient, exactly 0, stays at rounding level --
-// a rowsum taken from the flash forward's O instead left 1.9e-4 of max|f.bias grad|,
-// against the 5e-5 bar). Cost: 14 HW^2 C FLOP per image against the single pass's 10; rows
-// of at most attn_kc() keys take the single pass (its S is then no larger than one chunk).
-// Workspace: S_c and dP_c (2 B HWc attn_kc()) + 3 B HWc row vectors.
-// (RPST_ATTN_KC overrides the chunk: A/B against the single pass, tests)
-static int attn_kc() {
-  static const int kc = [] {
-    const char* e = std::getenv("RPST_ATTN_KC");
+// ---- SANet attention backward over query chunks (no B x HW x HW workspace) -------------
+// The same gradients with S and dP formed for attn_qc() = 1024 queries (full rows) at a time:
+// per chunk S_q = F_q^T G, the row statistics, dH += dO_q P_q (P formed while S_q is staged),
+// dP_q = dO_q^T H, dS_q = P (dP - rowsum(dP P)) in place (softmax_bwd_logits_kernel: whole
+// rows, so every row of dS sums to zero to rounding as in the single pass), dF_q = G dS_q^T,
+// dG += F_q dS_q; dH and dG sum the chunks in order. S, its statistics and dS are the single
+// pass's bit for bit (the GEMM's k order does not depend on M); 10 HW^2 C FLOP per image like
+// the single pass. Workspace: S_q and dP_q (2 B qc HWs) + 2 B qc row vectors.
+// (RPST_ATTN_QC overrides the chunk: A/B against the single pass, tests.)
+static int attn_qc() {
+  static const int qc = [] {
+    const char* e = std::getenv("RPST_ATTN_QC");
     const int v = (e && *e) ? std::atoi(e) : 1024;
     return v >= 16 ? v / 4 * 4 : 1024;
   }();
-  return kc;
-}
-
-// Fold one chunk's logits row into the running (m, l, dot) of that row; first: initialise.
-// One wave per row, fixed-order sums.
-__global__ __launch_bounds__(256) void attn_rows_merge_kernel(
-    const float* __restrict__ S, const float* __restrict__ dP, float* __restrict__ m,
-    float* __restrict__ l, float* __restrict__ dot, int64_t rows, int L, int first) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
-  const float* s = S + row * L;
-  const float* d = dP + row * L;
-  float mx = -INFINITY;
-  for (int i = lane; i < L; i += 64) mx = fmaxf(mx, s[i]);
-  mx = wave_max(mx);
-  float ls = 0.f, ds = 0.f;
-  for (int i = lane; i < L; i += 64) {
-    const float e = expf(s[i] - mx);
-    ls += e;
-    ds = fmaf(e, d[i], ds);
-  }
-  ls = wave_sum(ls);
-  ds = wave_sum(ds);
-  if (lane == 0) {
-    if (first) {
-      m[row] = mx;
-      l[row] = ls;
-      dot[row] = ds;
-    } else {
-      const float m0 = m[row], mn = fmaxf(m0, mx);
-      const float a = expf(m0 - mn), b = expf(mx - mn);
-      m[row] = mn;
-      l[row] = l[row] * a + ls * b;
-      dot[row] = dot[row] * a + ds * b;
-    }
-  }
-}
-
-// l -> 1 / l, dot -> dot / l (the row's rowsum(dP P))
-__global__ void attn_rows_finish_kernel(float* __restrict__ l, float* __restrict__ dot,
-                                        int64_t rows) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= rows) return;
-  const float inv = 1.f / l[i];
-  l[i] = inv;
-  dot[i] *= inv;
+  return qc;
 }
 
 extern "C" size_t rpst_sanet_attention_backward_chunked_workspace_size(int B, int C, int HWc,
                                                                        int HWs) {
   if (B <= 0 || C <= 0 || HWc <= 0 || HWs <= 0) return 0;
-  if (HWs <= attn_kc()) return rpst_sanet_attention_backward_workspace_size(B, HWc, HWs);
-  return sizeof(float) * (2 * (size_t)B * HWc * attn_kc() + 3 * (size_t)B * HWc);
+  const size_t qc = (size_t)std::min(HWc, attn_qc());
+  return sizeof(float) * (2 * (size_t)B * qc * HWs + 2 * (size_t)B * qc);
 }
 
 extern "C" int rpst_sanet_attention_backward_chunked(const float* F, const float* G,
@@ -1117,60 +1071,44 @@ extern "C" int rpst_sanet_attention_backward_chunked(const float* F, const float
                "sanet_attention_backward_chunked: null pointer");
   RPST_REQUIRE(B > 0 && C > 0 && HWc > 0 && HWs > 0 && B <= 65535,
                "sanet_attention_backward_chunked: bad shape B=%d C=%d HW=%d/%d", B, C, HWc, HWs);
-  if (HWs <= attn_kc())  // one chunk: the single pass
-    return rpst_sanet_attention_backward(F, G, H, dO, dF, dG, dH, B, C, HWc, HWs, workspace,
-                                         workspace_bytes, stream);
   if (!workspace ||
       workspace_bytes < rpst_sanet_attention_backward_chunked_workspace_size(B, C, HWc, HWs)) {
     set_error("sanet_attention_backward_chunked: workspace too small");
     return RPST_EWORKSPACE;
   }
   hipStream_t st = as_stream(stream);
-  const int kc = attn_kc();
-  const int64_t fc = (int64_t)C * HWc, fs = (int64_t)C * HWs, sc = (int64_t)HWc * kc;
-  const int64_t rows = (int64_t)B * HWc;
-  float* Sc = static_cast<float*>(workspace);
-  float* dPc = Sc + (size_t)B * sc;
-  float* rmax = dPc + (size_t)B * sc;
-  float* rinv = rmax + rows;  // l, then 1 / l
-  float* D = rinv + rows;     // dot, then dot / l
-  auto logits = [&](int j0, int n) -> int {
-    const int64_t sn = (int64_t)HWc * n;
-    GemmArgs g1{F, G + j0, Sc, {}, nullptr, nullptr, 0, HWc, n, C, HWc, HWs, n, fc, fs, sn, 0};
+  const int qc = std::min(HWc, attn_qc());
+  const int64_t fc = (int64_t)C * HWc, fs = (int64_t)C * HWs, sq = (int64_t)qc * HWs;
+  float* Sq = static_cast<float*>(workspace);
+  float* dPq = Sq + (size_t)B * sq;
+  float* rmax = dPq + (size_t)B * sq;
+  float* rinv = rmax + (size_t)B * qc;
+  for (int q0 = 0; q0 < HWc; q0 += qc) {
+    const int n = std::min(qc, HWc - q0);
+    const int64_t sn = (int64_t)n * HWs, rows = (int64_t)B * n;
+    GemmArgs g1{F + q0, G, Sq, {}, nullptr, nullptr, 0, n, HWs, C, HWc, HWs, HWs, fc, fs, sn, 0};
     launch_gemm<LAY_KR, LAY_KR, BX_NONE>(g1, B, st);
-    if (int e = launch_status("gemm_f32_kernel(S_c=F^T G_c)")) return e;
-    GemmArgs gp{dO, H + j0, dPc, {}, nullptr, nullptr, 0, HWc, n, C, HWc, HWs, n, fc, fs, sn, 0};
-    launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gp, B, st);
-    return launch_status("gemm_f32_kernel(dP_c=dO^T H_c)");
-  };
-  for (int j0 = 0; j0 < HWs; j0 += kc) {  // pass 1: row statistics and rowsum(dP P)
-    const int n = std::min(kc, HWs - j0);
-    if (int e = logits(j0, n)) return e;
-    attn_rows_merge_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Sc, dPc, rmax, rinv, D,
-                                                                       rows, n, j0 == 0);
-    if (int e = launch_status("attn_rows_merge_kernel")) return e;
-  }
-  attn_rows_finish_kernel<<<(unsigned)((rows + 255) / 256), 256, 0, st>>>(rinv, D, rows);
-  if (int e = launch_status("attn_rows_finish_kernel")) return e;
-  for (int j0 = 0; j0 < HWs; j0 += kc) {  // pass 2: the gradients
-    const int n = std::min(kc, HWs - j0);
-    const int64_t sn = (int64_t)HWc * n;
-    if (int e = logits(j0, n)) return e;
-    GemmArgs gh{dO, Sc, dH + j0, {rmax, rinv, nullptr, nullptr, 0.f}, nullptr, nullptr, 0,
-                C, n, HWc, HWc, n, HWs, fc, sn, fs, HWc};
+    if (int e = launch_status("gemm_f32_kernel(S_q=F_q^T G)")) return e;
+    rowstats_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Sq, rmax, rinv, rows, HWs);
+    if (int e = launch_status("rowstats_kernel")) return e;
+    GemmArgs gh{dO + q0, Sq, dH, {rmax, rinv, nullptr, nullptr, 0.f}, nullptr, nullptr, 0,
+                C, HWs, n, HWc, HWs, HWs, fc, sn, fs, n};
+    gh.accum = q0 > 0;
     launch_gemm<LAY_RK, LAY_KR, BX_PROB>(gh, B, st);
-    if (int e = launch_status("gemm_f32_kernel(dH_c=dO P_c)")) return e;
-    const int64_t tot = (int64_t)B * sn;
-    softmax_bwd_chunk_kernel<<<(unsigned)((tot + 255) / 256), 256, 0, st>>>(Sc, rmax, rinv, D,
-                                                                            dPc, tot, n);
-    if (int e = launch_status("softmax_bwd_chunk_kernel")) return e;
-    GemmArgs gf{G + j0, dPc, dF, {}, nullptr, nullptr, 0, C, HWc, n, HWs, n, HWc, fs, sn, fc, 0};
-    gf.accum = j0 > 0;
+    if (int e = launch_status("gemm_f32_kernel(dH+=dO_q P_q)")) return e;
+    GemmArgs gp{dO + q0, H, dPq, {}, nullptr, nullptr, 0, n, HWs, C, HWc, HWs, HWs, fc, fs, sn, 0};
+    launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gp, B, st);
+    if (int e = launch_status("gemm_f32_kernel(dP_q=dO_q^T H)")) return e;
+    softmax_bwd_logits_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Sq, rmax, rinv, dPq,
+                                                                          rows, HWs);
+    if (int e = launch_status("softmax_bwd_logits_kernel")) return e;
+    GemmArgs gf{G, dPq, dF + q0, {}, nullptr, nullptr, 0, C, n, HWs, HWs, HWs, HWc, fs, sn, fc, 0};
     launch_gemm<LAY_RK, LAY_RK, BX_NONE>(gf, B, st);
-    if (int e = launch_status("gemm_f32_kernel(dF+=G_c dS_c^T)")) return e;
-    GemmArgs gg{F, dPc, dG + j0, {}, nullptr, nullptr, 0, C, n, HWc, HWc, n, HWs, fc, sn, fs, 0};
+    if (int e = launch_status("gemm_f32_kernel(dF_q=G dS_q^T)")) return e;
+    GemmArgs gg{F + q0, dPq, dG, {}, nullptr, nullptr, 0, C, HWs, n, HWc, HWs, HWs, fc, sn, fs, 0};
+    gg.accum = q0 > 0;
     launch_gemm<LAY_RK, LAY_KR, BX_NONE>(gg, B, st);
-    if (int e = launch_status("gemm_f32_kernel(dG_c=F dS_c)")) return e;
+    if (int e = launch_status("gemm_f32_kernel(dG+=F_q dS_q)")) return e;
   }
   return RPST_OK;
 }
@@ -1225,13 +1163,13 @@ extern "C" int rpst_conv1x1_wgrad(const float* x, const float* dy, float* dw, fl
 extern "C" size_t rpst_adaptive_attention_backward_workspace_size(int B, int C, int HW,
                                                                   int hidden) {
   if (B <= 0 || C <= 0 || HW <= 0 || hidden <= 0) return 0;
-  const size_t hw2 = (size_t)B * HW * HW;
+  const size_t qc = (size_t)std::min(HW, attn_qc());
   const size_t chunks = ((size_t)B * HW + kColChunk - 1) / kColChunk;
-  // (the first region holds T and then R, C x hidden per image, never the affinity) + the
-  // per-image dW1 partials and the column-sum chunk partials
-  return sizeof(float) * ((size_t)B * C * hidden + 2 * hw2 + 2 * (size_t)B * HW * hidden +
-                          2 * (size_t)B * C * HW +
-                          8 * (size_t)B * HW + (size_t)B * hidden * HW +
+  // (the first region holds T and then R, C x hidden per image, never the affinity) + S and
+  // dQ of one query chunk + the per-image dW1 partials and the column-sum chunk partials
+  return sizeof(float) * ((size_t)B * C * hidden + 2 * (size_t)B * qc * HW +
+                          2 * (size_t)B * HW * hidden + 2 * (size_t)B * C * HW +
+                          3 * (size_t)B * HW + 6 * (size_t)B * qc + (size_t)B * hidden * HW +
                           3 * (size_t)(hidden + 1) * chunks);
 }
 
@@ -1255,22 +1193,25 @@ extern "C" int rpst_adaptive_attention_backward(
     return RPST_EWORKSPACE;
   }
   hipStream_t st = as_stream(stream);
-  const int64_t hw2 = (int64_t)HW * HW, fhw = (int64_t)C * HW, rows = (int64_t)B * HW;
+  const int qc = std::min(HW, attn_qc());
+  const int64_t fhw = (int64_t)C * HW, rows = (int64_t)B * HW, sq = (int64_t)qc * HW;
   float* Aff = static_cast<float*>(workspace);  // T, then R (C x hidden per image)
-  float* S = Aff + (size_t)B * C * hidden;
-  float* dQ = S + (size_t)B * hw2;
-  float* Z = dQ + (size_t)B * hw2;
+  float* Sq = Aff + (size_t)B * C * hidden;     // S and dQ of one query chunk
+  float* dQq = Sq + (size_t)B * sq;
+  float* Z = dQq + (size_t)B * sq;
   float* du = Z + (size_t)rows * hidden;
   float* cn = du + (size_t)rows * hidden;
   float* sn = cn + (size_t)B * fhw;
-  float* rmax = sn + (size_t)B * fhw;
-  float* rinv = rmax + rows;
-  float* clamp = rinv + rows;
-  float* m2 = clamp + rows;
-  float* inv2 = m2 + rows;
-  float* dc = inv2 + rows;
+  float* clamp = sn + (size_t)B * fhw;
+  float* dc = clamp + rows;
   float* dt = dc + rows;
-  float* w1part = dt + rows;                               // [B][hidden][HW]
+  float* rmax = dt + rows;  // per query chunk: [B][qc] each
+  float* rinv = rmax + (size_t)B * qc;
+  float* clq = rinv + (size_t)B * qc;
+  float* m2 = clq + (size_t)B * qc;
+  float* inv2 = m2 + (size_t)B * qc;
+  float* dcq = inv2 + (size_t)B * qc;
+  float* w1part = dcq + (size_t)B * qc;                    // [B][hidden][HW]
   float* cpart = w1part + (size_t)B * hidden * HW;         // [chunks][3][hidden + 1]
   // forward quantities: clamp (and Z) as the forward forms them (the affinity folded into
   // f_psi's first Linear; T in the Aff region), logits, softmax / relu-softmax statistics
@@ -1278,35 +1219,45 @@ extern "C" int rpst_adaptive_attention_backward(
   if (int e = clamp_values_factored(cn, sn, w1, b1, w2, b2, hidden, mode, from, interval, Aff,
                                     Z, clamp, B, C, HW, st))
     return e;
-  GemmArgs g1{F, G, S, {}, nullptr, nullptr, 0, HW, HW, C, HW, HW, HW, fhw, fhw, hw2, 0};
-  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(g1, B, st);
-  if (int e = launch_status("gemm_f32_kernel(S=F^T G)")) return e;
-  rowstats_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rmax, rinv, rows, HW);
-  if (int e = launch_status("rowstats_kernel")) return e;
-  if (mode == 1) {
-    rowstats_relu_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rmax, rinv, clamp, m2,
-                                                                     inv2, rows, HW);
-    if (int e = launch_status("rowstats_relu_kernel")) return e;
+  // attention part over query chunks of whole rows (as rpst_sanet_attention_backward_chunked):
+  // S_q, its softmax / relu-softmax statistics, dH += dO_q Q_q, dQ_q = dO_q^T H -> dS_q and
+  // dc (aea_bwd_rows_kernel on whole rows), dF_q = G dS_q^T, dG += F_q dS_q
+  for (int q0 = 0; q0 < HW; q0 += qc) {
+    const int n = std::min(qc, HW - q0);
+    const int64_t sn_ = (int64_t)n * HW, rq = (int64_t)B * n;
+    const unsigned rb = (unsigned)((rq + 255) / 256), wb = (unsigned)((rq + 3) / 4);
+    GemmArgs g1{F + q0, G, Sq, {}, nullptr, nullptr, 0, n, HW, C, HW, HW, HW, fhw, fhw, sn_, 0};
+    launch_gemm<LAY_KR, LAY_KR, BX_NONE>(g1, B, st);
+    if (int e = launch_status("gemm_f32_kernel(S_q=F_q^T G)")) return e;
+    rowstats_kernel<<<wb, 256, 0, st>>>(Sq, rmax, rinv, rq, HW);
+    if (int e = launch_status("rowstats_kernel")) return e;
+    rows_gather_kernel<<<rb, 256, 0, st>>>(clamp, clq, B, HW, q0, n);
+    if (int e = launch_status("rows_gather_kernel")) return e;
+    if (mode == 1) {
+      rowstats_relu_kernel<<<wb, 256, 0, st>>>(Sq, rmax, rinv, clq, m2, inv2, rq, HW);
+      if (int e = launch_status("rowstats_relu_kernel")) return e;
+    }
+    RowVec rv{rmax, rinv, clq, m2, scale, inv2};
+    GemmArgs gh{dO + q0, Sq, dH, rv, nullptr, nullptr, 0, C, HW, n, HW, HW, HW, fhw, sn_, fhw, n};
+    gh.accum = q0 > 0;
+    if (mode == 0) launch_gemm<LAY_RK, LAY_KR, BX_AEA>(gh, B, st);
+    else launch_gemm<LAY_RK, LAY_KR, BX_AEARQ>(gh, B, st);
+    if (int e = launch_status("gemm_f32_kernel(dH+=dO_q Q_q)")) return e;
+    GemmArgs gq{dO + q0, H, dQq, {}, nullptr, nullptr, 0, n, HW, C, HW, HW, HW, fhw, fhw, sn_, 0};
+    launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gq, B, st);
+    if (int e = launch_status("gemm_f32_kernel(dQ_q=dO_q^T H)")) return e;
+    aea_bwd_rows_kernel<<<wb, 256, 0, st>>>(Sq, rv, dQq, dcq, mode, rq, HW);
+    if (int e = launch_status("aea_bwd_rows_kernel")) return e;
+    rows_scatter_kernel<<<rb, 256, 0, st>>>(dcq, dc, B, HW, q0, n);
+    if (int e = launch_status("rows_scatter_kernel")) return e;
+    GemmArgs gf{G, dQq, dF + q0, {}, nullptr, nullptr, 0, C, n, HW, HW, HW, HW, fhw, sn_, fhw, 0};
+    launch_gemm<LAY_RK, LAY_RK, BX_NONE>(gf, B, st);
+    if (int e = launch_status("gemm_f32_kernel(dF_q=G dS_q^T)")) return e;
+    GemmArgs gg{F + q0, dQq, dG, {}, nullptr, nullptr, 0, C, HW, n, HW, HW, HW, fhw, sn_, fhw, 0};
+    gg.accum = q0 > 0;
+    launch_gemm<LAY_RK, LAY_KR, BX_NONE>(gg, B, st);
+    if (int e = launch_status("gemm_f32_kernel(dG+=F_q dS_q)")) return e;
   }
-  RowVec rv{rmax, rinv, clamp, m2, scale, inv2};
-  // dH = dO Q (Q formed while S is staged: KR staging, the query is the k index)
-  GemmArgs gh{dO, S, dH, rv, nullptr, nullptr, 0, C, HW, HW, HW, HW, HW, fhw, hw2, fhw, HW};
-  if (mode == 0) launch_gemm<LAY_RK, LAY_KR, BX_AEA>(gh, B, st);
-  else launch_gemm<LAY_RK, LAY_KR, BX_AEARQ>(gh, B, st);
-  if (int e = launch_status("gemm_f32_kernel(dH=dO Q)")) return e;
-  // dQ = dO^T H -> dS (in place) and dc
-  GemmArgs gq{dO, H, dQ, {}, nullptr, nullptr, 0, HW, HW, C, HW, HW, HW, fhw, fhw, hw2, 0};
-  launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gq, B, st);
-  if (int e = launch_status("gemm_f32_kernel(dQ=dO^T H)")) return e;
-  aea_bwd_rows_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(S, rv, dQ, dc, mode, rows, HW);
-  if (int e = launch_status("aea_bwd_rows_kernel")) return e;
-  // dF = G dS^T, dG = F dS
-  GemmArgs gf{G, dQ, dF, {}, nullptr, nullptr, 0, C, HW, HW, HW, HW, HW, fhw, hw2, fhw, 0};
-  launch_gemm<LAY_RK, LAY_RK, BX_NONE>(gf, B, st);
-  if (int e = launch_status("gemm_f32_kernel(dF=G dS^T)")) return e;
-  GemmArgs gg{F, dQ, dG, {}, nullptr, nullptr, 0, C, HW, HW, HW, HW, HW, fhw, hw2, fhw, 0};
-  launch_gemm<LAY_RK, LAY_KR, BX_NONE>(gg, B, st);
-  if (int e = launch_status("gemm_f32_kernel(dG=F dS)")) return e;
   // f_psi: dt, du, then dW1 = du^T Aff over all B * HW query rows (one GEMM), the column sums
   fpsi_bwd_rows_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(Z, w2, b2, dc, dt, du, rows,
                                                                    hidden, mode, interval);

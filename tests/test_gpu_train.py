@@ -481,10 +481,8 @@ def test_adaptive_samodel_training_gradients_match_reference(cuda, golden):
 def test_samodel_training_step_matches_cpu_autograd(cuda, shape):
     """Every transform / decoder gradient tensor against float64 CPU autograd of the oracle
     (oracle.samodel_grads), per-tensor rel-L2 <= 1e-4 (TOL_SOFTMAX_GRAD for SANet f / g).
-    (The key-chunked attention backward, HW > 1024, is checked against fp64 autograd in
-    tests/test_gpu_attn_bwd.py; at 272 x 272, relu4_1 = 1156 keys, it gives this test's
-    worst tensor, sanet4_1.f.weight, 4.25644e-3 where the single pass gives 4.25640e-3 --
-    the softmax conditioning of the larger image, not the chunking, profiles/r05.)"""
+    (The query-chunked attention backward, HW > 1024, is checked against fp64 autograd in
+    tests/test_gpu_attn_bwd.py.)"""
     from rpst import synth
     m = _sam_model(27, shape[-1], cuda)
     sd = {k: v.double() for k, v in state_dict_of(m).items()}
