@@ -32,13 +32,15 @@ import sys
 
 # kernels whose global reads are (predominantly) 16 B per lane: FETCH_SIZE is doubled
 WIDE_READ = ("plane_stats_kernel", "plane_apply_kernel", "rowmean_kernel", "wino4_mfma_kernel",
+             "wino4q_mfma_kernel",
              "cov_syrk_kernel<16, true>", "cov_syrk_kernel<8, true>", "cov_syrk_kernel<4, true>",
              "cov_syrk16_kernel<true>")
 # the kernels of one rpst_wct_params launch on fp32 features with C <= 256 (configs[2]):
 # covariance SYRK + finish, matrix functions (gemm_f64_kernel is not listed: the decoder's
 # mix-weight GEMM runs on it)
 WCT_KERNELS = ("cov_syrk_kernel", "cov_syrk16_kernel", "cov_finish_kernel", "matfun_kernel")
-CONV_MAIN = ("wino4_mfma_kernel", "wino_mfma_kernel", "conv_mfma_kernel", "conv3x3_narrow_kernel")
+CONV_MAIN = ("wino4_mfma_kernel", "wino4q_mfma_kernel", "wino_mfma_kernel", "conv_mfma_kernel",
+             "conv3x3_narrow_kernel")
 CONV_PREFIX = ("conv", "wino", "narrow")
 
 

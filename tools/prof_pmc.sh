@@ -15,11 +15,11 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 3 > $O/bench.json 2> $O/be
 cat $O/bench.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 60 rocprofv3 -L > $O/counters_list.txt 2>&1 || true
-B="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --layer-order $O/order.json"
+B="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-configs --layer-order $O/order.json"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- $B > $O/pmc_fetch.log 2>&1 || { tail $O/pmc_fetch.log; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- $B > $O/pmc_write.log 2>&1 || { tail $O/pmc_write.log; exit 1; }
 python3 $R/tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write $O/order.json $O/pmc_traffic.json
-B1="python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --layer-order $O/order1.json"
+B1="python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-configs --layer-order $O/order1.json"
 SQA="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
 SQB="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
 for p in A B; do
