@@ -320,6 +320,11 @@ def roofline_from_trace(summary, pmc_path=None):
         next((p for p in ("wino4", "wino", "wgrad", "narrow") if name.startswith(p)), ""),
         "conv_mfma_kernel")
     traffic = pmc_lookup("launches", name, pmc_path)
+    try:  # the kernel the profiled run dispatched for this launch (e.g. the quarter F(4x4) form)
+        with open(pmc_path) as f:
+            kname = json.load(f)["launches"][name]["kernel"].split("::")[-1].split("<")[0]
+    except (OSError, KeyError, TypeError, ValueError):
+        pass
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
             "traffic": traffic, "kernel": f"{kname} [{name}]",
