@@ -378,10 +378,10 @@ int rpst_sanet_attention_backward(const float* F, const float* G, const float* H
                                   int HWc, int HWs, void* workspace, size_t workspace_bytes,
                                   rpst_stream_t stream);
 /* The same gradients without the B x HWc x HWs terms (the training path): S and dP exist for
- * 1024 queries (whole rows) at a time; dF is written per query chunk, dH and dG are summed
+ * 2048 queries (whole rows) at a time; dF is written per query chunk, dH and dG are summed
  * over the chunks in order. S, its row statistics and dS are the single pass's bit for bit.
  * Workspace: rpst_sanet_attention_backward_chunked_workspace_size(B, C, HWc, HWs) =
- * 4 (2 B q HWs + 2 B q) bytes, q = min(HWc, 1024). */
+ * 4 (2 B q HWs + 2 B q) bytes, q = min(HWc, 2048). */
 size_t rpst_sanet_attention_backward_chunked_workspace_size(int B, int C, int HWc, int HWs);
 int rpst_sanet_attention_backward_chunked(const float* F, const float* G, const float* H,
                                           const float* dO, float* dF, float* dG, float* dH,
@@ -392,7 +392,7 @@ int rpst_sanet_attention_backward_chunked(const float* F, const float* G, const 
  * clamp, S = F^T G, P = softmax_rows(S) and Q = AEA(P) (mode 0 aea: sigmoid(scale (P - c)),
  * mode 1 relu: softmax_rows(relu(P - c))), O = H Q^T: from dO (B,C,HW) -> dF, dG, dH (B,C,HW)
  * and the f_psi gradients dw1 (hidden,HW), db1 (hidden), dw2 (hidden), db2 (1). Q and P are
- * formed from S where staged, never stored; S and dQ exist for 1024 queries (whole rows) at
+ * formed from S where staged, never stored; S and dQ exist for 2048 queries (whole rows) at
  * a time (no B x HW x HW term; dH, dG summed over the query chunks in order). Workspace:
  * rpst_adaptive_attention_backward_workspace_size(B, C, HW, hidden). */
 size_t rpst_adaptive_attention_backward_workspace_size(int B, int C, int HW, int hidden);

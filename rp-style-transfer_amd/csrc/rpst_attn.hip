@@ -573,23 +573,45 @@ __global__ void fpsi_colsum_final_kernel(const float* __restrict__ part, float* 
 
 // ---- AdaptiveSANet (sanet.py:12-18, 26-71, 100-138) -----------------------------------
 // functional.normalize(x, dim=1): x / max(||x||_2 over channels, 1e-12), per position.
-// One thread per (b, position): the channel loop strides by HW, so a wave reads 64
-// consecutive positions of one channel row per step (coalesced).
+// Block = 64 consecutive positions (of one image) x 4 channel quarters (one wave each; a
+// wave reads 64 consecutive positions of one channel row per load: coalesced); each lane
+// sums its quarter's squares in fp64 over 4 interleaved chains, the quarters are combined in
+// order through LDS, and every lane scales its quarter by the one reciprocal of the norm (one
+// rounding more than the division: <= 1 ulp). (The thread-per-position form with a serial
+// fp64 chain and a division per element took 0.49 ms per call at B = 32, C = 512, HW = 4096.)
 __global__ __launch_bounds__(256) void colnorm_kernel(const float* __restrict__ x,
                                                       float* __restrict__ out, int B, int C,
                                                       int HW) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (int64_t)B * HW) return;
-  const int64_t b = idx / HW, i = idx - b * HW;
-  const float* xp = x + b * C * (int64_t)HW + i;
-  double ss = 0.0;
-  for (int c = 0; c < C; ++c) {
-    const double v = xp[(int64_t)c * HW];
-    ss += v * v;
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, qtr = threadIdx.x >> 6;
+  const int pblocks = (HW + 63) / 64;
+  const int64_t b = blockIdx.x / pblocks;
+  const int i = (int)(blockIdx.x - b * pblocks) * 64 + lane;
+  const bool ok = i < HW;
+  const int c0 = (int)((int64_t)C * qtr / 4), c1 = (int)((int64_t)C * (qtr + 1) / 4);
+  const float* xp = x + b * C * (int64_t)HW + (ok ? i : 0);
+  double ss[4] = {0.0, 0.0, 0.0, 0.0};
+  if (ok) {
+    int c = c0;
+    for (; c + 4 <= c1; c += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double v = xp[(int64_t)(c + u) * HW];
+        ss[u] = fma(v, v, ss[u]);
+      }
+    }
+    for (; c < c1; ++c) {
+      const double v = xp[(int64_t)c * HW];
+      ss[0] = fma(v, v, ss[0]);
+    }
   }
-  const float nrm = fmaxf((float)sqrt(ss), 1e-12f);
+  part[qtr][lane] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
+  __syncthreads();
+  if (!ok) return;
+  const double tot = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  const float r = 1.f / fmaxf((float)sqrt(tot), 1e-12f);
   float* op = out + b * C * (int64_t)HW + i;
-  for (int c = 0; c < C; ++c) op[(int64_t)c * HW] = xp[(int64_t)c * HW] / nrm;
+  for (int c = c0; c < c1; ++c) op[(int64_t)c * HW] = xp[(int64_t)c * HW] * r;
 }
 
 // f_psi's last Linear(hid -> 1) + head: AEA  clamp = sigmoid(t) * interval + from
@@ -735,17 +757,17 @@ static int clamp_values_factored(const float* cn, const float* sn, const float* 
 
 static int col_norms(const float* c, const float* s, float* cn, float* sn, int B, int C, int HW,
                      hipStream_t st) {
-  const int64_t pos = (int64_t)B * HW;
-  colnorm_kernel<<<(unsigned)((pos + 255) / 256), 256, 0, st>>>(c, cn, B, C, HW);
-  colnorm_kernel<<<(unsigned)((pos + 255) / 256), 256, 0, st>>>(s, sn, B, C, HW);
+  const unsigned nb = (unsigned)((int64_t)B * ((HW + 63) / 64));
+  colnorm_kernel<<<nb, 256, 0, st>>>(c, cn, B, C, HW);
+  colnorm_kernel<<<nb, 256, 0, st>>>(s, sn, B, C, HW);
   return launch_status("colnorm_kernel");
 }
 
 static int affinity(const float* c, const float* s, float* out, float* cn, float* sn, int B,
                     int C, int HW, hipStream_t st) {
-  const int64_t pos = (int64_t)B * HW;
-  colnorm_kernel<<<(unsigned)((pos + 255) / 256), 256, 0, st>>>(c, cn, B, C, HW);
-  colnorm_kernel<<<(unsigned)((pos + 255) / 256), 256, 0, st>>>(s, sn, B, C, HW);
+  const unsigned nb = (unsigned)((int64_t)B * ((HW + 63) / 64));
+  colnorm_kernel<<<nb, 256, 0, st>>>(c, cn, B, C, HW);
+  colnorm_kernel<<<nb, 256, 0, st>>>(s, sn, B, C, HW);
   if (int e = launch_status("colnorm_kernel")) return e;
   const int64_t fhw = (int64_t)C * HW;
   // A[b][i][j] = sum_c cn[b][c][i] sn[b][c][j]
@@ -1037,19 +1059,22 @@ extern "C" int rpst_sanet_attention_backward(const float* F, const float* G, con
 }
 
 // ---- SANet attention backward over query chunks (no B x HW x HW workspace) -------------
-// The same gradients with S and dP formed for attn_qc() = 1024 queries (full rows) at a time:
+// The same gradients with S and dP formed for attn_qc() = 2048 queries (full rows) at a time:
 // per chunk S_q = F_q^T G, the row statistics, dH += dO_q P_q (P formed while S_q is staged),
 // dP_q = dO_q^T H, dS_q = P (dP - rowsum(dP P)) in place (softmax_bwd_logits_kernel: whole
 // rows, so every row of dS sums to zero to rounding as in the single pass), dF_q = G dS_q^T,
 // dG += F_q dS_q; dH and dG sum the chunks in order. S, its statistics and dS are the single
 // pass's bit for bit (the GEMM's k order does not depend on M); 10 HW^2 C FLOP per image like
-// the single pass. Workspace: S_q and dP_q (2 B qc HWs) + 2 B qc row vectors.
+// the single pass. Workspace: S_q and dP_q (2 B qc HWs) + 2 B qc row vectors. (2048: the dF_q
+// GEMM's grid is C/256 x qc/128 tiles per image -- at 1024 queries, C = 512 and B = 8 only 128
+// workgroups, and the SAModel training step ran 2.8 % slower than the single pass; at 2048
+// 0.6 %, profiles/r05/attn_bwd_qc.log.)
 // (RPST_ATTN_QC overrides the chunk: A/B against the single pass, tests.)
 static int attn_qc() {
   static const int qc = [] {
     const char* e = std::getenv("RPST_ATTN_QC");
-    const int v = (e && *e) ? std::atoi(e) : 1024;
-    return v >= 16 ? v / 4 * 4 : 1024;
+    const int v = (e && *e) ? std::atoi(e) : 2048;
+    return v >= 16 ? v / 4 * 4 : 2048;
   }();
   return qc;
 }

@@ -574,7 +574,7 @@ def _sanet_backward(m, saved, d_out, grads):
     _acc(grads, m.out_conv.weight, dw)
     _acc(grads, m.out_conv.bias, db)
     dO = ops.conv2d(d_out, flip_packed_weight(m.out_conv), None, c, 1).contiguous()
-    # attention gradients (rpst_sanet_attention_backward_chunked): S = F^T G and dP for 1024
+    # attention gradients (rpst_sanet_attention_backward_chunked): S = F^T G and dP for 2048
     # queries at a time on gemm_f32_kernel, the softmax probabilities formed while S is
     # staged, dS = P (dP - rowsum(dP P)) -- no B x HW x HW workspace
     dF, dG, dH = torch.empty_like(F), torch.empty_like(G), torch.empty_like(H)

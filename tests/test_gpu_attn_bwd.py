@@ -1,8 +1,8 @@
 """SANet attention backward over query chunks (rpst_sanet_attention_backward_chunked, the
 training path of sanet.py:82-99 under autograd): dF, dG, dH against
 float64 torch autograd of O = H softmax(F^T G)^T, with a ragged last query chunk (HW = 2400
-= 2 x 1024 + 352), four chunks at C = 512 (HW = 4096), HWc != HWs (1200 queries, 2100 keys)
-and one chunk (HW = 600). Tolerance rel-L2 1e-5 (fp32 vs fp64, logits of moderate spread).
+= 2048 + 352), two chunks at C = 512 (HW = 4096), HWc != HWs (1200 queries, 2100 keys) and
+one chunk (HW = 600). Tolerance rel-L2 1e-5 (fp32 vs fp64, logits of moderate spread).
 The workspace has no B x HW x HW term."""
 import pytest
 import torch
@@ -34,7 +34,7 @@ def test_sanet_attention_backward_chunked(cuda, shape):
     O, dF_ref, dG_ref, dH_ref = _ref_grads(F, G, H, dO)
     lib = _lib.load()
     nbytes = lib.rpst_sanet_attention_backward_chunked_workspace_size(B, C, hw, hws)
-    q = min(hw, 1024)  # S and dP of one 1024-query chunk + 2 row vectors: no B x HW x HW term
+    q = min(hw, 2048)  # S and dP of one 2048-query chunk + 2 row vectors: no B x HW x HW term
     assert nbytes == 4 * (2 * B * q * hws + 2 * B * q), nbytes
     ws = torch.empty(nbytes, device=cuda, dtype=torch.uint8)
     dF, dG, dH = (torch.empty_like(x) for x in (F, G, H))
@@ -51,7 +51,7 @@ def test_sanet_attention_backward_chunked(cuda, shape):
 
 @pytest.mark.parametrize("mode", ("aea", "relu"))
 def test_adaptive_attention_backward_query_chunks(cuda, mode):
-    """rpst_adaptive_attention_backward over query chunks (HW = 2400: 1024 + 1024 + 352): the
+    """rpst_adaptive_attention_backward over query chunks (HW = 2400: 2048 + 352): the
     gradients of O = H AEA(A, softmax(F^T G))^T against float64 torch autograd of the oracle's
     restatement (R.aea), and a workspace with no B x HW x HW term."""
     import network as net
