@@ -19,6 +19,7 @@ while batch k runs on the GPU; a copy stream carries the pixels; the PNG encodes
 """
 from __future__ import annotations
 
+import collections
 import os
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -190,7 +191,10 @@ class Pipeline:
     HIP event on the copy stream), one task per file. png_level / png_strategy: zlib level
     and strategy of the PNGs (PIL's default level 6 and strategy is what
     torchvision.save_image writes; the pixels are identical at any setting: "rle" at level 6
-    encodes ~6x faster for ~1.5 % larger files, level 0 stores)."""
+    encodes ~6x faster for ~1.5 % larger files, level 0 stores). At most BACKLOG batches'
+    encodes are outstanding: past that, the loop waits for the oldest batch's files."""
+
+    BACKLOG = 3
 
     def __init__(self, stylize: Callable[[torch.Tensor, torch.Tensor], torch.Tensor],
                  device, img_size: int, batch_size: int = 1, num_workers: int = 4,
@@ -233,7 +237,11 @@ class Pipeline:
         with ThreadPoolExecutor(self.workers) as readers, \
                 ThreadPoolExecutor(self.encode_workers) as writers, torch.no_grad():
             pending = [self._decode_start(readers, dataset, batches[0])]
-            saves = []
+            # encode futures per batch, oldest first: each holds its batch's pinned host
+            # buffers until written, so at most BACKLOG batches may be outstanding (a
+            # host-encode-bound run would otherwise grow them with the dataset)
+            saves = collections.deque()
+            n = 0
             back = None  # (event, items, host buffers) of the previous batch
             for k in range(len(batches)):
                 if k + 1 < len(batches):  # decode the next batch while this one runs
@@ -269,12 +277,17 @@ class Pipeline:
                 # the previous batch's pixels are back by now (its work was queued first):
                 # queue its encodes while this batch computes
                 if back is not None:
-                    saves += self._write_start(writers, *back, out_dir, log)
+                    saves.append(self._write_start(writers, *back, out_dir, log))
                 st["wait_d2h"] += clock() - t2
                 back = (done, items, host)
+                t4 = clock()
+                while len(saves) > self.BACKLOG:
+                    n += sum(f.result() for f in saves.popleft())
+                st["wait_encode"] += clock() - t4
             t3 = clock()
-            saves += self._write_start(writers, *back, out_dir, log)
-            n = sum(f.result() for f in saves)
+            saves.append(self._write_start(writers, *back, out_dir, log))
+            while saves:
+                n += sum(f.result() for f in saves.popleft())
             st["wait_encode"] += clock() - t3
             return n
 
