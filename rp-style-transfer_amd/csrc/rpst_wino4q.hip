@@ -456,9 +456,11 @@ __device__ __forceinline__ void q_finish(const QEpi& e, int co, float (&Y)[16], 
     if (RPST_W4Q_SDBG & 2) m2 = mean;
     if (!(RPST_W4Q_SDBG & 4)) m2 = q_row16_sum(m2);
     // partials in [n][partial][co] order (stat_merge_t_kernel): a wave's 16 channels of one
-    // partial fill whole cache lines; in [n][co][partial] order they were 8-B pieces
-    // scattered over 16 planes, 1.1 ms of 28.3 on 128->256 N64 (RPST_W4Q_SDBG=1 skips the store)
-    if (!(RPST_W4Q_SDBG & 1) && tn == 0 && cok)
+    // partial fill whole cache lines (in [n][co][partial] order they were 8-B pieces
+    // scattered over 16 planes). Statistics cost, 128->256 N64 (tools/ab_stats.py): 1.5 ms
+    // of 28.4, of which the store 0.2 (SDBG 8: the store kept but never taken at run time),
+    // the centred-square pass 0.33 (SDBG 2); SDBG 1 drops the whole computation (dead code)
+    if (!(RPST_W4Q_SDBG & 1) && tn == 0 && cok && (!(RPST_W4Q_SDBG & 8) || e.statP < 0))
       e.statp[((int64_t)n * e.statP + e.sidx) * e.Cout + co] = make_float2(mean, m2);
   }
 }
