@@ -465,30 +465,6 @@ __device__ __forceinline__ void q_finish(const QEpi& e, int co, float (&Y)[16], 
   }
 }
 
-// Y = A^T M A (M: 6x6 row-major) with the bias b added to transformed row 1 after the column
-// pass (column 1 of A^T is all ones: b reaches every output row)
-__device__ __forceinline__ void q_out_transform(const float (&M)[36], float b, float (&Y)[16]) {
-  float P[6][4];
-#pragma unroll
-  for (int I = 0; I < 6; ++I) {
-    float m[6];
-#pragma unroll
-    for (int J = 0; J < 6; ++J) m[J] = M[I * 6 + J];
-    q_at6(m, P[I]);
-  }
-#pragma unroll
-  for (int x = 0; x < 4; ++x) P[1][x] += b;
-#pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    float m[6], y[4];
-#pragma unroll
-    for (int I = 0; I < 6; ++I) m[I] = P[I][x];
-    q_at6(m, y);
-#pragma unroll
-    for (int yy = 0; yy < 4; ++yy) Y[yy * 4 + x] = y[yy];
-  }
-}
-
 template <int INOP, bool STATS, bool BTAB, bool RELU>
 __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
   // ring: weights in 2 stages (W(x) in wsx % 2), patches in 4 (P(x) in ps x % 4); a co tile
