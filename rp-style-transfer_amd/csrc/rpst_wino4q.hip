@@ -155,8 +155,17 @@ constexpr int kQXS = 4 * 3 * 3 * 64 * 2;     // epilogue exchange floats per til
 #ifndef RPST_W4Q_DBG
 #define RPST_W4Q_DBG 0
 #endif
+#ifndef RPST_W4Q_WG0
+#define RPST_W4Q_WG0 0  // MFMA group of a step whose issue slot takes the first W(x + 1) piece
+#endif
+#ifndef RPST_W4Q_PG
+#define RPST_W4Q_PG 5   // MFMA group after which the P(x + 4) pieces are issued
+#endif
 #ifndef RPST_W4Q_AHEAD
-#define RPST_W4Q_AHEAD 2                     // MFMA groups whose A operands are read ahead
+// MFMA groups whose A operands are read ahead: configs[1] 539.7 / 541.7 img/s at 2, 545.2 /
+// 546.6 at 3 (128->256 N64 28.05 -> 27.65 ms), 537 at 4, 522 at 5 (tools/ab_bench_libs.sh,
+// profiles/r05/ahead_ab.log)
+#define RPST_W4Q_AHEAD 3
 #endif
 static_assert(10 * 17 <= kQDMA4 * 64 && kQDMA4 * 256 <= kQCS, "16-B pieces in a channel");
 static_assert(10 * kQPS <= kQDMA * 64 && kQDMA * 64 <= kQCS, "4-B pieces in a channel");
@@ -710,9 +719,9 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
         q_mfma<0>(acc[p][1], w4[p].y, V[p]);
         q_mfma<0>(acc[p][2], w4[p].z, V[p]);
         q_mfma<0>(acc[p][3], w4[p].w, V[p]);
-        if (q < kQWPI) issue_w(x + 1, wsn, q);
+        if (q >= RPST_W4Q_WG0 && q < RPST_W4Q_WG0 + kQWPI) issue_w(x + 1, wsn, q - RPST_W4Q_WG0);
         // P(x + 4): K step ks + 4 of this co tile, or of the next one
-        if (q == 5) {
+        if (q == RPST_W4Q_PG) {
           const int k4 = ks + 4 < K4 ? ks + 4 : ks + 4 - K4;
           if (wide) issue_p(std::true_type{}, x + 4, k4, psx);
           else issue_p(std::false_type{}, x + 4, k4, psx);
