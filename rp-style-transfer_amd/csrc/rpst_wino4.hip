@@ -53,6 +53,11 @@ constexpr int kW4CK = 8;                   // input channels per chunk
 #ifndef RPST_W4_HP
 #define RPST_W4_HP 2
 #endif
+#ifndef RPST_W4_AHEAD  // MFMA groups whose A operands are read ahead (NR = 4; NR = 2: 3)
+// 2: 64->128 N64 8.17 -> 8.02 ms, 32->64 2.57 -> 2.50, 64->32 1.15 -> 1.11 against 3; NR = 2's
+// 16->32 / 32->16 measured 0.005 ms slower at 2 (tools/ab_bench_libs.sh, profiles/r05/ahead_ab.log)
+#define RPST_W4_AHEAD 2
+#endif
 #ifndef RPST_W4_ORDER  // spatial block order (w4_tile)
 #define RPST_W4_ORDER 0
 #endif
@@ -539,8 +544,9 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
     {
       const float* wq = pbuf + Geo::SPATCH + ph * 9 * 256 + lane * 4;
       float4 w4[9];
+      constexpr int kA = NR == 4 ? RPST_W4_AHEAD : 3;  // A-operand groups read ahead
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < kA; ++q)
         w4[q] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
                            : *reinterpret_cast<const float4*>(wq + q * 256);
       // rows 3ph..3ph+2 of B^T d (d[r] = input row ph + r), then B along each row
@@ -572,9 +578,9 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
         if (!(DBG & 8)) bt6(t[i][0], t[i][1], t[i][2], t[i][3], t[i][4], t[i][5]);
 #pragma unroll
       for (int q = 0; q < 9; ++q) {
-        if (q + 3 < 9)
-          w4[q + 3] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
-                                 : *reinterpret_cast<const float4*>(wq + (q + 3) * 256);
+        if (q + kA < 9)
+          w4[q + kA] = (DBG & 64) ? make_float4(1.f, 2.f, 3.f, (float)q)
+                                  : *reinterpret_cast<const float4*>(wq + (q + kA) * 256);
         const int p0 = 2 * q, p1 = 2 * q + 1;
         const float v0 = t[p0 / 6][p0 % 6], v1 = t[p1 / 6][p1 % 6];
         acc[p0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[q].x, v0, acc[p0][0], 0, 0, 0);

@@ -8,6 +8,6 @@ for rep in 1 2; do
   for v in "$@"; do
     if [ "$v" = base ]; then unset RPST_LIB; else export RPST_LIB=var/$v/librpst.so; fi
     timeout -k 10 300 python bench.py --no-configs --no-cpu-baseline > $O/$v.$rep.json 2> $O/$v.$rep.err || { tail $O/$v.$rep.err; exit 1; }
-    python -c "import json;d=json.load(open('$O/$v.$rep.json'));k=d['kernel_ms_per_step'];print('$v', d['value'], [round(k[x],3) for x in k if '128->256' in x or '256->128' in x or '128->64' in x])"
+    python -c "import json;d=json.load(open('$O/$v.$rep.json'));k=d['kernel_ms_per_step'];print('$v', d['value'], ' '.join(x.split()[1] + ':' + str(round(k[x], 3)) for x in k))"
   done
 done
