@@ -199,14 +199,18 @@ int wino4_persist() { return 1; }  // one block per spatial tile loops over the 
 // second block per CU overlaps little, and de-phasing the two (the second-resident blocks
 // of the first dispatch round sleeping 16k / 36k cycles first) changed nothing (16->32
 // 0.970 / 0.976 / 0.969 ms, profiles/r03/wino4_half_ab.log): the small layers are not bound
-// by exposed prologues. Only the two smallest layers switch.
+// by exposed prologues. Only the two smallest layers switch. Round 5 (A operands read 2
+// groups ahead at NR = 4): 64->32 N32 1.10 -> 1.06 ms at NR = 2 (32->64 2.50 either way), so
+// layers with <= 32 output channels switch up to Cin * Cout = 2048 (profiles/r05/half_ab.log).
 int wino4_rows(int Cin, int Cout, int in_op) {
-  static const int lim = [] {
+  static const int lim = [] {  // RPST_WINO4_HALF: the product threshold alone (A/B)
     const char* e = getenv("RPST_WINO4_HALF");
-    return (e && *e) ? atoi(e) : 512;
+    return (e && *e) ? atoi(e) : -1;
   }();
   if (wino4q_applies(Cin, Cout, in_op)) return 2;  // rpst_wino4q.hip: 8 output rows
-  return (int64_t)Cin * Cout <= lim ? 2 : 4;
+  const int64_t cc = (int64_t)Cin * Cout;
+  if (lim >= 0) return cc <= lim ? 2 : 4;
+  return cc <= 512 || (Cout <= 32 && cc <= 2048) ? 2 : 4;
 }
 
 // B^T row transform of one 6-vector (in place): the shared terms of rows (1,2) and (3,4)
