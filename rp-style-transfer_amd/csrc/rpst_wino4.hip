@@ -58,6 +58,12 @@ constexpr int kW4CK = 8;                   // input channels per chunk
 // 16->32 / 32->16 measured 0.005 ms slower at 2 (tools/ab_bench_libs.sh, profiles/r05/ahead_ab.log)
 #define RPST_W4_AHEAD 2
 #endif
+#ifndef RPST_W4_HW2  // the same issue slots for the NR = 2 form
+#define RPST_W4_HW2 RPST_W4_HW
+#endif
+#ifndef RPST_W4_HP2
+#define RPST_W4_HP2 RPST_W4_HP
+#endif
 #ifndef RPST_W4_ORDER  // spatial block order (w4_tile)
 #define RPST_W4_ORDER 0
 #endif
@@ -331,7 +337,7 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
   // 64 no weight LDS reads, 128 no DMA waits
   constexpr int DBG = RPST_W4DBG;
   // DMA placement of step g + 3: before the transform (-1) or after MFMA pair q of step g
-  constexpr int kHW = RPST_W4_HW, kHP = RPST_W4_HP;
+  constexpr int kHW = NR == 2 ? RPST_W4_HW2 : RPST_W4_HW, kHP = NR == 2 ? RPST_W4_HP2 : RPST_W4_HP;
   static_assert(RawN<INOP>::R == 1, "one raw load per patch element");
   // one __shared__ object per ring stage: the stage a K step reads and the one its DMA
   // fills are then distinct objects, so the compiler's wait insertion does not drain the
