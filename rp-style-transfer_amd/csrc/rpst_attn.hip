@@ -731,20 +731,53 @@ static int clamp_values(const float* A, const float* w1, const float* b1, const 
   return launch_status("clamp_head_kernel");
 }
 
+// K chunks of T = sn W1^T (C x hidden per image, K = HW): its grid is C/256 x hidden/128
+// tiles per image (2 x 2 at C = 512, HW = 4096), so the pixels are split 4 ways once HW >=
+// 2048 (128 -> 512 workgroups at B = 32; 0.58 ms per call before); the partials sum in order
+static int clamp_t_ks(int HW) { return HW >= 2048 ? 4 : 1; }
+// floats of the T region: T itself and, when split, its ks partials
+static size_t clamp_t_floats(int B, int C, int HW, int hidden) {
+  const int ks = clamp_t_ks(HW);
+  return (size_t)B * C * hidden * (ks > 1 ? 1 + ks : 1);
+}
+// out[b][i] = sum_j part[b * ks + j][i] (fixed order over j)
+__global__ void ksum_kernel(const float* __restrict__ part, float* __restrict__ out,
+                            int64_t per, int ks, int B) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= per * B) return;
+  const int64_t b = t / per, i = t - b * per;
+  const float* p = part + b * ks * per + i;
+  float acc = p[0];
+  for (int j = 1; j < ks; ++j) acc += p[j * per];
+  out[t] = acc;
+}
+
 // The clamp values without the affinity matrix: f_psi's first Linear only ever sees
 // A = cn^T sn through Z = A W1^T, and Z = cn^T (sn W1^T) (sanet.py:45-66, 110): T = sn W1^T
 // (C x hid per image, K = HW), then Z = cn^T T + b1 (K = C): 2 x 2 C hid HW FLOP per image
 // instead of 2 HW^2 (C + hid), and the B x HW x HW affinity is never written or read (the
 // same sums in another association: ~1e-7 relative from the two-GEMM form).
-// T: B * C * hid floats of scratch.
+// T: clamp_t_floats(B, C, HW, hid) floats of scratch (T, then its K-chunk partials).
 static int clamp_values_factored(const float* cn, const float* sn, const float* w1,
                                  const float* b1, const float* w2, const float* b2, int hid,
                                  int mode, float from, float interval, float* T, float* Z,
                                  float* clamp, int B, int C, int HW, hipStream_t st) {
-  GemmArgs gt{sn, w1, T, {}, nullptr, nullptr, 0, C, hid, HW, HW, HW, hid,
-              (int64_t)C * HW, 0, (int64_t)C * hid, 0};
+  const int ks = clamp_t_ks(HW);
+  const int64_t per = (int64_t)C * hid;
+  GemmArgs gt{sn, w1, ks > 1 ? T + (size_t)B * per : T, {}, nullptr, nullptr, 0, C, hid, HW,
+              HW, HW, hid, (int64_t)C * HW, 0, per, 0};
+  if (ks > 1) {
+    gt.ks = ks;
+    gt.kc = (HW + ks - 1) / ks;
+    gt.kc = (gt.kc + 31) / 32 * 32;
+  }
   launch_gemm<LAY_RK, LAY_RK, BX_NONE>(gt, B, st);
   if (int e = launch_status("gemm_f32_kernel(T=sn W1^T)")) return e;
+  if (ks > 1) {
+    ksum_kernel<<<(unsigned)((per * B + 255) / 256), 256, 0, st>>>(T + (size_t)B * per, T, per,
+                                                                   ks, B);
+    if (int e = launch_status("ksum_kernel(T)")) return e;
+  }
   GemmArgs gz{cn, T, Z, {}, nullptr, b1, 1, HW, hid, C, HW, hid, hid,
               (int64_t)C * HW, (int64_t)C * hid, (int64_t)HW * hid, 0};
   launch_gemm<LAY_KR, LAY_KR, BX_NONE>(gz, B, st);
@@ -881,8 +914,8 @@ extern "C" int rpst_aea_clamp(const float* x, const float* fx, const float* w1,
 // the logits' region first holds T = sn W1^T (C x hidden per image): whichever is larger.
 // On the flash path (sanet_flash_ok) S is never formed: T only.
 static size_t sq_or_t(int B, int C, int HW, int hidden) {
-  if (sanet_flash_ok(C, HW)) return (size_t)B * C * hidden;
-  return (size_t)B * std::max((size_t)HW * HW, (size_t)C * hidden);
+  if (sanet_flash_ok(C, HW)) return clamp_t_floats(B, C, HW, hidden);
+  return std::max((size_t)B * HW * HW, clamp_t_floats(B, C, HW, hidden));
 }
 
 extern "C" size_t rpst_adaptive_attention_workspace_size(int B, int C, int HW, int hidden) {
@@ -1192,7 +1225,7 @@ extern "C" size_t rpst_adaptive_attention_backward_workspace_size(int B, int C, 
   const size_t chunks = ((size_t)B * HW + kColChunk - 1) / kColChunk;
   // (the first region holds T and then R, C x hidden per image, never the affinity) + S and
   // dQ of one query chunk + the per-image dW1 partials and the column-sum chunk partials
-  return sizeof(float) * ((size_t)B * C * hidden + 2 * (size_t)B * qc * HW +
+  return sizeof(float) * (clamp_t_floats(B, C, HW, hidden) + 2 * (size_t)B * qc * HW +
                           2 * (size_t)B * HW * hidden + 2 * (size_t)B * C * HW +
                           3 * (size_t)B * HW + 6 * (size_t)B * qc + (size_t)B * hidden * HW +
                           3 * (size_t)(hidden + 1) * chunks);
@@ -1221,7 +1254,7 @@ extern "C" int rpst_adaptive_attention_backward(
   const int qc = std::min(HW, attn_qc());
   const int64_t fhw = (int64_t)C * HW, rows = (int64_t)B * HW, sq = (int64_t)qc * HW;
   float* Aff = static_cast<float*>(workspace);  // T, then R (C x hidden per image)
-  float* Sq = Aff + (size_t)B * C * hidden;     // S and dQ of one query chunk
+  float* Sq = Aff + clamp_t_floats(B, C, HW, hidden);  // S and dQ of one query chunk
   float* dQq = Sq + (size_t)B * sq;
   float* Z = dQq + (size_t)B * sq;
   float* du = Z + (size_t)rows * hidden;

@@ -135,9 +135,10 @@ def test_adaptive_attention_relu4_1_at_1024(cuda, mode):
     synth_(mod, 31)
     hid = mod.f_psi[0].out_features
     nbytes = _lib.load().rpst_adaptive_attention_workspace_size(B, C, hw, hid)
-    # T = sn W1^T, Z = cn^T T (f_psi's hidden layer: HW x HW/16 by the reference's design),
-    # the normalised features and 7 per-query vectors -- no B x HW x HW term (S: 1 GiB)
-    assert nbytes == 4 * (B * C * hid + B * hw * hid + 2 * B * C * hw + 7 * B * hw), nbytes
+    # T = sn W1^T (+ its 4 K-chunk partials), Z = cn^T T (f_psi's hidden layer: HW x HW/16
+    # by the reference's design), the normalised features and 7 per-query vectors -- no
+    # B x HW x HW term (S: 1 GiB)
+    assert nbytes == 4 * (5 * B * C * hid + B * hw * hid + 2 * B * C * hw + 7 * B * hw), nbytes
     g = torch.Generator(device=cuda).manual_seed(5)
     F, G, H = ((torch.rand((B, C, h, w), device=cuda, generator=g) * 2 - 1) * sc
                for sc in (0.3, 0.3, 1.0))
