@@ -138,6 +138,41 @@ def test_sanet_attention_flash_shapes(cuda, shape):
     assert flash == (C in (64, 128, 256, 512) and (h * w) % 4 == 0)
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 9, 20), (1, 256, 12, 15)])
+def test_sanet_attention_ragged_tail_nan_after_tensor(cuda, shape):
+    """HW % 16 != 0: the last key block of the last channel row of the last image reaches
+    past the tensor. The flash kernels put the whole offset in the buffer descriptor's
+    range-checked voffset, so those keys read 0 whatever follows the tensor: F,
+    G and H live at the front of NaN-filled buffers, and the output is finite and matches
+    float64 (SANet and both AdaptiveSANet modules)."""
+    import network as net
+    from rpst import ops
+    B, C, h, w = shape
+    n = B * C * h * w
+
+    def at_front_of_nan(x):
+        buf = torch.full((n + 4096,), float("nan"), device=cuda)
+        v = buf[:n].view(shape)
+        v.copy_(x)
+        return v
+    F, G, H = gen(51, shape, 0.6), gen(52, shape, 0.6), gen(53, shape, 1.0)
+    Fc, Gc, Hc = (at_front_of_nan(x.to(cuda)) for x in (F, G, H))
+    out = ops.sanet_attention(Fc, Gc, Hc)
+    assert torch.isfinite(out).all()
+    assert rel_l2(out, _attn_ref64(F, G, H).view(shape)) < 1e-5
+    c = at_front_of_nan(gen(54, shape, 1.0, 0.2, relu=True).to(cuda))
+    s_ = at_front_of_nan(gen(55, shape, 1.0, 0.2, relu=True).to(cuda))
+    for mode in ("aea", "relu"):
+        mod = (net.AEAModule(h * w) if mode == "aea" else net.AEALReluModule(h * w)).to(cuda)
+        with torch.no_grad():
+            o, _, _, _ = ops.adaptive_attention(Fc, Gc, Hc, c, s_, mod.f_psi, mod.mode, 50.0,
+                                                0.4, 0.5)
+            o2, _, _, _ = ops.adaptive_attention(F.to(cuda), G.to(cuda), H.to(cuda),
+                                                 c.clone(), s_.clone(), mod.f_psi, mod.mode,
+                                                 50.0, 0.4, 0.5)
+        assert torch.isfinite(o).all() and torch.equal(o, o2), mode
+
+
 def test_sanet_attention_relu4_1_at_1024(cuda):
     """The relu4_1 shape of a 1024x1024 image (HW = 16384, C = 512): the flash path needs no
     B x HW x HW workspace (1 GiB per image materialised); checked on 256 queries against
