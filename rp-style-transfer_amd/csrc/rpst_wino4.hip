@@ -297,6 +297,13 @@ __device__ __forceinline__ bool resolve_bf(int& v, int n, bool zero_pad) {
   return in || !zero_pad;
 }
 
+#ifndef RPST_W4_SWZ  // 1: consecutive logical blocks on one XCD (xcd_swizzle)
+#define RPST_W4_SWZ 1
+#endif
+__device__ __forceinline__ int w4_block_id() {
+  return RPST_W4_SWZ ? xcd_swizzle(blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+}
+
 // spatial tile of logical block b (after the co-split digit): order 0 = column tile fastest,
 // then row tile, then image; 1 = image fastest, then column, row; 2 = column, image, row
 // (RPST_W4_ORDER at build time: which tiles the resident blocks share). tools/ab_variants.sh,
@@ -316,6 +323,11 @@ __device__ __forceinline__ void w4_tile(int b, int order, int tiles_x, int tiles
     b /= tiles_x;
     n = b % N;
     ty = b / N;
+  } else if (order == 3) {  // row tile fastest, then column tile, image
+    ty = b % tiles_y;
+    b /= tiles_y;
+    tx = b % tiles_x;
+    n = b / tiles_x;
   } else {
     tx = b % tiles_x;
     b /= tiles_x;
@@ -351,7 +363,7 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
   // block -> (column tile, row tile, image), XCD-swizzled (neighbouring spatial tiles share
   // halo rows and every block of an XCD streams the same weight slices through its L2);
   // one block loops over every co tile of its spatial tile
-  int bid = xcd_swizzle(blockIdx.x, (int)gridDim.x);
+  int bid = w4_block_id();
   // a.cosplit blocks per spatial tile (consecutive logical ids: one XCD, dispatched
   // together, so the patch they all stream is served by that XCD's L2), each looping over
   // co_tiles / cosplit co tiles
@@ -651,7 +663,7 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
     e.Cout = L->Cout;
     e.slope = L->relu == RPST_ACT_RELU ? 0.f : (L->relu == RPST_ACT_LRELU ? 0.2f : 1.f);
     int btx, bty;
-    w4_tile(xcd_swizzle(blockIdx.x, (int)gridDim.x) / L->cosplit, RPST_W4_ORDER,
+    w4_tile(w4_block_id() / L->cosplit, RPST_W4_ORDER,
             L->tiles_x, L->tiles_y, L->N, btx, bty, e.n);
     const int bx0 = btx * kW4TW;
     e.gy0 = bty * Geo::TH + 4 * wr;

@@ -302,6 +302,47 @@ struct QEpi {
   int statP;
 };
 
+// Block order (tools/ab_bench_libs.sh, profiles/r05/order_ab.log; configs[1], two rounds):
+// row tile fastest with the hardware's round-robin XCD assignment (consecutive blocks on
+// consecutive XCDs) 553.3 / 553.1 img/s; column tile fastest with consecutive logical blocks
+// on one XCD (xcd_swizzle, the round-4 choice) 548.3 / 547.3; row tile fastest swizzled
+// 534.7; column tile fastest unswizzled 536.2; image-fastest orders 503-538.
+#ifndef RPST_W4Q_ORDER  // 0 column tile fastest, 1 row tile fastest, 2 / 3 image-fastest forms
+#define RPST_W4Q_ORDER 1
+#endif
+#ifndef RPST_W4Q_SWZ  // 1: consecutive logical blocks on one XCD (xcd_swizzle)
+#define RPST_W4Q_SWZ 0
+#endif
+__device__ __forceinline__ int q_block_id() {
+  return RPST_W4Q_SWZ ? xcd_swizzle(blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+}
+__device__ __forceinline__ void q_tile(int b, int tiles_x, int tiles_y, int cosplit, int& tx,
+                                       int& ty, int& n) {
+  if (RPST_W4Q_ORDER == 1) {
+    ty = b % tiles_y;
+    b /= tiles_y;
+    tx = b % tiles_x;
+    n = b / tiles_x;
+  } else if (RPST_W4Q_ORDER == 2) {  // image fastest, then row tile, column tile
+    const int nimg = (int)(gridDim.x / ((unsigned)tiles_x * tiles_y * cosplit));
+    n = b % nimg;
+    b /= nimg;
+    ty = b % tiles_y;
+    tx = b / tiles_y;
+  } else if (RPST_W4Q_ORDER == 3) {  // row tile, image, column tile
+    const int nimg = (int)(gridDim.x / ((unsigned)tiles_x * tiles_y * cosplit));
+    ty = b % tiles_y;
+    b /= tiles_y;
+    n = b % nimg;
+    tx = b / nimg;
+  } else {
+    tx = b % tiles_x;
+    b /= tiles_x;
+    ty = b % tiles_y;
+    n = b / tiles_y;
+  }
+}
+
 __device__ __forceinline__ QEpi q_epi_ctx(int wr, int tn) {
   const QArgs L = q_args();
   QEpi e;
@@ -309,11 +350,8 @@ __device__ __forceinline__ QEpi q_epi_ctx(int wr, int tn) {
   e.H = L->H;
   e.Cout = L->Cout;
   e.slope = L->relu == RPST_ACT_RELU ? 0.f : (L->relu == RPST_ACT_LRELU ? 0.2f : 1.f);
-  int b = xcd_swizzle(blockIdx.x, (int)gridDim.x) / L->cosplit;
-  const int btx = b % L->tiles_x;
-  b /= L->tiles_x;
-  const int bty = b % L->tiles_y;
-  e.n = b / L->tiles_y;
+  int btx, bty;
+  q_tile(q_block_id() / L->cosplit, L->tiles_x, L->tiles_y, L->cosplit, btx, bty, e.n);
   const int bx0 = btx * kQTW;
   e.gy0 = bty * kQTH + 4 * wr;
   e.gx0 = bx0 + 4 * tn;
@@ -502,14 +540,12 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
   const int k = lane >> 4, tn = lane & 15, wr = wave >> 2;
 
   // block -> (co-split group, column tile, row tile, image); XCD-swizzled
-  int bid = xcd_swizzle(blockIdx.x, (int)gridDim.x);
+  int bid = q_block_id();
   const int cog = bid % a.cosplit;
   bid /= a.cosplit;
   const int nct = a.co_tiles / a.cosplit, ct0 = cog * nct;
-  const int tx = bid % a.tiles_x;
-  bid /= a.tiles_x;
-  const int ty = bid % a.tiles_y;
-  const int n = bid / a.tiles_y;
+  int tx, ty, n;
+  q_tile(bid, a.tiles_x, a.tiles_y, a.cosplit, tx, ty, n);
   const int K4 = a.nchunks, G = nct * K4;
   const int y0 = ty * kQTH, x0 = tx * kQTW;
 
