@@ -64,8 +64,8 @@ constexpr int kW4CK = 8;                   // input channels per chunk
 #ifndef RPST_W4_HP2
 #define RPST_W4_HP2 RPST_W4_HP
 #endif
-#ifndef RPST_W4_ORDER  // spatial block order (w4_tile)
-#define RPST_W4_ORDER 0
+#ifndef RPST_W4_ORDER  // spatial block order (w4_tile): 3 = row tile fastest (round 5)
+#define RPST_W4_ORDER 3
 #endif
 constexpr int kW4BM = 32;                  // output channels per co tile
 constexpr int kW4TH = 16, kW4TW = 64;      // output rows x columns per block
@@ -297,15 +297,20 @@ __device__ __forceinline__ bool resolve_bf(int& v, int n, bool zero_pad) {
   return in || !zero_pad;
 }
 
+// Round 5 (tools/ab_bench_libs.sh, profiles/r05/order_ab.log, configs[1], two rounds): row
+// tile fastest with the hardware's round-robin XCD assignment 546.5 / 547.6 img/s against
+// 543.1 / 544.1 for the round-4 order 0 swizzled (16->32 0.94 -> 0.88 ms, 64->128 8.02 ->
+// 7.90); order 0 unswizzled 545.4 / 544.1, order 3 swizzled 543.7 / 543.5.
 #ifndef RPST_W4_SWZ  // 1: consecutive logical blocks on one XCD (xcd_swizzle)
-#define RPST_W4_SWZ 1
+#define RPST_W4_SWZ 0
 #endif
 __device__ __forceinline__ int w4_block_id() {
   return RPST_W4_SWZ ? xcd_swizzle(blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
 }
 
 // spatial tile of logical block b (after the co-split digit): order 0 = column tile fastest,
-// then row tile, then image; 1 = image fastest, then column, row; 2 = column, image, row
+// then row tile, then image; 1 = image fastest, then column, row; 2 = column, image, row;
+// 3 = row, column, image
 // (RPST_W4_ORDER at build time: which tiles the resident blocks share). tools/ab_variants.sh,
 // two rounds (ms, order 0 / 1 / 2): 128->256 N64 28.46 / 28.86 / 28.37, 64->128 8.00 /
 // 8.47 / 7.83, 256->128 N32 13.81 / 14.17 / 13.76, 32->64 2.54 / 2.69 / 2.57; in bench.py
