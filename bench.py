@@ -295,7 +295,7 @@ def pmc_source(path=None):
     return os.path.relpath(p, ROOT) if p else None
 
 
-def roofline_from_trace(summary, pmc_path=None):
+def roofline_from_trace(summary, pmc_path=None, inference=True):
     from rpst import _lib
     best = None
     for name, a in summary.items():
@@ -319,12 +319,16 @@ def roofline_from_trace(summary, pmc_path=None):
              "wgrad": "conv_wgrad_kernel", "narrow": "conv3x3_narrow_kernel"}.get(
         next((p for p in ("wino4", "wino", "wgrad", "narrow") if name.startswith(p)), ""),
         "conv_mfma_kernel")
-    traffic = pmc_lookup("launches", name, pmc_path)
-    try:  # the kernel the profiled run dispatched for this launch (e.g. the quarter F(4x4) form)
-        with open(pmc_path) as f:
-            kname = json.load(f)["launches"][name]["kernel"].split("::")[-1].split("<")[0]
-    except (OSError, KeyError, TypeError, ValueError):
-        pass
+    # the PMC tables profile inference runs: a training step (precise levels, rpst/ops.py)
+    # may dispatch another kernel under the same launch name
+    traffic = pmc_lookup("launches", name, pmc_path) if inference else None
+    # the kernel a profiled run dispatched for this launch (e.g. the quarter F(4x4) form): the
+    # launch name fixes the shape and loader, so any inference table holding it names it
+    for path in ([pmc_table(pmc_path)[1]] + list(PMC_CONFIG.values())) if inference else []:
+        rec = pmc_table(path)[0].get("launches", {}).get(name) if path else None
+        if rec and rec.get("kernel"):
+            kname = rec["kernel"].split("::")[-1].split("<")[0]
+            break
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
             "traffic": traffic, "kernel": f"{kname} [{name}]",
@@ -800,7 +804,8 @@ def main():
             rec["host_gather"] = meas["host"]
         if cuda:
             cfg_i = args.config if args.config is not None else (1 if default_run else None)
-            rec["roofline"] = roofline_from_trace(summary, PMC_CONFIG.get(cfg_i))
+            rec["roofline"] = roofline_from_trace(summary, PMC_CONFIG.get(cfg_i),
+                                                  not model_kind.startswith("train"))
             rec["roofline_stack"] = stack_roofline(summary, args.steps, dt)
             if model_kind == "wct":
                 rec["roofline_wct"] = wct_roofline(summary, meas.get("wct_phases"))
