@@ -442,6 +442,9 @@ static int ck_of(int ksize) { return ksize == 3 ? ConvK<3>::CK : ConvK<1>::CK; }
 // staged in LDS with the padding resolved, weights [ci][tap][co] sit in LDS for the
 // whole block. Same epilogue as the direct kernel: bias, activation, residual. Images go
 // on grid.z: batches above 65535 images (or 65535 row tiles) take the MFMA direct path.
+#ifndef RPST_NR_ALL  // 3->16 @512^2 N64 0.453 -> 0.437 (patch loads before the weight
+#define RPST_NR_ALL 1  // staging) -> 0.364 ms (every channel up front): profiles/r05/narrow_ab.log
+#endif
 constexpr int kNrTW = 64, kNrPW = kNrTW + 2;
 constexpr int kNrMaxCin = 64, kNrMaxCo = 16, kNrWl = 256 * 9;  // weight floats in LDS
 
@@ -460,11 +463,6 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(8))) float wl[kNrWl];  // Cin * 9 * CO <= 2304 (narrow_shape)
   const int x0 = blockIdx.x * kNrTW, y0 = blockIdx.y * kNrTH, n = blockIdx.z;
   const int tid = threadIdx.x, col = tid & 63, rg = tid >> 6;  // output rows RPT rg ..
-  // direct-packed weights [ci / CK][tap][ci % CK][Cout_pad] (zero beyond Cout)
-  for (int i = tid; i < a.Cin * 9 * CO; i += 256) {
-    const int co = i % CO, t = (i / CO) % 9, ci = i / (9 * CO);
-    wl[i] = a.wpk[((int64_t)(ci / CK) * 9 + t) * CK * a.Cout_pad + (ci % CK) * a.Cout_pad + co];
-  }
   // accumulators in channel pairs: one v_pk_fma_f32 per two output channels
   typedef float f2 __attribute__((ext_vector_type(2)));
   f2 acc2[RPT][CO / 2];
@@ -502,8 +500,31 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
       for (int sl = 0; sl < kSl; ++sl) prc[sl] = off[sl] >= 0 ? cs[off[sl]] : 0.f;
     }
   };
-  fetch(0);
+  // RPST_NR_ALL: with Cin <= 4 (the 16-channel form) every channel's patch is loaded up
+  // front, so no channel waits on its own loads
+  constexpr bool kAll = RPST_NR_ALL && CO == 16 && !kSkip;
+  float preA[kAll ? 4 : 1][kSl];
+  if constexpr (kAll) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int sl = 0; sl < kSl; ++sl)
+        preA[c][sl] = (c < a.Cin && off[sl] >= 0) ? in[(int64_t)c * plane + off[sl]] : 0.f;
+  } else {
+    fetch(0);
+  }
+  // direct-packed weights [ci / CK][tap][ci % CK][Cout_pad] (zero beyond Cout), staged while
+  // the first patch loads are in flight
+  for (int i = tid; i < a.Cin * 9 * CO; i += 256) {
+    const int co = i % CO, t = (i / CO) % 9, ci = i / (9 * CO);
+    wl[i] = a.wpk[((int64_t)(ci / CK) * 9 + t) * CK * a.Cout_pad + (ci % CK) * a.Cout_pad + co];
+  }
   for (int ci = 0; ci < a.Cin; ++ci) {
+    if constexpr (kAll) {
+#pragma unroll
+      for (int sl = 0; sl < kSl; ++sl)
+        pre[sl] = ci == 0 ? preA[0][sl] : ci == 1 ? preA[1][sl] : ci == 2 ? preA[2][sl] : preA[3][sl];
+    }
     __syncthreads();  // the previous channel's patch is consumed (first pass: weights)
     if constexpr (kSkip) {
       const AdainP pa = adain_params(a.aux, n, ci, a);
@@ -517,7 +538,7 @@ __global__ __launch_bounds__(256) void conv3x3_narrow_kernel(ConvArgs a) {
         if (tid + 256 * sl < kNrPS) patch[tid + 256 * sl] = pre[sl];
     }
     __syncthreads();
-    if (ci + 1 < a.Cin) fetch(ci + 1);
+    if (!kAll && ci + 1 < a.Cin) fetch(ci + 1);
     float win[RPT + 2][3];
 #pragma unroll
     for (int r = 0; r < RPT + 2; ++r)
