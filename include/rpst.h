@@ -205,6 +205,16 @@ int rpst_conv2d_algorithm(int Cout, int Cin, int Hs, int Ws, int ksize, int in_o
  * sets it; an explicit RPST_CONV_ALGO still wins. */
 int rpst_conv2d_set_precise(int on);
 
+/* Position-quarter F(4x4) kernel (rpst_wino4q.hip) for the CALLING THREAD (host-only): mode
+ * 0 off (every F(4x4) layer on the 32-channel kernel), 1 the default rule (Cin >= 128, Cin %
+ * 16 == 0, 64 <= Cout <= 512, loader NONE / UPSAMPLE2 or the folded AdaIN), 2 forced on for
+ * every shape it supports (Cin >= 16), -1 back to the RPST_W4Q environment variable (read
+ * per launch; unset = 1). Same arithmetic as the 32-channel kernel within fp32 rounding.
+ * Returns the previous setting. Workspace-size queries cover every setting.
+ * rpst_conv2d_quarter reports whether a layer runs on it under the current settings. */
+int rpst_conv2d_set_quarter(int mode);
+int rpst_conv2d_quarter(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op);
+
 /* ---- stand-alone pool / upsample (same semantics as the conv input operators) ----- */
 int rpst_maxpool2x2_ceil(const float* in, float* out, int N, int C, int H, int W,
                          rpst_stream_t stream);

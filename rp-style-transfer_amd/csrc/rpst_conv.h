@@ -279,6 +279,9 @@ int wino4_mix(ConvArgs& a, const double* T, const double* cvec, const float* dir
 bool wino4q_applies(int Cin, int Cout, int in_op);
 // false while the calling thread is at precise level 2 (rpst_conv.hip)
 bool conv_quarter_allowed();
+// 0 off / 1 default rule / 2 forced: the calling thread's rpst_conv2d_set_quarter, else the
+// RPST_W4Q environment variable, read per call (rpst_conv.hip)
+int conv_quarter_mode();
 size_t wino4q_packed_floats(int Cout, int Cin);
 int wino4q_pack(const float* w, float* pk, int Cout, int Cin, hipStream_t st);
 int wino4q_pack_mix(const double* wm, float* pk, int N, int Cout, int Cin, hipStream_t st);
@@ -289,6 +292,13 @@ int wino4q_launch(ConvArgs& a, int in_op, hipStream_t st);
 inline size_t wino4_image_floats(int Cout, int Cin, int in_op) {
   return wino4q_applies(Cin, Cout, in_op) ? wino4q_packed_floats(Cout, Cin)
                                           : wino4_packed_floats(Cout, Cin);
+}
+// the larger of the two images: workspace sizes use it, so a workspace sized under one
+// precise / quarter setting stays large enough for a launch under another (with Cout % 64
+// in 1..32 the quarter image is the larger one)
+inline size_t wino4_image_floats_max(int Cout, int Cin) {
+  const size_t q = wino4q_packed_floats(Cout, Cin), p = wino4_packed_floats(Cout, Cin);
+  return q > p ? q : p;
 }
 
 

@@ -686,8 +686,16 @@ static int conv_variant(int BM, int ksize, int in_op) {
 // rpst_conv2d_set_precise: at 1 this thread's launches keep to F(2x2) where F(4x4) would
 // run; at 2 F(4x4) runs, on its 32-channel form only (wino4q_applies)
 static thread_local int t_conv_precise = 0;
+// rpst_conv2d_set_quarter: -1 (default) follows RPST_W4Q, read per launch
+static thread_local int t_conv_quarter = -1;
 
 bool conv_quarter_allowed() { return t_conv_precise != 2; }
+
+int conv_quarter_mode() {
+  if (t_conv_quarter >= 0) return t_conv_quarter;
+  const char* e = getenv("RPST_W4Q");
+  return (e && *e) ? atoi(e) : 1;
+}
 
 static int conv_algo(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
   if (ksize != 3) return RPST_CONV_DIRECT;
@@ -839,8 +847,19 @@ extern "C" int rpst_conv2d_set_precise(int on) {
   return old;
 }
 
+extern "C" int rpst_conv2d_set_quarter(int mode) {
+  const int old = t_conv_quarter;
+  t_conv_quarter = mode < 0 ? -1 : (mode > 2 ? 2 : mode);
+  return old;
+}
+
 extern "C" int rpst_conv2d_algorithm(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
   return conv_algo(Cout, Cin, Hs, Ws, ksize, in_op);
+}
+
+extern "C" int rpst_conv2d_quarter(int Cout, int Cin, int Hs, int Ws, int ksize, int in_op) {
+  if (conv_algo(Cout, Cin, Hs, Ws, ksize, in_op) != RPST_CONV_WINOGRAD4) return 0;
+  return wino4q_applies(Cin, Cout, in_op) ? 1 : 0;
 }
 
 extern "C" int rpst_conv2d_pack(const float* weight, float* packed, int Cout, int Cin,
@@ -1193,8 +1212,23 @@ extern "C" int rpst_conv2d_skip_adain(const float* stylized, const float* conten
 extern "C" size_t rpst_conv2d_stats_workspace_size(int N, int Cin, int Hs, int Ws, int Cout,
                                                    int ksize, int in_op) {
   if (N <= 0 || Cin <= 0 || Hs <= 0 || Ws <= 0 || Cout <= 0 || (ksize != 1 && ksize != 3)) return 0;
-  const ConvGeom g = conv_geom(N, Cin, Hs, Ws, Cout, ksize, in_op, true);
-  const size_t stats = ((size_t)N * Cout * g.stat_P * sizeof(float2) + 255) / 256 * 256;
+  // the partial count depends on the kernel the thread's precise / quarter settings select:
+  // sized for the largest of them, so a workspace sized under one setting serves a launch
+  // under any other
+  int stat_P = 0;
+  {
+    const int sp = t_conv_precise, sq = t_conv_quarter;
+    for (int p = 0; p < 3; ++p)
+      for (int q = -1; q < 3; ++q) {
+        t_conv_precise = p;
+        t_conv_quarter = q;
+        const ConvGeom g = conv_geom(N, Cin, Hs, Ws, Cout, ksize, in_op, true);
+        stat_P = g.stat_P > stat_P ? g.stat_P : stat_P;
+      }
+    t_conv_precise = sp;
+    t_conv_quarter = sq;
+  }
+  const size_t stats = ((size_t)N * Cout * stat_P * sizeof(float2) + 255) / 256 * 256;
   return stats + fold_bytes(N, Cin, Hs, Ws, Cout, ksize, in_op);
 }
 

@@ -972,7 +972,7 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
 size_t wino4_fold_floats(int N, int Cin, int Cout) {
   // per-image packed U (the layout the folded NONE launch runs) and border biases, then the
   // class sums (fp64)
-  return (size_t)N * (wino4_image_floats(Cout, Cin, RPST_IN_NONE) + (size_t)Cout * 9) +
+  return (size_t)N * (wino4_image_floats_max(Cout, Cin) + (size_t)Cout * 9) +
          2 * (size_t)9 * Cout * Cin + 2;
 }
 

@@ -273,15 +273,14 @@ int wino4q_fold_w(const float* pk, float* out, const float* aux, int N, int Cout
 // input channels in multiples of 16 (a co tile = a whole number of 4-step ring turns).
 // Below 128 input channels a block's 8-16 K steps per co tile leave the prologue and the
 // 4-way epilogue exposed: 32->64 @512^2 N64 3.12 vs 2.54 ms, 64->128 8.16 vs 8.09 on the
-// 32-channel kernel (gpurun_out/w4q_d, profiles/r05). RPST_W4Q=0 turns it off, =2 forces it
-// on for every shape it supports (Cin >= 16; tests, A/B). A training step's constant
-// branches (rpst_conv2d_set_precise(2)) keep the 32-channel form: same per-conv error
-// (tools/conv_err.py), but the gradient goldens were pinned on its rounding pattern.
+// 32-channel kernel (gpurun_out/w4q_d, profiles/r05). Mode (conv_quarter_mode: the calling
+// thread's rpst_conv2d_set_quarter, else RPST_W4Q read per launch like RPST_CONV_ALGO): 0
+// off, 1 the rule above, 2 forced on for every shape it supports (Cin >= 16; parity tests,
+// A/B). A training step's constant branches (rpst_conv2d_set_precise(2)) keep the 32-channel
+// form: same per-conv error (tools/conv_err.py), but the gradient goldens were pinned on its
+// rounding pattern.
 bool wino4q_applies(int Cin, int Cout, int in_op) {
-  static const int en = [] {
-    const char* e = getenv("RPST_W4Q");
-    return (e && *e) ? atoi(e) : 1;
-  }();
+  const int en = conv_quarter_mode();
   const int min_cin = en == 2 ? 16 : 128;
   return en && conv_quarter_allowed() && (in_op == RPST_IN_NONE || in_op == RPST_IN_UPSAMPLE2) &&
          Cout >= 64 && Cout <= kQMaxCo &&

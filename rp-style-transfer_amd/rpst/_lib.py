@@ -35,6 +35,8 @@ SIGNATURES = {
     "rpst_conv2d_grid_threads": (_I64, [_I, _I, _I, _I, _I, _I, _I]),
     "rpst_conv2d_algorithm": (_I, [_I, _I, _I, _I, _I, _I]),
     "rpst_conv2d_set_precise": (_I, [_I]),
+    "rpst_conv2d_set_quarter": (_I, [_I]),
+    "rpst_conv2d_quarter": (_I, [_I, _I, _I, _I, _I, _I]),
     "rpst_conv2d_stats_workspace_size": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),
     "rpst_conv2d_stats": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I,
                                _P, _P, _F, _P, _SZ, _P]),

@@ -192,15 +192,21 @@ class Pipeline:
     and strategy of the PNGs (PIL's default level 6 and strategy is what
     torchvision.save_image writes; the pixels are identical at any setting: "rle" at level 6
     encodes ~6x faster for ~1.5 % larger files, level 0 stores). At most BACKLOG batches'
-    encodes are outstanding: past that, the loop waits for the oldest batch's files."""
+    encodes are outstanding: past that, the loop waits for the oldest batch's files.
+
+    check: called before the LAST batch's files are queued (e.g. WCTRPNet.check, which waits
+    for and raises on that batch's deferred WCT status). Every earlier batch is checked by
+    the model itself before its files are queued: its status is raised during the next
+    batch's stylize() call (ops.WCTStatusWatch), which runs before that batch's writes."""
 
     BACKLOG = 3
 
     def __init__(self, stylize: Callable[[torch.Tensor, torch.Tensor], torch.Tensor],
                  device, img_size: int, batch_size: int = 1, num_workers: int = 4,
                  cat: bool = True, png_level: int = 6, encode_workers: Optional[int] = None,
-                 png_strategy: str = "default"):
+                 png_strategy: str = "default", check: Optional[Callable[[], None]] = None):
         self.stylize = stylize
+        self.check = check
         self.device = torch.device(device)
         self.img_size = img_size
         self.batch_size = max(1, batch_size)
@@ -285,6 +291,8 @@ class Pipeline:
                     n += sum(f.result() for f in saves.popleft())
                 st["wait_encode"] += clock() - t4
             t3 = clock()
+            if self.check is not None:
+                self.check()
             saves.append(self._write_start(writers, *back, out_dir, log))
             while saves:
                 n += sum(f.result() for f in saves.popleft())

@@ -107,7 +107,8 @@ def main(argv=None) -> int:
     with torch.cuda.device(device):
         n = Pipeline(stylize, device, opt["img_size"], opt.get("batch_size", 1),
                      opt.get("num_workers", 4), png_level=args.png_compress_level,
-                     png_strategy=args.png_strategy, encode_workers=args.encode_workers).run(
+                     png_strategy=args.png_strategy, encode_workers=args.encode_workers,
+                     check=getattr(network, "check", None)).run(
                          dataset, str(out_dir), log=logger.info)
     logger.info(f"stylised {n} pairs into {out_dir}")
     return 0

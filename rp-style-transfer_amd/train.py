@@ -218,8 +218,11 @@ def main(argv=None) -> int:
             def stylize_fn(c, s):
                 return network.test(c, s, iterations=i)
 
+            # check: the last test batch's deferred WCT status is raised here, before its
+            # files are written, not at the next test run thousands of steps later
             Pipeline(stylize_fn, device, opt["img_size"], opt["batch_size"],
-                     opt.get("num_workers", 4)).run(test_set, str(out), log=logger.info)
+                     opt.get("num_workers", 4), check=getattr(network, "check", None)).run(
+                         test_set, str(out), log=logger.info)
         if i % opt["log_iter"] == 0:
             loss_str = "".join(f", {k} {v}" for k, v in scalars.items())
             logger.info(f"Iterations {_begin(network) + i}, elapsed time: {elapsed} {loss_str}")

@@ -163,6 +163,51 @@ def test_conv_algorithm_choice_is_host_only(monkeypatch):
     assert lib.rpst_conv2d_algorithm(3, 16, 512, 512, 3, 0) == NR
 
 
+def test_quarter_kernel_switch_is_per_launch(monkeypatch):
+    """rpst_conv2d_quarter / rpst_conv2d_set_quarter: the position-quarter F(4x4) kernel takes
+    the Cin >= 128 layers by default; RPST_W4Q is read per launch (0 off, 2 forced on every
+    shape it supports) and the thread-local setter overrides it; precise level 2 keeps the
+    32-channel form. Workspace sizes do not depend on the setting."""
+    monkeypatch.delenv("RPST_CONV_ALGO", raising=False)
+    monkeypatch.delenv("RPST_W4Q", raising=False)
+    lib = _lib.load()
+    q = lib.rpst_conv2d_quarter
+    assert q(256, 128, 512, 512, 3, 0) == 1
+    assert q(128, 64, 512, 512, 3, 0) == 0           # Cin < 128: 32-channel kernel
+    assert q(32, 128, 512, 512, 3, 0) == 0           # Cout < 64
+    assert q(128, 128, 64, 64, 3, 1) == 0            # max-pool loader: F(2x2)
+    assert q(64, 128, 23, 70, 3, 2) == 1             # upsample loader
+    assert q(200, 144, 19, 90, 3, 0) == 1            # Cin % 16 == 0, partial co tile
+    assert q(256, 136, 64, 64, 3, 0) == 0            # Cin % 16 != 0
+    sizes = (lib.rpst_conv2d_stats_workspace_size(2, 128, 37, 200, 256, 3, 0),
+             lib.rpst_conv2d_workspace_size(2, 256, 37, 70, 96, 3, 4),
+             lib.rpst_conv2d_mix_workspace_size(2, 128, 37, 70, 96, 3))
+    monkeypatch.setenv("RPST_W4Q", "0")
+    assert q(256, 128, 512, 512, 3, 0) == 0
+    monkeypatch.setenv("RPST_W4Q", "2")
+    assert q(128, 64, 512, 512, 3, 0) == 1
+    assert q(64, 16, 512, 512, 3, 0) == 1
+    assert q(32, 64, 512, 512, 3, 0) == 0            # Cout < 64 even when forced
+    assert (lib.rpst_conv2d_stats_workspace_size(2, 128, 37, 200, 256, 3, 0),
+            lib.rpst_conv2d_workspace_size(2, 256, 37, 70, 96, 3, 4),
+            lib.rpst_conv2d_mix_workspace_size(2, 128, 37, 70, 96, 3)) == sizes
+    old = lib.rpst_conv2d_set_quarter(0)
+    try:
+        assert old == -1
+        assert q(128, 64, 512, 512, 3, 0) == 0       # the setter wins over RPST_W4Q
+        lib.rpst_conv2d_set_quarter(2)
+        assert q(128, 64, 512, 512, 3, 0) == 1
+        p = lib.rpst_conv2d_set_precise(2)
+        try:
+            assert q(256, 128, 512, 512, 3, 0) == 0  # training constant branch
+        finally:
+            lib.rpst_conv2d_set_precise(p)
+    finally:
+        lib.rpst_conv2d_set_quarter(old)
+    monkeypatch.delenv("RPST_W4Q")
+    assert q(128, 64, 512, 512, 3, 0) == 0
+
+
 def test_plan_rejects_unfused_first_transform():
     """A plan whose first step is not a conv cannot fuse the WCT colour transform (first_mix)
     or an AdaIN input operator: run() must refuse instead of silently decoding raw features."""

@@ -279,3 +279,42 @@ def test_adaptive_requires_matching_spatial_dims(cuda):
     x = torch.rand(1, 16, 4, 4, device=cuda)
     with torch.no_grad(), pytest.raises(AssertionError):
         mod(x, x)
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("C,hw2,scale", [(512, (16, 16), 1.0), (64, (12, 16), 3.0)])
+def test_adaptive_forward_matches_backward_statistics(cuda, mode, C, hw2, scale):
+    """the training forward runs the two flash passes (P normalised by row
+    statistics summed in the flash kernel's key order), while rpst_adaptive_attention_backward
+    recomputes S and its row statistics with gemm_f32_kernel + rowstats_kernel -- the form the
+    keep_claims maps are made with. The output implied by that form, H Q_gemm^T, agrees with
+    the flash output to within 3x the flash output's own fp32 distance to float64, so the
+    gradients are taken at the point the forward reported (bound: max(3 e, 1e-6))."""
+    import network as net
+    from rpst import ops
+    B = 2
+    h, w = hw2
+    hw = h * w
+    mod = net.AEAModule(hw) if mode == "aea" else net.AEALReluModule(hw)
+    synth_(mod, 17)
+    sd = {k: v.double() for k, v in state_dict_of(mod).items()}
+    F = gen(15, (B, C, h, w), scale)
+    G = gen(16, (B, C, h, w), scale)
+    H = gen(17, (B, C, h, w), 1.0)
+    c = gen(18, (B, C, h, w), 1.0, 0.2, relu=True)
+    s = gen(19, (B, C, h, w), 1.0, 0.2, relu=True)
+    S = torch.bmm(F.view(B, C, -1).permute(0, 2, 1).double(), G.view(B, C, -1).double())
+    Q, _ = R.aea(R.cal_affinity_matrix(c.double(), s.double()), torch.softmax(S, -1), sd, "",
+                 mode)
+    ref64 = torch.bmm(H.view(B, C, -1).double(), Q.permute(0, 2, 1)).view(B, C, h, w)
+    mod = mod.to(cuda)
+    with torch.no_grad():
+        out, _, _, after = ops.adaptive_attention(
+            F.to(cuda), G.to(cuda), H.to(cuda), c.to(cuda), s.to(cuda), mod.f_psi, mod.mode,
+            50.0, 0.4, 0.5, keep_claims=True)
+    implied = torch.bmm(H.view(B, C, -1).double().to(cuda),
+                        after.double().permute(0, 2, 1)).view(B, C, h, w)
+    e = rel_l2(out, ref64)
+    mismatch = rel_l2(out, implied)
+    assert e < 1e-5, e
+    assert mismatch <= max(3 * e, 1e-6), (mismatch, e)

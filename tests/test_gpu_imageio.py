@@ -172,3 +172,41 @@ def test_stylize_png_strategies_same_pixels(cuda, tmp_path):
         assert got.keys() == ref.keys(), key
         for name in ref:
             np.testing.assert_array_equal(got[name], ref[name], err_msg=f"{key} {name}")
+
+
+def test_pipeline_checks_last_batch_wct_status(cuda, tmp_path, monkeypatch):
+    """The stylize.py / train.py pipeline passes WCTRPNet.check as Pipeline(check=...): a WCT
+    failure in the LAST batch (its status is deferred one call, ops.WCTStatusWatch) raises
+    before that batch's files are written; earlier batches are written."""
+    import copy
+
+    import network as net
+    from network import wct_rp
+    from rpst.imageio import PairedDataset, Pipeline
+    from helpers import rp_config, synth_
+    monkeypatch.setattr(wct_rp, "CHECK_WCT", False)
+    monkeypatch.delenv("RPST_MATFUN_DEBUG_SKIP", raising=False)
+    root = str(tmp_path / "data")
+    names = _write_pairs(root, [(40, 30, "RGB"), (32, 32, "RGB")])
+    m = net.WCTRPNet(rp_config(8), copy.deepcopy(net.vgg))  # C = 128: four-workgroup groups
+    synth_(m, 7)
+    m = m.to(cuda)
+    calls = []
+
+    def fn(c, s):
+        if calls:  # the second (last) batch: force the persistent launch's timeout
+            monkeypatch.setenv("RPST_MATFUN_DEBUG_SKIP", "1")
+        calls.append(1)
+        try:
+            return m.test(c, s)
+        finally:
+            monkeypatch.delenv("RPST_MATFUN_DEBUG_SKIP", raising=False)
+
+    out = tmp_path / "out"
+    with pytest.raises(RuntimeError, match="timeout"):
+        Pipeline(fn, cuda, 32, 1, 1, check=m.check).run(PairedDataset(root), str(out))
+    assert len(calls) == 2
+    written = sorted(p.name for p in out.glob("*.png"))
+    first = os.path.splitext(names[0])[0]
+    assert all(w.startswith(f"{first}-") for w in written), written
+    m.check()  # nothing left pending

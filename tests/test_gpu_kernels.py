@@ -142,14 +142,31 @@ CONV_CASES = [
     (2, 16, 17, 70, 3, 3, 1, 0, False),     # narrow: 16->3 reflect, no relu
     (1, 4, 9, 66, 16, 3, 1, 0, True),       # narrow: Cin 4 -> 16
     (1, 16, 2, 2, 4, 3, 1, 0, False),       # narrow: tiny reflect
+    # position-quarter F(4x4) kernel (Cin >= 128, the default for 64 % of the configs[1] step):
+    # interior (16-B DMA) and edge column tiles in one launch, ragged 8-row tiles, partial
+    # 64-channel co tiles, W % 4 != 0 (the scalar store path), both paddings, the upsample loader
+    (2, 128, 37, 200, 256, 3, 0, 0, True),  # 4 column tiles (2 interior), H % 8 = 5
+    (1, 256, 45, 260, 128, 3, 1, 0, True),  # reflect, 5 column tiles, 32 K steps per co tile
+    (1, 128, 23, 70, 64, 3, 0, 2, True),    # upsample loader (46 x 140), one co tile
+    (1, 144, 19, 90, 200, 3, 1, 0, True),   # Cout 200: last co tile 8 channels; W % 4 = 2
+    (2, 128, 13, 66, 96, 3, 0, 0, False),   # Cout 96, no activation, W % 4 = 2, H < 2 tiles
+    (1, 512, 9, 140, 256, 3, 1, 2, True),   # upsample loader from a ragged source, 128 K steps
 ]
 
 
-@pytest.fixture(params=["direct", "winograd", "winograd4"])
+@pytest.fixture(params=["direct", "winograd", "winograd4", "winograd4_32", "winograd4q"])
 def conv_algo(request, monkeypatch):
-    """Run a 3x3 conv test on every algorithm (librpst reads RPST_CONV_ALGO per launch;
-    winograd4 falls back to winograd for the loader operators it does not implement)."""
-    monkeypatch.setenv("RPST_CONV_ALGO", request.param)
+    """Run a 3x3 conv test on every algorithm (librpst reads RPST_CONV_ALGO and RPST_W4Q per
+    launch; winograd4 falls back to winograd for the loader operators it does not implement).
+    winograd4 is F(4x4) under the production rule (the position-quarter kernel for Cin >=
+    128), winograd4_32 keeps every F(4x4) layer on the 32-channel kernel (RPST_W4Q=0) and
+    winograd4q forces the position-quarter kernel on every shape it supports (RPST_W4Q=2:
+    Cin >= 16, Cin % 16 == 0, Cout >= 64)."""
+    algo = {"winograd4_32": "winograd4", "winograd4q": "winograd4"}.get(request.param,
+                                                                        request.param)
+    monkeypatch.setenv("RPST_CONV_ALGO", algo)
+    monkeypatch.setenv("RPST_W4Q", {"winograd4_32": "0", "winograd4q": "2"}.get(request.param,
+                                                                               "1"))
     return request.param
 
 
@@ -168,6 +185,16 @@ def test_conv2d_vs_torch(cuda, case, conv_algo):
                      aux=None if aux is None else aux.to(cuda))
     assert out.shape == ref.shape
     assert rel_l2(out, ref) < 1e-5, rel_l2(out, ref)
+    if k == 3 and in_op in (0, 2):  # which F(4x4) kernel ran
+        from rpst import _lib
+        quarter = _lib.load().rpst_conv2d_quarter(cout, cin, hs, ws, k, in_op)
+        q_shape = cin >= 16 and cin % 16 == 0 and 64 <= cout <= 512
+        if conv_algo == "winograd4q":
+            assert quarter == int(q_shape)
+        elif conv_algo == "winograd4":
+            assert quarter == int(q_shape and cin >= 128)
+        else:
+            assert quarter == 0
 
 
 def test_conv2d_residual(cuda):
@@ -259,12 +286,18 @@ def test_conv_dgrad_masked_matches_relu_backward(cuda, case, conv_algo):
     (2, 16, 33, 65, 32, 0, 0, True),     # NR = 2 block (Cin * Cout <= 512), odd width
     (1, 64, 18, 22, 64, 0, 0, False),    # no activation
     (1, 32, 10, 17, 32, 1, 2, True),     # nearest-upsample loader
+    (2, 128, 37, 70, 128, 1, 0, True),   # quarter kernel: VGG relu3_x-like, odd height
+    (1, 256, 21, 134, 64, 0, 0, True),   # quarter kernel: interior column tile, ragged rows
+    (1, 128, 11, 35, 96, 1, 2, False),   # quarter kernel: upsample loader, partial co tile
 ])
-def test_conv2d_pool_matches_conv_then_pool(cuda, case, monkeypatch):
+@pytest.mark.parametrize("w4q", ["0", "2"])
+def test_conv2d_pool_matches_conv_then_pool(cuda, case, w4q, monkeypatch):
     """rpst_conv2d_pool (the 2x2 ceil-mode max pool taken in the F(4x4) epilogue) is
-    bit-identical to rpst_conv2d followed by rpst_maxpool2x2_ceil."""
+    bit-identical to rpst_conv2d followed by rpst_maxpool2x2_ceil, on the 32-channel kernel
+    (RPST_W4Q=0) and with the position-quarter kernel on every shape it supports (=2)."""
     from rpst import ops
     monkeypatch.setenv("RPST_CONV_ALGO", "winograd4")
+    monkeypatch.setenv("RPST_W4Q", w4q)
     n, cin, h, w_, cout, pad, in_op, relu = case
     x = gen(47, (n, cin, h, w_), 1.0, -0.2).to(cuda)
     wt = gen(48, (cout, cin, 3, 3), (2.0 / (cin * 9)) ** 0.5).to(cuda)
@@ -463,7 +496,11 @@ def test_vgg_and_decoder_golden(cuda, golden):
 
 # ---- fused AdaIN (statistics in the producing conv's epilogue, apply in the consumer's loader)
 @pytest.mark.parametrize("shape", [(2, 16, 64, 96, 256), (1, 8, 17, 45, 64), (3, 3, 9, 7, 32),
-                                   (2, 64, 40, 40, 128), (2, 32, 40, 200, 64)])
+                                   (2, 64, 40, 40, 128), (2, 32, 40, 200, 64),
+                                   # quarter kernel (stat_merge_t_kernel): ragged rows and
+                                   # interior + edge column tiles, a partial co tile
+                                   (2, 128, 37, 200, 256), (1, 256, 45, 130, 128),
+                                   (2, 128, 19, 70, 96)])
 def test_conv2d_stats_equal_calc_mean_std(cuda, shape, conv_algo):
     from rpst import ops
     n, cin, h, w, cout = shape
@@ -516,7 +553,12 @@ def test_conv2d_stats_store_head(cuda, shape, store, conv_algo):
 @pytest.mark.parametrize("fold", [True, False])
 @pytest.mark.parametrize("pad,shape,cin,cout", [(0, (2, 24, 40), 32, 16),
                                                 (0, (3, 37, 70), 64, 48),
-                                                (1, (2, 37, 70), 40, 32)])
+                                                (1, (2, 37, 70), 40, 32),
+                                                # quarter kernel's bias table (BTAB): the
+                                                # AdaIN-RP decoder's 256 -> 128 shape, ragged
+                                                (0, (2, 37, 200), 256, 128),
+                                                (1, (1, 23, 134), 128, 96),
+                                                (0, (2, 19, 66), 128, 64)])
 def test_conv2d_adain_input_op(cuda, conv_algo, fold, pad, shape, cin, cout):
     """AdaIN -> conv: fold=True runs the F(4x4) conv with the affine folded into per-image
     weights and a border-class bias (rpst_conv2d_ws), fold=False the in-loader affine."""
