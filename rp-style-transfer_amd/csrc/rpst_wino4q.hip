@@ -71,7 +71,14 @@ __device__ __forceinline__ bool q_resolve(int& v, int n, bool zero_pad) {
   return in || !zero_pad;
 }
 // A^T applied to one 6-vector -> 4 values
+#ifndef RPST_W4Q_DBG
+#define RPST_W4Q_DBG 0
+#endif
 __device__ __forceinline__ void q_at6(const float (&m)[6], float (&p)[4]) {
+  if (RPST_W4Q_DBG & 256) {  // timing only: no output transform
+    p[0] = m[0]; p[1] = m[1]; p[2] = m[2]; p[3] = m[3] + m[4] + m[5];
+    return;
+  }
   const float s12 = m[1] + m[2], d12 = m[1] - m[2];
   const float s34 = m[3] + m[4], d34 = m[3] - m[4];
   p[0] = (m[0] + s12) + s34;
@@ -151,10 +158,9 @@ constexpr int kQDMA4 = 3, kQDMA = 11;        // patch pieces per channel: 16-B /
 constexpr int kQXS = 4 * 3 * 3 * 64 * 2;     // epilogue exchange floats per tile row and pass
 // timing-only experiments (results wrong; tools/build_variants.sh -DRPST_W4Q_DBG=n): 1 no patch
 // DMA, 2 no weight DMA, 4 no epilogue exchange, 8 no input transform, 16 no step barriers,
-// 32 no epilogue at all, 128 no DMA waits
-#ifndef RPST_W4Q_DBG
-#define RPST_W4Q_DBG 0
-#endif
+// 32 no epilogue at all, 64 no output stores (issued never), 128 no DMA waits, 256 no output
+// transform. Round 6 on the final kernel, 128->256 @512^2 N64 (profiles/r06/epilogue_ab.log):
+// 26.8 ms; no epilogue 25.3; no output stores 24.8; no exchange 25.7; no transform 26.1
 #ifndef RPST_W4Q_WG0
 #define RPST_W4Q_WG0 0  // MFMA group of a step whose issue slot takes the first W(x + 1) piece
 #endif
@@ -426,7 +432,8 @@ __device__ __forceinline__ void q_finish(const QEpi& e, int co, float (&Y)[16], 
         for (int xx = 0; xx < 4; ++xx) sum += (yy < rows && gx0 + xx < e.W) ? Y[yy * 4 + xx] : 0.f;
     }
   }
-  if (e.bst) {
+  if ((RPST_W4Q_DBG & 64) && e.statP > -7) {  // timing only: the stores never taken
+  } else if (e.bst) {
     const auto ro = q_rsrc(e.oimg, e.obytes, true);
     const unsigned cofs = cok ? (unsigned)co * (unsigned)(e.H * e.W) * 4u : 0x7fffffffu;
 #pragma unroll

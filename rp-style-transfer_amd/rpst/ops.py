@@ -223,7 +223,10 @@ class precise_convs:
             on = self.on
         else:
             on = not TRAIN_F4.get(self.model, False)
-        self._old = _lib.load().rpst_conv2d_set_precise(1 if on else 2)
+        # RPST_TRAIN_QUARTER=1: the constant branches may take the position-quarter kernel
+        # too (level 0 instead of 2; accuracy / speed A/B)
+        quarter = os.environ.get("RPST_TRAIN_QUARTER", "") == "1"
+        self._old = _lib.load().rpst_conv2d_set_precise(1 if on else (0 if quarter else 2))
         return self
 
     def __exit__(self, *exc):

@@ -654,6 +654,76 @@ def gen_grads_ms(net):
     np.savez_compressed(os.path.join(HERE, "grads_ms.npz"), n=len(cases), **out)
 
 
+def _reference_model(net, family, g, i):
+    """The reference model of case i of golden file `family` (grads*.npz), synth weights."""
+    if family in ("grads", "grads_wct"):
+        cfg = dict(rp_config(int(g[f"hidden{i}"])), content_weight=float(g[f"cw{i}"]),
+                   style_weight=float(g[f"sw{i}"]))
+        m = (net.AdaINRPNet if family == "grads" else net.WCTRPNet)(cfg, copy.deepcopy(net.vgg))
+    elif family in ("grads_sam", "grads_adaptive"):
+        cfg = dict(SAM_CFG)
+        if family == "grads_adaptive":
+            cfg["ada_module"] = str(g[f"mode{i}"])
+        cls = net.SAModel if family == "grads_sam" else net.AdaptiveSAModel
+        m = cls(cfg, copy.deepcopy(net.vgg), 0, g[f"content{i}"].shape[-1])
+        m.decoder = copy.deepcopy(m.decoder)
+    elif family == "grads_src":
+        m = net.SourceNet({"use_mask": False, "content_weight": float(g[f"cw{i}"]),
+                           "style_weight": float(g[f"sw{i}"])}, copy.deepcopy(net.vgg))
+        m.decoder = copy.deepcopy(m.decoder)
+    else:  # grads_ms
+        cfg = multiscale_config(int(g[f"hidden{i}"]), int(g[f"blocks{i}"]), int(g[f"inception{i}"]))
+        cfg.update(enc_stack_way=str(g[f"way{i}"]), content_weight=float(g[f"cw{i}"]),
+                   style_weight=float(g[f"sw{i}"]))
+        m = net.MultiScaleAdaINRPNet(cfg, copy.deepcopy(net.vgg))
+    ck = synth_model_(m, int(g[f"seed{i}"]))
+    assert np.array_equal(ck, g[f"checksum{i}"]), (family, i)
+    return m
+
+
+def gen_grad_floors(net):
+    """The reference's own fp32 noise floor of every training-gradient golden (VERDICT r05
+    item 4). Each case of grads / grads_wct / grads_sam / grads_src / grads_ms /
+    grads_adaptive runs through the REFERENCE model twice: in fp32 (reproducing the committed
+    golden; checked) and in float64 (m.double(), float64 inputs). Stored per gradient tensor:
+    the floor rel-L2(fp32, float64) of the WHOLE tensor, and the float64 gradient's probe
+    (helpers.grad_probe), which pins the oracle's float64 gradients to the reference's at
+    test time. Per loss: rel-L2(fp32, float64). (A probe difference is not a floor: a random
+    rounding error of relative norm e moves a probe by only ~e / sqrt(n).) The GPU tests hold
+    each gradient tensor to max(1e-4, 3 x its floor) in full-tensor rel-L2."""
+    out = {}
+    for family in ("grads", "grads_wct", "grads_sam", "grads_src", "grads_ms",
+                   "grads_adaptive"):
+        g = np.load(os.path.join(HERE, f"{family}.npz"))
+        for i in range(int(g["n"])):
+            res = {}
+            for dt in (torch.float32, torch.float64):
+                m = _reference_model(net, family, g, i).to(dt)
+                if family == "grads_wct" and dt == torch.float64:
+                    # fuse() returns .float() (wct_rp.py:166): widen it back
+                    m.fuse = (lambda mm: lambda c, s: type(mm).fuse(mm, c, s).double())(m)
+                m.zero_grad()
+                d, tot = m.forward(t(g[f"content{i}"]).to(dt), t(g[f"style{i}"]).to(dt))
+                tot.backward()
+                res[dt] = ({k: v.detach() for k, v in d.items()},
+                           {k: p.grad.detach() for k, p in m.named_parameters() if p.grad is not None})
+            (l32, g32), (l64, g64) = res[torch.float32], res[torch.float64]
+            for k in l64:
+                if f"{k}{i}" in g:
+                    assert helpers.rel_l2(l32[k], g[f"{k}{i}"]) == 0.0, (family, i, k)
+                    out[f"{family}/{i}/loss:{k}"] = np.array(helpers.rel_l2(l32[k], l64[k]))
+            for name in (str(n) for n in g[f"names{i}"]):
+                if f"grad{i}:{name}" in g:  # the fp32 run reproduces the golden
+                    assert helpers.rel_l2(g32[name], g[f"grad{i}:{name}"]) == 0.0, (family, i, name)
+                else:
+                    assert np.array_equal(helpers.grad_probe(name, g32[name]), g[f"gprobe{i}:{name}"])
+                out[f"{family}/{i}:{name}"] = np.array(helpers.rel_l2(g32[name], g64[name]))
+                out[f"{family}/{i}/p64:{name}"] = helpers.grad_probe(name, g64[name])
+            print(family, i, "worst floor", max(float(v) for k, v in out.items()
+                                                if k.startswith(f"{family}/{i}:")), flush=True)
+    np.savez_compressed(os.path.join(HERE, "grad_floors.npz"), **out)
+
+
 def gen_keys(net):
     """state_dict key/shape lists of the reference models (checkpoint compatibility)."""
     import json
@@ -683,7 +753,8 @@ GENERATORS = {"keys": gen_keys, "stats": gen_stats, "adain_rp": gen_adain_rp,
               "grads_wct": gen_grads_wct, "wct_large": gen_wct_large,
               "grads_sam": gen_grads_sam, "grads_src": gen_grads_src,
               "grads_ms": gen_grads_ms, "wct_edge": gen_wct_edge,
-              "grads_adaptive": gen_grads_adaptive, "wct_original": gen_wct_original}
+              "grads_adaptive": gen_grads_adaptive, "wct_original": gen_wct_original,
+              "grad_floors": gen_grad_floors}
 
 
 def main():

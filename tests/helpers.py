@@ -88,3 +88,41 @@ def probe_err(ours, ref, n):
     return max(abs(ours[0] - ref[0]) / (nrm * np.sqrt(n)),
                abs(np.sqrt(max(ours[1], 0.0)) - nrm) / nrm,
                abs(ours[2] - ref[2]) / (nrm * np.sqrt(n / 3.0)))
+
+
+TOL_GRAD = 1e-4  # training gradients: base bar per tensor / probe (rel-L2 scale)
+_FLOORS = None
+
+
+def grad_bar(family, i, name, base=TOL_GRAD):
+    """Bar of one training-gradient golden: max(base, 3 x the reference's own fp32 noise
+    floor), the floor being the committed fp32 golden's distance to the same REFERENCE model
+    re-run in float64 (tests/golden/grad_floors.npz, gen_golden.gen_grad_floors): a
+    form as accurate as the reference's own fp32 passes whatever its rounding pattern."""
+    global _FLOORS
+    if _FLOORS is None:
+        import os
+        _FLOORS = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                            "golden", "grad_floors.npz")))
+    return max(base, 3.0 * float(_FLOORS[f"{family}/{i}:{name}"]))
+
+
+def check_grads_vs_fp64(family, i, named, g64, skip=()):
+    """Training gradients `named` (name -> parameter with .grad, on the GPU) against float64
+    gradients g64 of the oracle on the same weights and inputs: each g64 tensor is first
+    pinned to the REFERENCE's float64 gradient (its probe in grad_floors.npz, to 1e-9), then
+    every gradient tensor is held to grad_bar in full-tensor rel-L2. Returns the worst
+    err / bar (x 1e-4)."""
+    global _FLOORS
+    grad_bar(family, i, next(iter(g64)))  # loads _FLOORS
+    worst = 0.0
+    for name, ref in g64.items():
+        if name in skip:
+            continue
+        pin = probe_err(grad_probe(name, ref), _FLOORS[f"{family}/{i}/p64:{name}"], ref.numel())
+        assert pin < 1e-9, (family, i, name, "oracle float64 off the reference's", pin)
+        e = rel_l2(named[name].grad, ref)
+        bar = grad_bar(family, i, name)
+        worst = max(worst, e / bar * 1e-4)
+        assert e < bar, (family, i, name, e, bar)
+    return worst

@@ -203,10 +203,12 @@ def test_pipeline_checks_last_batch_wct_status(cuda, tmp_path, monkeypatch):
             monkeypatch.delenv("RPST_MATFUN_DEBUG_SKIP", raising=False)
 
     out = tmp_path / "out"
+    ds = PairedDataset(root)
+    assert len(ds) == len(names) == 2
     with pytest.raises(RuntimeError, match="timeout"):
-        Pipeline(fn, cuda, 32, 1, 1, check=m.check).run(PairedDataset(root), str(out))
+        Pipeline(fn, cuda, 32, 1, 1, check=m.check).run(ds, str(out))
     assert len(calls) == 2
     written = sorted(p.name for p in out.glob("*.png"))
-    first = os.path.splitext(names[0])[0]
-    assert all(w.startswith(f"{first}-") for w in written), written
+    _, _, cn, sn, _, _ = ds.item(0)  # the first (clean) batch's pair
+    assert written == sorted([f"{cn}-{sn}.png", f"{cn}-{sn}-cat.png"]), written
     m.check()  # nothing left pending
