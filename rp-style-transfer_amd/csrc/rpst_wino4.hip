@@ -71,6 +71,14 @@ constexpr int kW4BM = 32;                  // output channels per co tile
 constexpr int kW4TH = 16, kW4TW = 64;      // output rows x columns per block
 constexpr int kW4PH = kW4TH + 2;           // patch rows
 constexpr int kW4PS = 68;                  // patch row stride (floats): 66 columns + 2 spare
+// window columns 4-7 read as a second ds_read_b128 (round 6) instead of 4-5 as a b64: the b64
+// reads of the four channel groups k of a wave hit the same banks (channel stride 768 floats
+// = 0 mod 64 banks): 13-17 % of LDS cycles bank-conflicted on the small-Cin layers
+// (profiles/r05_sq_layers.csv), 0 % with the b128 (profiles/r06/sq_rd128.log); layer times
+// unchanged within noise (32->64 2.52 / 2.55 ms, 64->128 7.91 / 7.93, profiles/r06/rd128_ab.log)
+#ifndef RPST_W4_RD128
+#define RPST_W4_RD128 1
+#endif
 constexpr int kW4CS = 1280;                // channel stride (floats)
 constexpr int kW4DMA = 20;                 // 4-B LDS-DMA pieces per patch channel (64 floats)
 constexpr int kW4DMA4 = 5;                 // 16-B pieces (256 floats) on interior blocks
@@ -555,6 +563,19 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
     const float* pr = pbuf + k * Geo::CS + (4 * wr + ph) * kW4PS + 4 * tn;
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
+#if RPST_W4_RD128
+      // columns 4 tn + 4 .. + 7 as a second ds_read_b128 (the empty asm keeps it whole: the
+      // compiler narrows it to the b64 of the 2 columns used, whose k-groups share banks)
+      floatx4 u = *reinterpret_cast<const floatx4*>(pr + r * kW4PS);
+      floatx4 v = *reinterpret_cast<const floatx4*>(pr + r * kW4PS + 4);
+      asm("" : "+v"(u), "+v"(v));
+      d[r][0] = u[0];
+      d[r][1] = u[1];
+      d[r][2] = u[2];
+      d[r][3] = u[3];
+      d[r][4] = v[0];
+      d[r][5] = v[1];
+#else
       const float4 u = *reinterpret_cast<const float4*>(pr + r * kW4PS);
       const float2 v = *reinterpret_cast<const float2*>(pr + r * kW4PS + 4);
       d[r][0] = u.x;
@@ -563,6 +584,7 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
       d[r][3] = u.w;
       d[r][4] = v.x;
       d[r][5] = v.y;
+#endif
     }
   };
   // one K step of 4 channels from a stage (its rows already in d): 72 VALU of input

@@ -188,20 +188,24 @@ def _conv_name(ksize, cin, cout, hs, ws, n, in_op):
     return f"{algo}{ksize}x{ksize} {cin}->{cout} {h}x{w} N{n} op{in_op}"
 
 
-# Training: every conv on a differentiated chain runs F(2x2) ("precise mode"). With F(4x4)
-# everywhere the reference-gradient goldens stay inside 1e-4 (tools/grad_precision_ab.py,
-# profiles/r04c: AdaIN-RP 7.3e-5, MultiScale 4.4e-5, SourceNet 6.2e-5, WCT 6.8e-7, SAModel
-# 8.0e-5 of its bar), but the CPU-autograd check at hidden 8, 40x56 does not (AdaIN-RP
-# rp_shared_encoder.0.weight 3.3e-3, profiles/r04e), so F(4x4) is kept to the step's
-# constant branches (precise_convs(on=False)): the VGG loss targets, WCT-RP's detached
-# encoder + WCT, the frozen VGG features of SourceNet. SAModel's frozen VGG features stay
-# precise: they feed the differentiated attention transforms, and on F(4x4) a
-# sanet5_1.h.weight gradient moves 1.06e-4 against its 1e-4 bar (profiles/r04g). TRAIN_F4
-# opts a whole step in. Where a training step runs F(4x4) it runs the 32-channel form
-# (rpst_conv2d_set_precise(2)), not the round-5 position-quarter kernel: the per-conv error
-# is the same (tools/conv_err.py), but SourceNet's frozen-VGG gradient probe, pinned on the
-# 32-channel rounding, reads 2.9e-4 against 1e-4 on the quarter kernel (6.1e-5 on its own).
-TRAIN_F4 = {"adain": False, "multiscale": False, "wct": False, "sanet": False, "source": False}
+# Training conv forms, chosen on the gradient bars derived from the reference's own fp32
+# noise floor (tests/test_gpu_train.py, tests/golden/grad_floors.npz; round 6, VERDICT r05
+# item 4). A family in TRAIN_F4 runs F(4x4) (the 32-channel form) on every chain of its
+# step; the others run F(2x2) ("precise mode") on the differentiated chains and F(4x4) only
+# on the step's constant branches (precise_convs(on=False): the VGG loss targets, WCT-RP's
+# detached encoder + WCT, SourceNet's frozen VGG). Measured (profiles/r06/train_forms.log):
+#   WCT-RP, MultiScale, SourceNet: every test green with F(4x4) throughout, training
+#     108.9 -> 118.9, 168.4 -> 188.0, 185.8 -> 206.7 img/s;
+#   AdaIN-RP: the CPU-autograd check at hidden 8, 40x56 reads rp_shared_encoder.0.weight
+#     3.3e-3 against its 1e-4 floor bar (64.3 -> 75.0 img/s forgone);
+#   SAModel / AdaptiveSAModel: the losses move 2.7e-4 against the reference's ~1e-7 floor
+#     (their frozen VGG features feed the attention, ~1e3 x amplification), and the steps are
+#     slower on F(4x4) anyway (42.8 -> 39.8, 39.8 -> 37.2 img/s); their frozen features stay
+#     precise too.
+# Where a training step runs F(4x4) it runs the 32-channel form (rpst_conv2d_set_precise(2)),
+# not the position-quarter kernel: on the quarter kernel SourceNet's decoder.1.weight gradient
+# reads 7.4e-4 against its 6.0e-4 floor bar (RPST_TRAIN_QUARTER=1 is the A/B switch).
+TRAIN_F4 = {"adain": False, "multiscale": True, "wct": True, "sanet": False, "source": True}
 
 
 class precise_convs:
@@ -217,10 +221,13 @@ class precise_convs:
 
     def __enter__(self):
         env = os.environ.get("RPST_TRAIN_PRECISE")
+        f4 = os.environ.get("RPST_TRAIN_F4")  # comma list of families: TRAIN_F4 override (A/B)
         if env is not None and env != "":
             on = env != "0"
         elif self.on is not None:
             on = self.on
+        elif f4 is not None:
+            on = self.model not in f4.split(",")
         else:
             on = not TRAIN_F4.get(self.model, False)
         # RPST_TRAIN_QUARTER=1: the constant branches may take the position-quarter kernel
