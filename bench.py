@@ -268,10 +268,10 @@ def cpu_baseline(kind, size, reps=3, batch=None):
                       f"{threads} torch threads = the CPUs this job is allotted ({share_src})"}
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05_pmc_traffic_config1.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r06_pmc_traffic_config1.json")
 # per-config PMC tables (tools/prof_pmc_configs.sh: FETCH_SIZE / WRITE_SIZE passes over
 # `bench.py --config k`, attributed per launch by tools/pmc_traffic.py): config -> table
-PMC_CONFIG = {i: os.path.join(ROOT, "profiles", f"r05_pmc_traffic_config{i}.json")
+PMC_CONFIG = {i: os.path.join(ROOT, "profiles", f"r06_pmc_traffic_config{i}.json")
               for i in (1, 2, 3, 4)}
 
 

@@ -32,6 +32,9 @@
 // the design minimises VALU per MFMA; measured alternatives and their timings:
 // profiles/r01_wino4_variants.log, profiles/r02_wino4_variants.log.
 #include "rpst_conv.h"
+#ifndef RPST_W4_CPOL
+#define RPST_W4_CPOL 0  // output-store cache policy (aux bits of buffer_store), A/B only
+#endif
 #include "rpst_wct.h"
 
 #include <type_traits>
@@ -780,7 +783,7 @@ __global__ __launch_bounds__(W4Geo<NR>::NTH, W4Geo<NR>::LAUNCH_WPE) void wino4_m
       for (int yy = 0; yy < 4; ++yy) {
         const floatx4 v = {Y[yy * 4], Y[yy * 4 + 1], Y[yy * 4 + 2], Y[yy * 4 + 3]};
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro,
-                                               (int)(e.voff[yy] + cofs), 0, 0);
+                                               (int)(e.voff[yy] + cofs), 0, RPST_W4_CPOL);
       }
     } else if (e.pool) {
       // max_pool2d(2, 2, ceil_mode) of the finished tile: tiles start on even rows and

@@ -23,6 +23,9 @@
 // quarters' 16-channel blocks through a weight stage (6 passes of 2 accumulator elements x 3
 // positions) and finishes its own block with the full output transform.
 #include "rpst_conv.h"
+#ifndef RPST_W4_CPOL
+#define RPST_W4_CPOL 0  // output-store cache policy (aux bits of buffer_store), A/B only
+#endif
 
 #include <type_traits>
 
@@ -440,7 +443,7 @@ __device__ __forceinline__ void q_finish(const QEpi& e, int co, float (&Y)[16], 
     for (int yy = 0; yy < 4; ++yy) {
       const floatx4 v = {Y[yy * 4], Y[yy * 4 + 1], Y[yy * 4 + 2], Y[yy * 4 + 3]};
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro,
-                                             (int)(e.voff[yy] + cofs), 0, 0);
+                                             (int)(e.voff[yy] + cofs), 0, RPST_W4_CPOL);
     }
   } else if (e.pool) {
     // max_pool2d(2, 2, ceil_mode) of the finished tile, fmaxf in maxpool2_kernel's order

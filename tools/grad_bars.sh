@@ -1,6 +1,6 @@
-# Round 6: training tests on the floor-derived gradient bars, then the worst err / bar per
+# training tests on the floor-derived gradient bars, then the worst err / bar per
 # golden case under each training conv setting (tools/grad_bars_ab.py).
-# Usage: bash tools/r06_grads.sh <tag>
+# Usage: bash tools/grad_bars.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-grads}

@@ -1,8 +1,8 @@
-# Round 6: which conv forms the training steps can take on the floor-derived gradient bars:
+# which conv forms the training steps can take on the floor-derived gradient bars:
 # the training test file under each setting (default: differentiated chains F(2x2), constant
 # branches F(4x4) 32-channel; RPST_TRAIN_QUARTER=1: constant branches may take the quarter
 # kernel; RPST_TRAIN_F4=...: F(4x4) on every chain of those families), then the training
-# benches of the SAModel and SourceNet steps. Usage: bash tools/r06_train_forms.sh <tag>
+# benches of the SAModel and SourceNet steps. Usage: bash tools/train_forms.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-forms}

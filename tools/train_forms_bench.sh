@@ -1,5 +1,5 @@
-# Round 6: training-step benches with the default training conv forms and with F(4x4) (the
-# 32-channel kernel) on every chain (RPST_TRAIN_F4=all families). Usage: bash tools/r06_train_bench.sh <tag>
+# training-step benches with the default training conv forms and with F(4x4) (the
+# 32-channel kernel) on every chain (RPST_TRAIN_F4=all families). Usage: bash tools/train_forms_bench.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-tb}
