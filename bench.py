@@ -341,10 +341,12 @@ def roofline_from_trace(summary, pmc_path=None, inference=True):
             "traffic_source": pmc_source(pmc_path) if traffic else None}
 
 
-def measure_adain_standalone(dev, n, c, hw, reps=3):
+def measure_adain_standalone(dev, n, c, hw, reps=7):
     """The model path fuses AdaIN into the encoder epilogue / decoder loader, so the
     HBM-bound AdaIN kernel pair (the function-level API, base.py:410-418) is timed on its
-    own here, on feature-shaped tensors of the benchmark (n, C, HW), after the timed loop."""
+    own here, on feature-shaped tensors of the benchmark (n, C, HW), after the timed loop.
+    It reports the median launch of `reps`: a host-side stall between the events of one
+    launch would otherwise move the mean."""
     import torch
     from rpst import ops
     g = torch.Generator(device=dev).manual_seed(0)
@@ -358,7 +360,7 @@ def measure_adain_standalone(dev, n, c, hw, reps=3):
         ops.adaptive_instance_normalization(x, y, out=out)
     for _ in range(reps):
         ops.calc_mean_std(x)
-    summary = ops.TRACE.summary()
+    summary = ops.TRACE.summary(median=True)
     ops.TRACE = None
     del x, y, out
     torch.cuda.empty_cache()

@@ -38,14 +38,22 @@ class Trace:
     def __init__(self):
         self.records = []
 
-    def summary(self):
+    def summary(self, median: bool = False):
+        """name -> {launches, ms (total), flops, bytes}. median=True reports launches x the
+        median launch time as "ms", so one launch delayed by host work between the events
+        (an idle GPU waiting on the host) does not move a short stand-alone measurement."""
         torch.cuda.synchronize()
-        agg = {}
+        agg, times = {}, {}
         for name, flops, nbytes, e0, e1 in self.records:
             ms = e0.elapsed_time(e1)
             a = agg.setdefault(name, {"launches": 0, "ms": 0.0, "flops": flops, "bytes": nbytes})
             a["launches"] += 1
             a["ms"] += ms
+            times.setdefault(name, []).append(ms)
+        if median:
+            for name, a in agg.items():
+                t = sorted(times[name])
+                a["ms"] = t[len(t) // 2] * a["launches"]
         return agg
 
 
