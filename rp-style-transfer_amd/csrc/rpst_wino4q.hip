@@ -149,7 +149,13 @@ __device__ __forceinline__ void q_bt3(float d0, float d1, float d2, float d3, fl
 
 constexpr int kQCo = 64;                     // output channels per co tile
 constexpr int kQTH = 8, kQTW = 64;           // output rows x columns per block
-constexpr int kQPS = 68;                     // patch row stride (floats): 66 columns + 2 spare
+#ifndef RPST_W4Q_AL
+// 1: patch rows staged from x0 - 4 (16-B aligned sources for the interior blocks' 16-B
+// pieces), column x0 - 1 at LDS column 3; 0: from x0 - 1 (4-B aligned sources)
+#define RPST_W4Q_AL 1
+#endif
+constexpr int kQXO = RPST_W4Q_AL ? 4 : 1;    // patch columns staged left of the tile
+constexpr int kQPS = RPST_W4Q_AL ? 72 : 68;  // patch row stride (floats): 66 used columns
 constexpr int kQCS = 768;                    // patch channel stride (floats)
 constexpr int kQWS = 9216;                   // weight floats per (co tile, K step)
 constexpr int kQPAT = 4 * kQCS;              // patch stage: 4 channels (12 KiB)
@@ -157,7 +163,8 @@ constexpr int kQNTH = 512;
 constexpr int kQMaxCo = 512;                 // output channels the LDS bias table holds
 constexpr int kQWPI = 5;                     // 1-KiB weight pieces per wave and step (36 / 8)
 constexpr int kQWide = 2, kQSlow = 6;        // patch pieces per wave and step: 16-B / 4-B
-constexpr int kQDMA4 = 3, kQDMA = 11;        // patch pieces per channel: 16-B / 4-B
+constexpr int kQDMA4 = 3, kQDMA = RPST_W4Q_AL ? 12 : 11;  // patch pieces per channel: 16-B / 4-B
+constexpr int kQRP = kQPS / 4;               // 16-B pieces per patch row
 constexpr int kQXS = 4 * 3 * 3 * 64 * 2;     // epilogue exchange floats per tile row and pass
 // timing-only experiments (results wrong; tools/build_variants.sh -DRPST_W4Q_DBG=n): 1 no patch
 // DMA, 2 no weight DMA, 4 no epilogue exchange, 8 no input transform, 16 no step barriers,
@@ -176,7 +183,7 @@ constexpr int kQXS = 4 * 3 * 3 * 64 * 2;     // epilogue exchange floats per til
 // profiles/r05/ahead_ab.log)
 #define RPST_W4Q_AHEAD 3
 #endif
-static_assert(10 * 17 <= kQDMA4 * 64 && kQDMA4 * 256 <= kQCS, "16-B pieces in a channel");
+static_assert(10 * kQRP <= kQDMA4 * 64 && kQDMA4 * 256 <= kQCS, "16-B pieces in a channel");
 static_assert(10 * kQPS <= kQDMA * 64 && kQDMA * 64 <= kQCS, "4-B pieces in a channel");
 static_assert(2 * kQWide >= kQDMA4 && 2 * kQSlow >= kQDMA && 8 * kQWPI >= 36, "coverage");
 static_assert(2 * kQXS <= kQWS, "the exchange fits a weight stage");
@@ -572,9 +579,13 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
 
   // patch of one K step: 4 channels x [10 rows][68] (66 columns + 2 spare) at channel stride
   // 768; waves 2c, 2c + 1 fill channel c. Interior blocks (every patch column inside the
-  // image, no upsampling): 16-B pieces (a 68-float row = 17 pieces, 170 per channel, 3
-  // wave-instructions: half 0 takes 0-1, half 1 takes 2 + a padding piece); elsewhere 4-B
-  // pieces (element 64 p + lane resolved against the padding, 11 per channel, 6 per half).
+  // image, no upsampling): 16-B pieces (a 72-float row from x0 - 4 = 18 pieces, 16-B aligned
+  // sources, 180 per channel, 3 wave-instructions: half 0 takes 0-1, half 1 takes 2 + a
+  // padding piece; columns x0 - 4 .. x0 - 2 and past x0 + 64 are staged but never read);
+  // elsewhere 4-B pieces (element 64 p + lane resolved against the padding, 12 per channel,
+  // 6 per half). RPST_W4Q_AL 0 stages from x0 - 1 (68-float rows, 4-B aligned sources):
+  // 128->256 N64 26.69-26.94 -> 26.55-26.61 ms, folded 256->128 13.01-13.12 -> 12.75-12.96
+  // (profiles/r06/aligned_patch_ab.log).
   // Per-lane source offsets are resolved once per block.
   const int hf = wave & 1;
   const bool zp = a.pad == RPST_PAD_ZERO;
@@ -586,10 +597,10 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < kQWide; ++i) {
       const int p = kQWide * hf + i;
-      const int f = 64 * p + lane, row = min(f / 17, 9), j = f - (f / 17) * 17;
+      const int f = 64 * p + lane, row = min(f / kQRP, 9), j = f - (f / kQRP) * kQRP;
       int y = y0 - 1 + row;
-      const bool ok = p < kQDMA4 && f < 170 && q_resolve(y, a.H, zp);
-      poff[i] = ok ? ((unsigned)(y * rs) + (unsigned)(x0 - 1 + 4 * j)) * 4u : oob;
+      const bool ok = p < kQDMA4 && f < 10 * kQRP && q_resolve(y, a.H, zp);
+      poff[i] = ok ? ((unsigned)(y * rs) + (unsigned)(x0 - kQXO + 4 * j)) * 4u : oob;
     }
 #pragma unroll
     for (int i = kQWide; i < kQSlow; ++i) poff[i] = oob;
@@ -599,9 +610,10 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
       const int p = kQSlow * hf + i;
       const int f = 64 * p + lane;
       const int row = min(f / kQPS, 9), col = f - (f / kQPS) * kQPS;
-      int y = y0 - 1 + row, x = x0 - 1 + col;
+      int y = y0 - 1 + row, x = x0 - kQXO + col;
       const bool oky = q_resolve(y, a.H, zp), okx = q_resolve(x, a.W, zp);
-      const bool ok = p < kQDMA && col < kQTW + 2 && f < 10 * kQPS && oky && okx;
+      const bool ok = p < kQDMA && col >= kQXO - 1 && col < kQXO + 1 + kQTW &&
+                      f < 10 * kQPS && oky && okx;
       poff[i] = ok ? ((unsigned)((up ? y >> 1 : y) * rs) + (unsigned)(up ? x >> 1 : x)) * 4u : oob;
     }
   }
@@ -644,7 +656,8 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < kQSlow - 1; ++i)
         q_dma4(r, xs + 64 * (h1 ? kQSlow + i : i), poffs[i][tid], so);
-      q_dma4(r, h1 ? dummy : xs + 64 * (kQSlow - 1), poffs[kQSlow - 1][tid], so);
+      q_dma4(r, h1 && !RPST_W4Q_AL ? dummy : xs + 64 * (h1 ? 2 * kQSlow - 1 : kQSlow - 1),
+             poffs[kQSlow - 1][tid], so);
     }
   };
   // before step x's barrier: W(x) (issued in step x - 1 ahead of its patch group) and
@@ -696,6 +709,17 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     // otherwise narrow them to the 5 floats a quarter uses, as bank-conflicted b32 reads)
     const int roff = k * kQCS + (4 * wr + QR) * kQPS + 4 * tn;
     auto read_row = [&](const float* stg, int rr, float (&d)[8]) {
+      if (RPST_W4Q_AL) {
+        // window columns 4 tn .. + 5 sit at LDS columns 4 tn + 3 .. + 8: the quarter's five
+        // (QC = 0: 0-4, QC = 1: 1-5) as one aligned ds_read_b128 and one ds_read_b32
+        const float* rp = stg + roff + rr * kQPS;
+        floatx4 u = *reinterpret_cast<const floatx4*>(rp + 4);
+        const float e = QC ? rp[8] : rp[3];
+        asm("" : "+v"(u));
+        d[0] = QC ? 0.f : e; d[1] = u[0]; d[2] = u[1]; d[3] = u[2]; d[4] = u[3];
+        d[5] = QC ? e : 0.f; d[6] = 0.f; d[7] = 0.f;
+        return;
+      }
       floatx4 u = *reinterpret_cast<const floatx4*>(stg + roff + rr * kQPS);
       floatx4 v = *reinterpret_cast<const floatx4*>(stg + roff + rr * kQPS + 4);
       asm("" : "+v"(u), "+v"(v));
