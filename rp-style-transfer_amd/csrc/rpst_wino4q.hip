@@ -154,6 +154,9 @@ constexpr int kQTH = 8, kQTW = 64;           // output rows x columns per block
 // pieces), column x0 - 1 at LDS column 3; 0: from x0 - 1 (4-B aligned sources)
 #define RPST_W4Q_AL 1
 #endif
+#ifndef RPST_W4Q_ALRD  // the odd window column: 1 = ds_read_b32, 2 = a whole ds_read_b128
+#define RPST_W4Q_ALRD 1
+#endif
 constexpr int kQXO = RPST_W4Q_AL ? 4 : 1;    // patch columns staged left of the tile
 constexpr int kQPS = RPST_W4Q_AL ? 72 : 68;  // patch row stride (floats): 66 used columns
 constexpr int kQCS = 768;                    // patch channel stride (floats)
@@ -711,13 +714,22 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     auto read_row = [&](const float* stg, int rr, float (&d)[8]) {
       if (RPST_W4Q_AL) {
         // window columns 4 tn .. + 5 sit at LDS columns 4 tn + 3 .. + 8: the quarter's five
-        // (QC = 0: 0-4, QC = 1: 1-5) as one aligned ds_read_b128 and one ds_read_b32
+        // (QC = 0: 0-4, QC = 1: 1-5) as two aligned ds_read_b128 (a ds_read_b32 for the odd
+        // one: all 64 lanes in one pass, and the four channel groups k share its banks)
         const float* rp = stg + roff + rr * kQPS;
-        floatx4 u = *reinterpret_cast<const floatx4*>(rp + 4);
-        const float e = QC ? rp[8] : rp[3];
-        asm("" : "+v"(u));
-        d[0] = QC ? 0.f : e; d[1] = u[0]; d[2] = u[1]; d[3] = u[2]; d[4] = u[3];
-        d[5] = QC ? e : 0.f; d[6] = 0.f; d[7] = 0.f;
+        if (RPST_W4Q_ALRD == 2) {
+          floatx4 e = *reinterpret_cast<const floatx4*>(rp + (QC ? 8 : 0));
+          floatx4 u = *reinterpret_cast<const floatx4*>(rp + 4);
+          asm("" : "+v"(e), "+v"(u));
+          d[0] = QC ? 0.f : e[3]; d[1] = u[0]; d[2] = u[1]; d[3] = u[2]; d[4] = u[3];
+          d[5] = QC ? e[0] : 0.f; d[6] = 0.f; d[7] = 0.f;
+        } else {
+          floatx4 u = *reinterpret_cast<const floatx4*>(rp + 4);
+          const float e = QC ? rp[8] : rp[3];
+          asm("" : "+v"(u));
+          d[0] = QC ? 0.f : e; d[1] = u[0]; d[2] = u[1]; d[3] = u[2]; d[4] = u[3];
+          d[5] = QC ? e : 0.f; d[6] = 0.f; d[7] = 0.f;
+        }
         return;
       }
       floatx4 u = *reinterpret_cast<const floatx4*>(stg + roff + rr * kQPS);
