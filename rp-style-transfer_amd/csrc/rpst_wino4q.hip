@@ -154,6 +154,9 @@ constexpr int kQTH = 8, kQTW = 64;           // output rows x columns per block
 // pieces), column x0 - 1 at LDS column 3; 0: from x0 - 1 (4-B aligned sources)
 #define RPST_W4Q_AL 1
 #endif
+#ifndef RPST_W4Q_EDGE
+#define RPST_W4Q_EDGE 1
+#endif
 #ifndef RPST_W4Q_ALRD  // the odd window column: 1 = ds_read_b32, 2 = a whole ds_read_b128
 #define RPST_W4Q_ALRD 1
 #endif
@@ -593,7 +596,14 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
   const int hf = wave & 1;
   const bool zp = a.pad == RPST_PAD_ZERO;
   const int rs = up ? a.Ws : a.W;
-  const bool wide = !up && x0 >= 1 && x0 + kQTW < a.W;
+  // RPST_W4Q_EDGE (with the aligned rows): in a row of W % 4 == 0 floats a 16-B piece is
+  // wholly inside or outside the image, so the full-width x-edge tiles take the 16-B pieces
+  // too: outside pieces read zero (zero padding), and reflect padding's one halo column is
+  // copied in after the stage lands (fix_halo)
+  const bool w4a = RPST_W4Q_AL && RPST_W4Q_EDGE && (a.W & 3) == 0;
+  const bool wide = !up && ((x0 >= 1 && x0 + kQTW < a.W) || (w4a && x0 + kQTW <= a.W));
+  const bool fixL = wide && w4a && !zp && x0 == 0;
+  const bool fixR = wide && w4a && !zp && x0 + kQTW == a.W;
   unsigned poff[kQSlow];
   const int tid = threadIdx.x;
   if (wide) {
@@ -602,8 +612,10 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
       const int p = kQWide * hf + i;
       const int f = 64 * p + lane, row = min(f / kQRP, 9), j = f - (f / kQRP) * kQRP;
       int y = y0 - 1 + row;
-      const bool ok = p < kQDMA4 && f < 10 * kQRP && q_resolve(y, a.H, zp);
-      poff[i] = ok ? ((unsigned)(y * rs) + (unsigned)(x0 - kQXO + 4 * j)) * 4u : oob;
+      const int xs = x0 - kQXO + 4 * j;
+      const bool okx = !w4a || (xs >= 0 && xs + 3 < a.W);
+      const bool ok = p < kQDMA4 && f < 10 * kQRP && q_resolve(y, a.H, zp) && okx;
+      poff[i] = ok ? ((unsigned)(y * rs) + (unsigned)xs) * 4u : oob;
     }
 #pragma unroll
     for (int i = kQWide; i < kQSlow; ++i) poff[i] = oob;
@@ -686,6 +698,21 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     if (first) post_epi = false;
   };
 
+  // reflect halo of an x-edge tile staged from 16-B pieces: wave 0 copies column x0 + 1 (LDS
+  // column kQXO + 1) into x0 - 1 (kQXO - 1), wave 1 column x0 + 62 into x0 + 64; lanes 0-39
+  // take channel l / 10, row l % 10 of the stage
+  auto fix_halo = [&](float* stg) {
+    if ((wave == 0 && fixL) || (wave == 1 && fixR)) {
+      int l = lane;
+      asm volatile("" : "+v"(l));
+      if (l < 40) {
+        const int ch = l / 10, row = l - 10 * ch;
+        float* rp = stg + ch * kQCS + row * kQPS;
+        if (wave == 0) rp[kQXO - 1] = rp[kQXO + 1];
+        else rp[kQXO + kQTW] = rp[kQXO + kQTW - 2];
+      }
+    }
+  };
   // ---- prologue: P(0), P(1), W(0), P(2), P(3) -------------------------------------------
   auto prologue = [&](auto WIDEc) {
     issue_p(WIDEc, 0, 0, ps0);
@@ -699,6 +726,11 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
   else prologue(std::false_type{});
   wait_ring(false);  // P(3) may stay in flight; conservative for P(2)
   q_lds_barrier();
+  if (fixL || fixR) {  // P(0), P(1) (P(x + 2) is fixed in step x)
+    fix_halo(ps0);
+    fix_halo(ps1);
+    q_lds_barrier();
+  }
 
   auto body = [&](auto Qc) {
     constexpr int Q = decltype(Qc)::value, QR = Q >> 1, QC = Q & 1;
@@ -778,7 +810,8 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     // P(x + 4) into psx. MFMA groups in column-major position order, so the row pass of
     // column j overwrites V[j], V[3 + j], V[6 + j] after their last use.
     // (first: the step that may follow an epilogue, the first of an iteration)
-    auto step = [&](float* wsx, float* psn, float* wsn, float* psx, int ks, bool first) {
+    auto step = [&](float* wsx, float* psn, float* wsn, float* psx, float* pfx, int ks,
+                    bool first) {
       wait_ring(first);
       if (DBG & 16) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else q_lds_barrier();  // W(x), P(x + 1) complete; every wave is done with step x - 1
@@ -814,6 +847,8 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
           if (q + 1 < 5) read_row(psn, q + 1, d);
         }
         if (q == 5 || q == 6 || q == 8) row_pass(u, q == 8 ? 2 : q - 5, V);
+        // P(x + 2) landed for every wave at this step's barrier and is read from step x + 1
+        if (q == 7) fix_halo(pfx);
       }
       ++x;
     };
@@ -948,10 +983,10 @@ __global__ __launch_bounds__(kQNTH, 1) void wino4q_mfma_kernel(ConvArgs a) {
     // values, and the compiler then renames every such MFMA's destination)
     int ks = 0, ct = ct0;
     for (int g = 0; g < G; g += 4) {
-      step(ws0, ps1, ws1, ps0, ks, true);
-      step(ws1, ps2, ws0, ps1, ks + 1, false);
-      step(ws0, ps3, ws1, ps2, ks + 2, false);
-      step(ws1, ps0, ws0, ps3, ks + 3, false);
+      step(ws0, ps1, ws1, ps0, ps2, ks, true);
+      step(ws1, ps2, ws0, ps1, ps3, ks + 1, false);
+      step(ws0, ps3, ws1, ps2, ps0, ks + 2, false);
+      step(ws1, ps0, ws0, ps3, ps1, ks + 3, false);
       ks += 4;
       if (ks == K4) {
         epilogue(ct);

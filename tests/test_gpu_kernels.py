@@ -151,6 +151,10 @@ CONV_CASES = [
     (1, 144, 19, 90, 200, 3, 1, 0, True),   # Cout 200: last co tile 8 channels; W % 4 = 2
     (2, 128, 13, 66, 96, 3, 0, 0, False),   # Cout 96, no activation, W % 4 = 2, H < 2 tiles
     (1, 512, 9, 140, 256, 3, 1, 2, True),   # upsample loader from a ragged source, 128 K steps
+    # x-edge tiles of rows of W % 4 == 0 on 16-B pieces with the reflect halo copied in
+    (1, 128, 20, 128, 64, 3, 1, 0, True),   # reflect, left and right edge tiles
+    (1, 256, 12, 64, 128, 3, 1, 0, False),  # reflect, one tile that is both edges
+    (2, 128, 10, 192, 64, 3, 0, 0, True),   # zero padding, edge tiles read zero pieces
 ]
 
 
