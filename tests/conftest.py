@@ -11,6 +11,15 @@ for p in (ROOT, PKG):
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# The GPU torch runs of the oracle (the reference's algorithm on MIOpen / rocBLAS) measure the
+# reference's fp32 noise on the platform it trains on, which the attention models' gradient
+# bars include (helpers.check_grads_rms_vs_fp64). MIOpen's default find mode benchmarks
+# candidate algorithms at the first call, so which one runs -- and the rounding it brings --
+# changed from box to box (that floor read 0.7-1.8e-4 on SAModel's decoder.1.weight over six
+# boxes). The immediate-mode heuristic (FAST) picks from the problem, the arch and the MIOpen
+# version alone. Our kernels do not use MIOpen.
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and librpst.so")

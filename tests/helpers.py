@@ -1,4 +1,6 @@
 """Shared test helpers: model construction with synthetic weights, tolerances."""
+import os
+
 import numpy as np
 import torch
 
@@ -178,6 +180,9 @@ def check_grads_rms_vs_fp64(family, i, content, style, step, oracle64, skip=(), 
         e = float(np.sqrt(v / GRAD_FLOOR_SAMPLES))
         f32 = float(np.sqrt(sq32[name] / GRAD_FLOOR_SAMPLES)) if name in sq32 else 0.0
         bar = max(grad_bar(family, i, name), 3.0 * f32)
+        if os.environ.get("RPST_GRAD_DEBUG"):
+            print(f"GRADDBG {family} {i} {name} rms {e:.3e} cpu_bar {grad_bar(family, i, name):.3e} "
+                  f"gpu32 {f32:.3e}")
         worst = max(worst, e / bar * 1e-4)
         assert e < bar, (family, i, name, "rms", e, bar)
     return worst
